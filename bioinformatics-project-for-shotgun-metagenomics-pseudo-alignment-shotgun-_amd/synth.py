@@ -1,0 +1,111 @@
+"""Synthetic FASTA/FASTQ workloads for the pseudo-alignment engine.
+
+The reference ships no data (its RUN_LOG names files that are not in the repo,
+SURVEY.md section 6), so every benchmark and most parity tests run on synthetic
+genomes and reads shaped like BASELINE.json's configs:
+
+* genomes are uniform i.i.d. ACGT, grouped into families whose members carry a
+  per-base substitution rate against the family base (shared k-mers, so reads
+  become ambiguous and unique reads get p-demoted);
+* one conserved segment is copied into every genome (so ``--max-genomes``
+  fires);
+* a small fraction of positions start an ``N`` run (exercises the N skip of
+  ``src/kmer.py:145``);
+* reads are forward-strand substrings with substitution errors and raw-ASCII
+  qualities from a clipped normal (quirk 5 of SURVEY.md section 8).
+
+Everything is numpy, seeded, and returns ASCII ``uint8`` arrays so the same
+bytes can be handed to the C-ABI (``pa_index_build`` / ``pa_reads_upload``) or
+written out as FASTA/FASTQ text for the CLI.
+"""
+
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def family_genomes(n_genomes: int, length: int, seed: int = 1, family_size: int = 5,
+                   sub_rate: float = 0.01, conserved_len: int = 5000,
+                   n_rate: float = 1e-4, n_run: int = 10) -> List[np.ndarray]:
+    """Return ``n_genomes`` ASCII genomes (``uint8`` arrays of ``length`` bases)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    conserved_len = int(min(conserved_len, length // 2))
+    conserved = ACGT[rng.integers(0, 4, size=conserved_len)] if conserved_len > 0 else None
+    out: List[np.ndarray] = []
+    base = None
+    for g in range(n_genomes):
+        if g % max(family_size, 1) == 0:
+            base = ACGT[rng.integers(0, 4, size=length)]
+        seq = base.copy()
+        if sub_rate > 0:
+            hit = np.flatnonzero(rng.random(length) < sub_rate)
+            # substitute with one of the three other bases
+            shift = rng.integers(1, 4, size=hit.size)
+            code = (np.searchsorted(ACGT, seq[hit]) + shift) % 4
+            seq[hit] = ACGT[code]
+        if conserved is not None:
+            at = int(rng.integers(0, length - conserved_len + 1))
+            seq[at:at + conserved_len] = conserved
+        if n_rate > 0 and n_run > 0:
+            starts = np.flatnonzero(rng.random(length) < n_rate)
+            for s in starts:
+                seq[s:s + n_run] = ord("N")
+        out.append(seq)
+    return out
+
+
+def sample_reads(genomes: Sequence[np.ndarray], n_reads: int, read_len: int, seed: int = 2,
+                 err_rate: float = 0.005, qual_mean: float = 60.0, qual_sd: float = 8.0,
+                 qual_min: int = 35, qual_max: int = 74) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Sample fixed-length forward-strand reads.
+
+    Returns ``(seq, qual, origin)`` where ``seq``/``qual`` are ``(n_reads, read_len)``
+    ASCII arrays and ``origin`` the source genome index of every read.  ``N`` bases
+    of the source are replaced by random bases (the FASTQ grammar only allows
+    ACGT in reads, ``src/records.py:262``).
+    """
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lens = np.array([len(g) for g in genomes], dtype=np.int64)
+    ok = np.flatnonzero(lens >= read_len)
+    if ok.size == 0:
+        raise ValueError("no genome is at least one read long")
+    origin = ok[rng.integers(0, ok.size, size=n_reads)]
+    starts = (rng.random(n_reads) * (lens[origin] - read_len + 1)).astype(np.int64)
+    seq = np.empty((n_reads, read_len), dtype=np.uint8)
+    for g in np.unique(origin):
+        rows = np.flatnonzero(origin == g)
+        idx = starts[rows, None] + np.arange(read_len)[None, :]
+        seq[rows] = genomes[g][idx]
+    nmask = seq == ord("N")
+    if nmask.any():
+        seq[nmask] = ACGT[rng.integers(0, 4, size=int(nmask.sum()))]
+    if err_rate > 0:
+        emask = rng.random(seq.shape) < err_rate
+        ne = int(emask.sum())
+        if ne:
+            code = (np.searchsorted(ACGT, seq[emask]) + rng.integers(1, 4, size=ne)) % 4
+            seq[emask] = ACGT[code]
+    q = np.clip(np.rint(rng.normal(qual_mean, qual_sd, size=seq.shape)), qual_min, qual_max)
+    qual = q.astype(np.uint8)
+    return seq, qual, origin
+
+
+def fasta_text(headers: Sequence[str], genomes: Sequence[np.ndarray], width: int = 0) -> str:
+    parts = []
+    for h, g in zip(headers, genomes):
+        s = bytes(g).decode("ascii")
+        if width and width > 0:
+            s = "\n".join(s[i:i + width] for i in range(0, len(s), width))
+        parts.append(f">{h}\n{s}\n")
+    return "".join(parts)
+
+
+def fastq_text(ids: Sequence[str], seq: np.ndarray, qual: np.ndarray) -> str:
+    parts = []
+    for i, rid in enumerate(ids):
+        parts.append(f"@{rid}\n{bytes(seq[i]).decode('ascii')}\n+\n{bytes(qual[i]).decode('ascii')}\n")
+    return "".join(parts)

@@ -1,0 +1,90 @@
+"""Pin the CPU restatement (oracle/) against the reference's own outputs.
+
+The golden vectors were produced by running the reference itself
+(tests/golden/make_golden.py); these tests run on CPU only.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pa_oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+UNIT = load("unit_cases.json")
+
+
+def _reads_arrays(reads):
+    seq, off = O.concat([r[1] for r in reads])
+    qual, _ = O.concat([r[2] for r in reads])
+    return seq, qual, off
+
+
+@pytest.mark.parametrize("case", UNIT, ids=[c["name"] for c in UNIT])
+def test_oracle_unit_cases(case):
+    genomes = [g[1] for g in case["genomes"]]
+    idents = [g[0] for g in case["genomes"]]
+    ix = O.OracleIndex(genomes, case["k"])
+    assert ix.n_kmers == case["n_kmers"]
+    exp_sets = {km: gl for km, gl in case["kmer_sets"]}
+    assert ix.export() == exp_sets
+    seq, qual, off = _reads_arrays(case["reads"])
+    for res in case["results"]:
+        ps = res["params"]
+        out = ix.align(seq, qual, off, m=ps["m"], p=ps["p"], mrq=ps["mrq"], mkq=ps["mkq"], mg=ps["mg"])
+        for r, (rid, tname, glist, qf, hr) in enumerate(res["reads"]):
+            assert O.TYPE_NAMES[int(out.types[r])] == tname, (rid, ps)
+            assert [idents[g] for g in out.genomes_of(r)] == glist, (rid, ps)
+            assert int(out.qf[r]) == qf and int(out.hr[r]) == hr, (rid, ps)
+        summ = O.summary_by_walk(out, idents, ps["mrq"], ps["mkq"], ps["mg"])
+        assert summ == res["summary"]
+        assert json.dumps(summ, indent=4) == res["summary_text"]
+
+
+def test_oracle_extract_kmers_known_answer():
+    # src/test_kmer.py:291-303: windows of AGCTAGCTAGCT with k=3
+    ix = O.OracleIndex(["AGCTAGCTAGCT"], 3)
+    assert sorted(ix.export()) == ["AGC", "CTA", "GCT", "TAG"]
+
+
+EXTSIM = load("extsim_cases.json")
+
+
+@pytest.mark.parametrize("case", EXTSIM, ids=[c["name"] for c in EXTSIM])
+def test_oracle_extsim(case):
+    idents = [g[0] for g in case["genomes"]]
+    seqs = [g[1] for g in case["genomes"]]
+    ix = O.OracleIndex(seqs, case["k"])
+    kept, info = O.extsim(idents, [len(s) for s in seqs], ix, case["threshold"])
+    assert json.dumps(info, indent=4) == case["similarity_text"]
+    assert [idents[i] for i in kept] == case["kept"]
+    ix2 = O.OracleIndex([seqs[i] for i in kept], case["k"])
+    assert ix2.n_kmers == case["n_kmers"]
+    seq, qual, off = _reads_arrays(case["reads"])
+    out = ix2.align(seq, qual, off)
+    summ = O.summary_by_walk(out, [idents[i] for i in kept])
+    assert json.dumps(summ, indent=4) == case["summary_text"]
+
+
+def test_oracle_first_key_matches_walk_order():
+    """The (read << 20 | position) first-appearance keys reproduce the walk order."""
+    case = next(c for c in UNIT if c["name"] == "rand_k11_1")
+    idents = [g[0] for g in case["genomes"]]
+    ix = O.OracleIndex([g[1] for g in case["genomes"]], case["k"])
+    seq, qual, off = _reads_arrays(case["reads"])
+    out = ix.align(seq, qual, off, m=0, p=0)
+    walk = O.summary_by_walk(out, idents)
+    keys = {}
+    for g, fk in enumerate(out.first_key):
+        if fk != np.iinfo(np.uint64).max:
+            keys[idents[g]] = min(keys.get(idents[g], fk), fk)
+    assert list(walk["Summary"].keys()) == sorted(keys, key=keys.get)
