@@ -1,0 +1,75 @@
+"""Build libpa.so (HIP, gfx950) in-tree with hipcc.
+
+    python build_native.py [--force]
+
+Objects go to ./build/, the shared library to ./libpa.so next to this file
+(both git-ignored; the .so travels to the GPU box with the repo snapshot).
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+BUILD = os.path.join(HERE, "build")
+LIB = os.path.join(HERE, "libpa.so")
+ARCH = os.environ.get("PA_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["pa_index.hip", "pa_align.hip", "pa_api.cpp"]
+HEADERS = ["pa_device.h", "pa_internal.h"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-value", "-Wno-unused-result", f"-I{INCLUDE}"]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "pa.h")]
+    jobs = []
+    objs = []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [path, __file__] + headers):
+            if src.endswith(".hip"):
+                cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, "-x", "hip", "-c", path, "-o", obj]
+            else:
+                cmd = [hipcc, *FLAGS, "-c", path, "-o", obj]
+            jobs.append(cmd)
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}")
+        return r.stdout
+
+    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), 4))) as ex:
+        list(ex.map(run, jobs))
+    if force or jobs or _stale(LIB, objs):
+        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,1110 @@
+// Per-read pseudo-alignment kernels: Read.pseudo_align + PseudoAlignment
+// counters of the reference (src/kmer.py:394-657), bit-exact.
+//
+// Two kernels implement the same per-read semantics:
+//
+//  * k_align_fast<NW, WPL> -- the hot path.  One wavefront per read (reads
+//    grid-strided over a persistent grid, 4 waves per workgroup), WPL windows
+//    per lane (W <= 64*WPL).  Per read:
+//      1. raw-ASCII quality prefix sums by a wave scan (quirk 5);
+//      2. the read is 2-bit packed in LDS by 32-lane OR reductions, non-ACGT
+//         bases recorded in a ballot bitmap; every window key is then an O(1)
+//         funnel shift out of the packed words;
+//      3. all WPL hash probes of a lane are issued together (independent 16-B
+//         HBM loads) -- this is the dominant cost;
+//      4. distinct k-mers (quirk 3) by an LDS hash keyed on the table slot, the
+//         first window of every slot kept with ds_min;
+//      5. the distinct k-mers are grouped by genome set ("class") in a second
+//         LDS hash (count + first window); singleton classes are the specific
+//         k-mers, so the m-decision (quirk 7) is a wave max/second-max;
+//      6. p-validation (quirk 8) expands the multi-genome classes of the read
+//         into an LDS genome hash (total counts + first window) -- reads whose
+//         genome union does not fit are deferred to the exact kernel;
+//      7. per-genome unique/ambiguous counts and first-appearance keys go to
+//         per-workgroup LDS counters, flushed with one atomic per genome at
+//         the end (no global atomics per read).
+//  * k_align_exact<NW> -- one workgroup per read with dense per-genome scratch
+//    in global memory; handles any read length / genome-set size.  It runs the
+//    deferred reads of the fast kernel and every read of the per-read detail
+//    API (PseudoAlignment.reads, Read.pseudo_align).
+//
+// Summary key order (quirk 9): get_summary inserts genomes in the order they
+// first appear in genomes_mapped_to lists walked read by read.  Each genome's
+// first appearance is kept as key = (global read index << 20) | position in
+// that read's list, min-reduced; the host sorts by it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "pa_device.h"
+#include "pa_internal.h"
+
+using namespace pad;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr uint32_t kLdsGenomeCap = 2048;  // per-workgroup LDS counters up to this many genomes
+
+enum : uint32_t { F_MRQ = 1, F_MKQ = 2, F_MG = 4 };
+
+struct AlignArgs {
+    const void *table;
+    uint64_t cap;
+    uint32_t G;
+    int k;
+    const uint64_t *class_off;
+    const uint32_t *class_size;
+    const uint32_t *class_genomes;
+    const uint8_t *seq;
+    const uint8_t *qual;
+    const uint64_t *off;
+    uint64_t n;
+    uint64_t base;  // global index of read 0
+    pa::DevParams prm;
+    // accumulators
+    unsigned long long *stats;   // [6]
+    unsigned long long *uniq;    // [G]
+    unsigned long long *amb;     // [G]
+    unsigned long long *first;   // [G]
+    // deferral
+    uint32_t *queue;
+    unsigned long long *qcount;
+    unsigned long long *deferred_total;
+};
+
+__device__ __forceinline__ uint64_t first_key(uint64_t read, uint32_t rank) { return (read << 20) | rank; }
+
+// ---------------------------------------------------------------------------
+// fast kernel
+// ---------------------------------------------------------------------------
+
+template <int WPL>
+struct FastCfg {
+    static constexpr int HS = 128 * WPL;        // LDS hash entries per wave (>= 2 x windows)
+    static constexpr int E = HS / 64;           // entries owned per lane
+    static constexpr int LCAP = 64 * WPL + 64;  // longest read (k <= 63)
+    static constexpr int PW = LCAP / 32 + 2;    // packed words
+    static constexpr int BW = LCAP / 64 + 2;    // poison bitmap words
+};
+
+template <int WPL>
+struct __align__(16) WaveLds {
+    using C = FastCfg<WPL>;
+    uint64_t packed[C::PW];
+    uint64_t poison[C::BW];
+    uint64_t hA_key[C::HS];   // dedup: table slot; p-check: genome id
+    uint64_t lst[C::HS];      // compaction scratch
+    uint32_t hA_v[C::HS];     // dedup: first window; p-check: total count
+    uint32_t hA_v2[C::HS];    // p-check: first window
+    uint32_t hB_key[C::HS];   // class id
+    uint32_t hB_cnt[C::HS];   // distinct k-mers of the class
+    uint32_t hB_min[C::HS];   // first window of the class
+    uint32_t pref[C::LCAP + 4];
+    uint32_t claims;
+};
+
+__device__ __forceinline__ uint32_t lds_hash_slot(uint64_t key, uint32_t mask) {
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & mask;
+}
+
+// Insert into an LDS open-addressing set of 64-bit keys; returns the entry.
+__device__ __forceinline__ uint32_t lds_insert64(uint64_t *keys, uint32_t hs, uint64_t key) {
+    uint32_t p = lds_hash_slot(key, hs - 1);
+    for (;;) {
+        uint64_t old = atomicCAS((unsigned long long *)&keys[p], (unsigned long long)EMPTY, (unsigned long long)key);
+        if (old == EMPTY || old == key) return p;
+        p = (p + 1) & (hs - 1);
+    }
+}
+
+__device__ __forceinline__ uint32_t lds_find64(const uint64_t *keys, uint32_t hs, uint64_t key) {
+    uint32_t p = lds_hash_slot(key, hs - 1);
+    while (keys[p] != key) p = (p + 1) & (hs - 1);
+    return p;
+}
+
+__device__ __forceinline__ uint32_t lds_insert32(uint32_t *keys, uint32_t hs, uint32_t key) {
+    uint32_t p = lds_hash_slot(key, hs - 1);
+    for (;;) {
+        uint32_t old = atomicCAS(&keys[p], NONE, key);
+        if (old == NONE || old == key) return p;
+        p = (p + 1) & (hs - 1);
+    }
+}
+
+// Bounded insert for the p-check genome hash; returns HS on overflow.
+__device__ __forceinline__ uint32_t lds_insert64_bounded(uint64_t *keys, uint32_t hs, uint64_t key, uint32_t *claims) {
+    uint32_t p = lds_hash_slot(key, hs - 1);
+    for (uint32_t it = 0; it < hs; it++) {
+        uint64_t old = atomicCAS((unsigned long long *)&keys[p], (unsigned long long)EMPTY, (unsigned long long)key);
+        if (old == EMPTY) {
+            atomicAdd(claims, 1u);
+            return p;
+        }
+        if (old == key) return p;
+        p = (p + 1) & (hs - 1);
+    }
+    return hs;
+}
+
+struct WgCounters {
+    uint32_t *uniq;
+    uint32_t *amb;
+    unsigned long long *first;
+    bool lds;
+};
+
+__device__ __forceinline__ void count_genome(const AlignArgs &a, const WgCounters &c, uint32_t g, bool unique,
+                                             uint32_t times, uint64_t key) {
+    if (c.lds) {
+        atomicAdd(unique ? &c.uniq[g] : &c.amb[g], times);
+        if (key < c.first[g]) atomicMin(&c.first[g], (unsigned long long)key);
+    } else {
+        atomicAdd(unique ? &a.uniq[g] : &a.amb[g], (unsigned long long)times);
+        atomicMin(&a.first[g], (unsigned long long)key);
+    }
+}
+
+template <int NW, int WPL>
+__global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
+    using C = FastCfg<WPL>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
+    const uint32_t G = a.G;
+    const int k = a.k;
+    const uint64_t mask_hs = C::HS - 1;
+    (void)mask_hs;
+
+    WgCounters wc;
+    wc.lds = G <= kLdsGenomeCap;
+    const uint32_t Gl = wc.lds ? ((G + 1) & ~1u) : 0;
+    wc.first = (unsigned long long *)smem;
+    wc.uniq = (uint32_t *)(wc.first + Gl);
+    wc.amb = wc.uniq + Gl;
+    WaveLds<WPL> *waves = (WaveLds<WPL> *)(smem + ((size_t)Gl * 16 + 15) / 16 * 16);
+    WaveLds<WPL> &L = waves[wid];
+    for (uint32_t i = threadIdx.x; i < Gl; i += kBlock) {
+        wc.first[i] = (unsigned long long)PA_NO_FIRST_KEY;
+        wc.uniq[i] = 0;
+        wc.amb[i] = 0;
+    }
+    __syncthreads();
+
+    const Slot<NW> *table = (const Slot<NW> *)a.table;
+    const bool has_mrq = a.prm.flags & F_MRQ, has_mkq = a.prm.flags & F_MKQ, has_mg = a.prm.flags & F_MG;
+    const bool need_q = has_mrq || has_mkq;
+    const int64_t mkq_k = (int64_t)a.prm.mkq * k;
+
+    uint32_t l_qf = 0, l_hr = 0;                     // per-lane window counters (committed reads only)
+    uint32_t w_unique = 0, w_amb = 0, w_unm = 0, w_drop = 0;  // lane 0 only
+
+    for (uint64_t r = (uint64_t)blockIdx.x * kWaves + wid; r < a.n; r += (uint64_t)gridDim.x * kWaves) {
+        const uint64_t off = a.off[r];
+        const uint32_t len = (uint32_t)(a.off[r + 1] - off);
+        const uint32_t W = (len >= (uint32_t)k) ? len - k + 1 : 0;
+        if (W > 64u * WPL || len > (uint32_t)(C::LCAP - 2)) {
+            if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;
+            continue;
+        }
+        // ---- raw-ASCII quality prefix sums (src/kmer.py:399, 408)
+        if (need_q) {
+            uint32_t carry = 0;
+            for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+                uint32_t i = c0 + lane;
+                uint32_t q = i < len ? (uint32_t)a.qual[off + i] : 0u;
+                uint32_t s = wave_incl_scan(q) + carry;
+                L.pref[i + 1] = s;
+                carry = __shfl(s, 63);
+            }
+            if (lane == 0) L.pref[0] = 0;
+            wave_sync();
+            if (has_mrq && (int64_t)L.pref[len] < (int64_t)a.prm.mrq * (int64_t)len) {
+                if (lane == 0) w_drop++;  // dropped, not unmapped (src/kmer.py:587-589)
+                continue;
+            }
+        }
+        // ---- 2-bit pack + non-ACGT bitmap
+        for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+            uint32_t i = c0 + lane;
+            uint32_t code = i < len ? base_code(a.seq[off + i]) : 0u;
+            uint64_t bad = __ballot(code > 3);
+            uint64_t v = (uint64_t)(code & 3) << (62 - 2 * (lane & 31));
+            v = half_or64(v);
+            if ((lane & 31) == 0) L.packed[c0 / 32 + (lane >> 5)] = v;
+            if (lane == 0) L.poison[c0 / 64] = bad;
+        }
+        if (lane < 2) {
+            uint32_t nc = (len + 63) / 64;
+            L.packed[nc * 2 + lane] = 0;
+            if (lane == 0) L.poison[nc] = 0;
+        }
+        // clear the dedup / class hashes
+#pragma unroll
+        for (int e = 0; e < C::E; e++) {
+            const int i = lane + 64 * e;
+            L.hA_key[i] = EMPTY;
+            L.hA_v[i] = NONE;
+            L.hB_key[i] = NONE;
+            L.hB_cnt[i] = 0;
+            L.hB_min[i] = NONE;
+        }
+        wave_sync();
+        // ---- windows: quality gate, key, probe (src/kmer.py:419-429)
+        Key<NW> key[WPL];
+        uint64_t hsh[WPL], pos[WPL], slot[WPL];
+        uint32_t cls[WPL], csz[WPL];
+        bool pend[WPL], inc[WPL];
+        uint32_t qf = 0, hr = 0;
+#pragma unroll
+        for (int j = 0; j < WPL; j++) {
+            const uint32_t w = lane + 64 * j;
+            bool ok = w < W;
+            if (ok && has_mkq) {
+                uint32_t s = L.pref[w + k] - L.pref[w];
+                if ((int64_t)s < mkq_k) {
+                    qf++;
+                    ok = false;
+                }
+            }
+            if (ok) ok = window_bits(L.poison, w, k) == 0;
+            pend[j] = ok;
+            inc[j] = false;
+            if (ok) {
+                key[j] = extract_key<NW>(L.packed, w, k);
+                hsh[j] = key_hash(key[j]);
+                pos[j] = home_slot(hsh[j], a.cap);
+            }
+        }
+        // batched linear probing: all pending probes of the lane in flight together
+        for (;;) {
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < WPL; j++) any |= pend[j];
+            if (!__ballot(any)) break;
+            Slot<NW> s[WPL];
+#pragma unroll
+            for (int j = 0; j < WPL; j++)
+                if (pend[j]) s[j] = table[pos[j]];
+#pragma unroll
+            for (int j = 0; j < WPL; j++) {
+                if (!pend[j]) continue;
+                if (s[j].key[0] == EMPTY) {
+                    pend[j] = false;
+                    continue;
+                }
+                bool eq = true;
+#pragma unroll
+                for (int t = 0; t < NW; t++) eq &= (s[j].key[t] == key[j].w[t]);
+                if (eq) {
+                    pend[j] = false;
+                    slot[j] = pos[j];
+                    cls[j] = s[j].cls;
+                    csz[j] = s[j].csize;
+                    if (has_mg && (int64_t)csz[j] > (int64_t)a.prm.mg)
+                        hr++;  // highly redundant k-mer (src/kmer.py:425-427)
+                    else
+                        inc[j] = true;
+                } else {
+                    pos[j] = (pos[j] + 1 == a.cap) ? 0 : pos[j] + 1;
+                }
+            }
+        }
+        bool any_inc = false;
+#pragma unroll
+        for (int j = 0; j < WPL; j++) any_inc |= inc[j];
+        if (!__ballot(any_inc)) {
+            l_qf += qf;
+            l_hr += hr;
+            if (lane == 0) w_unm++;  // no k-mer references -> UNMAPPED (src/kmer.py:516-517)
+            continue;
+        }
+        // ---- distinct k-mers: first window per table slot (quirk 3)
+        uint32_t hp[WPL];
+#pragma unroll
+        for (int j = 0; j < WPL; j++)
+            if (inc[j]) {
+                hp[j] = lds_insert64(L.hA_key, C::HS, slot[j]);
+                atomicMin(&L.hA_v[hp[j]], (uint32_t)(lane + 64 * j));
+            }
+        wave_sync();
+        // ---- group distinct k-mers by genome set
+#pragma unroll
+        for (int j = 0; j < WPL; j++)
+            if (inc[j] && L.hA_v[hp[j]] == (uint32_t)(lane + 64 * j)) {
+                uint32_t p = lds_insert32(L.hB_key, C::HS, cls[j]);
+                atomicAdd(&L.hB_cnt[p], 1u);
+                atomicMin(&L.hB_min[p], (uint32_t)(lane + 64 * j));
+            }
+        wave_sync();
+        // ---- specific counts: singleton classes (src/kmer.py:431-462)
+        uint32_t nspec_l = 0, nmulti_l = 0;
+        uint64_t top_l = 0;
+#pragma unroll
+        for (int e = 0; e < C::E; e++) {
+            const int i = lane + 64 * e;
+            uint32_t c = L.hB_key[i];
+            if (c == NONE) continue;
+            if (c < G) {
+                nspec_l++;
+                uint64_t t = ((uint64_t)L.hB_cnt[i] << 48) | ((uint64_t)(0xFFFFu - L.hB_min[i]) << 32) | c;
+                top_l = t > top_l ? t : top_l;
+            } else {
+                nmulti_l++;
+            }
+        }
+        const uint32_t nspec = wave_sum(nspec_l);
+        const uint32_t nmulti = wave_sum(nmulti_l);
+        const uint64_t read_idx = a.base + r;
+        l_qf += qf;  // from here on the read is committed by this kernel unless deferred below
+        l_hr += hr;
+        if (nspec == 0) {
+            if (lane == 0) w_amb++;  // AMBIGUOUS with an empty genome list
+            continue;
+        }
+        const uint64_t top = wave_max64(top_l);
+        const uint32_t gstar = (uint32_t)top, topcnt = (uint32_t)(top >> 48);
+        uint32_t sec_l = 0;
+#pragma unroll
+        for (int e = 0; e < C::E; e++) {
+            const int i = lane + 64 * e;
+            uint32_t c = L.hB_key[i];
+            if (c != NONE && c < G && c != gstar) sec_l = max(sec_l, L.hB_cnt[i]);
+        }
+        const uint32_t second = wave_max(sec_l);
+        const bool unique = nspec == 1 || (int64_t)topcnt >= (int64_t)second + a.prm.m;
+        if (!unique) {
+            // AMBIGUOUS: every specific genome, in first-insertion order
+            uint32_t mine = 0;
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                uint32_t c = L.hB_key[lane + 64 * e];
+                mine += (c != NONE && c < G);
+            }
+            uint32_t at = wave_excl_scan(mine);
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                const int i = lane + 64 * e;
+                uint32_t c = L.hB_key[i];
+                if (c != NONE && c < G) L.lst[at++] = ((uint64_t)L.hB_min[i] << 32) | c;
+            }
+            wave_sync();
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                const int i = lane + 64 * e;
+                uint32_t c = L.hB_key[i];
+                if (c == NONE || c >= G) continue;
+                uint64_t me = ((uint64_t)L.hB_min[i] << 32) | c;
+                uint32_t rank = 0;
+                for (uint32_t t = 0; t < nspec; t++) rank += L.lst[t] < me;
+                count_genome(a, wc, c, false, 1, first_key(read_idx, rank));
+            }
+            if (lane == 0) w_amb++;
+            continue;
+        }
+        if (a.prm.p < 0 || nmulti == 0) {
+            // UNIQUE; with only specific k-mers the p-check cannot demote
+            if (lane == 0) {
+                count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
+                w_unique++;
+            }
+            continue;
+        }
+        // ---- p-validation (src/kmer.py:464-480): total counts over all genomes
+        wave_sync();
+#pragma unroll
+        for (int e = 0; e < C::E; e++) {
+            const int i = lane + 64 * e;
+            L.hA_key[i] = EMPTY;
+            L.hA_v[i] = 0;
+            L.hA_v2[i] = NONE;
+        }
+        if (lane == 0) L.claims = 0;
+        // compact the multi classes into lst: (class << 32 | cnt << 16 | first window)
+        {
+            uint32_t mine = 0;
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                uint32_t c = L.hB_key[lane + 64 * e];
+                mine += (c != NONE && c >= G);
+            }
+            uint32_t at = wave_excl_scan(mine);
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                const int i = lane + 64 * e;
+                uint32_t c = L.hB_key[i];
+                if (c != NONE && c >= G)
+                    L.lst[at++] = ((uint64_t)c << 32) | ((uint64_t)L.hB_cnt[i] << 16) | L.hB_min[i];
+            }
+        }
+        wave_sync();
+        bool ovf = false;
+        const uint32_t limit = (C::HS * 3) / 4;
+#pragma unroll
+        for (int e = 0; e < C::E; e++) {
+            const int i = lane + 64 * e;
+            uint32_t c = L.hB_key[i];
+            if (c != NONE && c < G) {
+                uint32_t p = lds_insert64_bounded(L.hA_key, C::HS, c, &L.claims);
+                if (p >= (uint32_t)C::HS) {
+                    ovf = true;
+                } else {
+                    atomicAdd(&L.hA_v[p], L.hB_cnt[i]);
+                    atomicMin(&L.hA_v2[p], L.hB_min[i]);
+                }
+            }
+        }
+        for (uint32_t t = 0; t < nmulti; t++) {
+            const uint64_t ent = L.lst[t];
+            const uint32_t c = (uint32_t)(ent >> 32) - G;
+            const uint32_t cnt = (uint32_t)(ent >> 16) & 0xFFFFu, mw = (uint32_t)ent & 0xFFFFu;
+            const uint32_t sz = a.class_size[c];
+            if (sz > limit) {
+                ovf = true;
+                break;
+            }
+            const uint32_t *gl = a.class_genomes + a.class_off[c];
+            for (uint32_t j = lane; j < sz; j += 64) {
+                uint32_t g = gl[j];
+                uint32_t p = lds_insert64_bounded(L.hA_key, C::HS, g, &L.claims);
+                if (p >= (uint32_t)C::HS) {
+                    ovf = true;
+                } else {
+                    atomicAdd(&L.hA_v[p], cnt);
+                    atomicMin(&L.hA_v2[p], mw);
+                }
+            }
+            wave_sync();
+            if (L.claims > limit) break;
+        }
+        wave_sync();
+        if (__ballot(ovf) || L.claims > limit) {
+            // genome union too large for the wave's LDS: exact kernel takes over
+            l_qf -= qf;
+            l_hr -= hr;
+            if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;
+            continue;
+        }
+        uint32_t ts_l = 0, mx_l = 0;
+#pragma unroll
+        for (int e = 0; e < C::E; e++) {
+            const int i = lane + 64 * e;
+            uint64_t g = L.hA_key[i];
+            if (g == EMPTY) continue;
+            mx_l = max(mx_l, L.hA_v[i]);
+            if (g == gstar) ts_l = L.hA_v[i];
+        }
+        const uint32_t tstar = wave_max(ts_l), maxtot = wave_max(mx_l);
+        if ((int64_t)maxtot - (int64_t)tstar > a.prm.p) {
+            // demoted: [G*] + every genome with total >= total[G*], first-appearance order
+            uint32_t mine = 0;
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                const int i = lane + 64 * e;
+                mine += (L.hA_key[i] != EMPTY && L.hA_v[i] >= tstar);
+            }
+            uint32_t at = wave_excl_scan(mine);
+            const uint32_t nq = wave_sum(mine);
+            wave_sync();
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                const int i = lane + 64 * e;
+                if (L.hA_key[i] != EMPTY && L.hA_v[i] >= tstar)
+                    L.lst[at++] = ((uint64_t)L.hA_v2[i] << 32) | (uint32_t)L.hA_key[i];
+            }
+            wave_sync();
+#pragma unroll
+            for (int e = 0; e < C::E; e++) {
+                const int i = lane + 64 * e;
+                if (L.hA_key[i] == EMPTY || L.hA_v[i] < tstar) continue;
+                const uint32_t g = (uint32_t)L.hA_key[i];
+                if (g == gstar) {
+                    count_genome(a, wc, g, false, 2, first_key(read_idx, 0));
+                } else {
+                    uint64_t me = ((uint64_t)L.hA_v2[i] << 32) | g;
+                    uint32_t rank = 1;
+                    for (uint32_t t = 0; t < nq; t++) rank += L.lst[t] < me;
+                    count_genome(a, wc, g, false, 1, first_key(read_idx, rank));
+                }
+            }
+            if (lane == 0) w_amb++;
+        } else {
+            if (lane == 0) {
+                count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
+                w_unique++;
+            }
+        }
+    }
+    // ---- flush
+    const uint32_t qf_w = wave_sum(l_qf), hr_w = wave_sum(l_hr);
+    if (lane == 0) {
+        if (w_unique) atomicAdd(&a.stats[0], (unsigned long long)w_unique);
+        if (w_amb) atomicAdd(&a.stats[1], (unsigned long long)w_amb);
+        if (w_unm) atomicAdd(&a.stats[2], (unsigned long long)w_unm);
+        if (w_drop) atomicAdd(&a.stats[3], (unsigned long long)w_drop);
+        if (qf_w && has_mkq) atomicAdd(&a.stats[4], (unsigned long long)qf_w);
+        if (hr_w && has_mg) atomicAdd(&a.stats[5], (unsigned long long)hr_w);
+    }
+    if (wc.lds) {
+        __syncthreads();
+        for (uint32_t g = threadIdx.x; g < G; g += kBlock) {
+            if (wc.uniq[g]) atomicAdd(&a.uniq[g], (unsigned long long)wc.uniq[g]);
+            if (wc.amb[g]) atomicAdd(&a.amb[g], (unsigned long long)wc.amb[g]);
+            if (wc.first[g] != (unsigned long long)PA_NO_FIRST_KEY) atomicMin(&a.first[g], wc.first[g]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// exact kernel (one workgroup per read, dense per-genome scratch)
+// ---------------------------------------------------------------------------
+
+struct ExactArgs {
+    AlignArgs a;
+    int detail;           // 0: counters; 1: per-read type/qf/hr/list length; 2: also write lists
+    uint8_t *type_out;
+    uint32_t *qf_out, *hr_out, *len_out;
+    const uint64_t *list_off;
+    uint32_t *lists;
+    unsigned char *ws;    // per-workgroup scratch
+    uint64_t ws_stride;
+    uint32_t wcap;        // windows capacity
+    uint32_t dh;          // dedup hash size (power of two >= 2*wcap)
+    int use_queue;
+};
+
+struct ExactWs {
+    uint64_t *wslot;
+    uint32_t *wcls;
+    uint64_t *dh_key;
+    uint32_t *dh_min;
+    uint32_t *g_spec, *g_specmin, *g_tot, *g_totmin, *touched;
+};
+
+__host__ __device__ inline uint64_t exact_ws_stride(uint32_t wcap, uint32_t dh, uint32_t G) {
+    uint64_t b = (uint64_t)wcap * 8 + (uint64_t)dh * 8 + (uint64_t)wcap * 4 + (uint64_t)dh * 4 + (uint64_t)G * 20;
+    return (b + 255) / 256 * 256;
+}
+
+__device__ inline ExactWs exact_ws(unsigned char *base, uint32_t wcap, uint32_t dh, uint32_t G) {
+    ExactWs w;
+    w.wslot = (uint64_t *)base;
+    w.dh_key = w.wslot + wcap;
+    w.wcls = (uint32_t *)(w.dh_key + dh);
+    w.dh_min = w.wcls + wcap;
+    w.g_spec = w.dh_min + dh;
+    w.g_specmin = w.g_spec + G;
+    w.g_tot = w.g_specmin + G;
+    w.g_totmin = w.g_tot + G;
+    w.touched = w.g_totmin + G;
+    return w;
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *red) {
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t s = 0;
+    for (int i = 0; i < kWaves; i++) s += red[i];
+    __syncthreads();
+    return s;
+}
+
+__device__ __forceinline__ uint64_t block_sum64(uint64_t v, unsigned long long *red) {
+    v = wave_sum64(v);
+    __syncthreads();
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t s = 0;
+    for (int i = 0; i < kWaves; i++) s += red[i];
+    __syncthreads();
+    return s;
+}
+
+__device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t *red) {
+    v = wave_max(v);
+    __syncthreads();
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t s = 0;
+    for (int i = 0; i < kWaves; i++) s = max(s, red[i]);
+    __syncthreads();
+    return s;
+}
+
+template <int NW>
+__global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
+    const AlignArgs &a = x.a;
+    __shared__ uint32_t red[kWaves];
+    __shared__ unsigned long long red64[kWaves];
+    __shared__ uint32_t n_touched;
+    const uint32_t G = a.G;
+    const int k = a.k;
+    const uint64_t mask0 = k > 0 ? mask0_of(k, NW) : 0;
+    const Slot<NW> *table = (const Slot<NW> *)a.table;
+    const bool has_mrq = a.prm.flags & F_MRQ, has_mkq = a.prm.flags & F_MKQ, has_mg = a.prm.flags & F_MG;
+    ExactWs ws = exact_ws(x.ws + (uint64_t)blockIdx.x * x.ws_stride, x.wcap, x.dh, G);
+    // scratch invariant: g_* clean (0 / NONE) between reads
+    for (uint32_t g = threadIdx.x; g < G; g += kBlock) {
+        st_agent(&ws.g_spec[g], 0u);
+        st_agent(&ws.g_specmin[g], NONE);
+        st_agent(&ws.g_tot[g], 0u);
+        st_agent(&ws.g_totmin[g], NONE);
+    }
+    if (threadIdx.x == 0) n_touched = 0;
+    __syncthreads();
+    const uint64_t nq = x.use_queue ? *a.qcount : a.n;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && x.use_queue && a.deferred_total) atomicAdd(a.deferred_total, nq);
+    for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const uint64_t r = x.use_queue ? a.queue[q] : q;
+        const uint64_t off = a.off[r];
+        const uint32_t len = (uint32_t)(a.off[r + 1] - off);
+        const uint32_t W = (k > 0 && len >= (uint32_t)k) ? len - k + 1 : 0;
+        const uint64_t read_idx = a.base + r;
+        // ---- mean read quality
+        if (has_mrq) {
+            uint64_t s = 0;
+            for (uint32_t i = threadIdx.x; i < len; i += kBlock) s += a.qual[off + i];
+            s = block_sum64(s, red64);
+            if ((int64_t)s < (int64_t)a.prm.mrq * (int64_t)len) {
+                if (threadIdx.x == 0) {
+                    if (x.detail) {
+                        x.type_out[r] = PA_DROPPED;
+                        x.qf_out[r] = 0;
+                        x.hr_out[r] = 0;
+                        x.len_out[r] = 0;
+                    } else {
+                        atomicAdd(&a.stats[3], 1ull);
+                    }
+                }
+                continue;
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < x.dh; i += kBlock) {
+            st_agent(&ws.dh_key[i], EMPTY);
+            st_agent(&ws.dh_min[i], NONE);
+        }
+        __syncthreads();
+        // ---- windows
+        uint32_t qf = 0, hr = 0, any = 0;
+        for (uint32_t w = threadIdx.x; w < W; w += kBlock) {
+            ws.wslot[w] = EMPTY;
+            if (has_mkq) {
+                uint32_t s = 0;
+                for (int i = 0; i < k; i++) s += a.qual[off + w + i];
+                if ((int64_t)s < (int64_t)a.prm.mkq * k) {
+                    qf++;
+                    continue;
+                }
+            }
+            Key<NW> key;
+#pragma unroll
+            for (int j = 0; j < NW; j++) key.w[j] = 0;
+            bool clean = true;
+            for (int i = 0; i < k; i++) {
+                uint32_t c = base_code(a.seq[off + w + i]);
+                clean &= c < 4;
+                key_push(key, c & 3, mask0);
+            }
+            if (!clean) continue;
+            uint64_t slot;
+            uint32_t cls, csize;
+            if (!table_find<NW>(table, a.cap, key, key_hash(key), slot, cls, csize)) continue;
+            if (has_mg && (int64_t)csize > (int64_t)a.prm.mg) {
+                hr++;
+                continue;
+            }
+            ws.wslot[w] = slot;
+            ws.wcls[w] = cls;
+            any = 1;
+            uint32_t p = (uint32_t)(fmix64(slot) & (x.dh - 1));
+            for (;;) {
+                uint64_t old = atomicCAS((unsigned long long *)&ws.dh_key[p], (unsigned long long)EMPTY,
+                                         (unsigned long long)slot);
+                if (old == EMPTY || old == slot) break;
+                p = (p + 1) & (x.dh - 1);
+            }
+            atomicMin(&ws.dh_min[p], w);
+        }
+        qf = block_sum(qf, red);
+        hr = block_sum(hr, red);
+        any = block_sum(any, red);
+        uint8_t type = PA_UNMAPPED;
+        uint32_t list_len = 0;
+        if (any) {
+            // ---- distinct k-mers -> specific and total counts per genome
+            for (uint32_t w = threadIdx.x; w < W; w += kBlock) {
+                const uint64_t slot = ws.wslot[w];
+                if (slot == EMPTY) continue;
+                uint32_t p = (uint32_t)(fmix64(slot) & (x.dh - 1));
+                while (ld_agent(&ws.dh_key[p]) != slot) p = (p + 1) & (x.dh - 1);
+                if (ld_agent(&ws.dh_min[p]) != w) continue;
+                const uint32_t c = ws.wcls[w];
+                const uint32_t *gl;
+                uint32_t sz, single = c;
+                if (c < G) {
+                    atomicAdd(&ws.g_spec[c], 1u);
+                    atomicMin(&ws.g_specmin[c], w);
+                    gl = &single;
+                    sz = 1;
+                } else {
+                    gl = a.class_genomes + a.class_off[c - G];
+                    sz = a.class_size[c - G];
+                }
+                for (uint32_t j = 0; j < sz; j++) {
+                    const uint32_t g = gl[j];
+                    if (atomicAdd(&ws.g_tot[g], 1u) == 0) ws.touched[atomicAdd(&n_touched, 1u)] = g;
+                    atomicMin(&ws.g_totmin[g], w);
+                }
+            }
+            __syncthreads();
+            const uint32_t nt = n_touched;
+            // ---- decision (src/kmer.py:444-480)
+            uint32_t nspec = 0, maxcnt = 0;
+            for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                uint32_t c = ld_agent(&ws.g_spec[ws.touched[t]]);
+                nspec += c > 0;
+                maxcnt = max(maxcnt, c);
+            }
+            nspec = block_sum(nspec, red);
+            maxcnt = block_max(maxcnt, red);
+            type = PA_AMBIGUOUSLY_MAPPED;
+            uint32_t gstar = NONE;
+            bool unique = false, demote = false;
+            uint32_t tstar = 0;
+            if (nspec > 0) {
+                // top = first-inserted genome among those with the max count
+                uint32_t best = 0;  // encodes (NONE - first window) to take a max
+                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                    uint32_t g = ws.touched[t];
+                    if (ld_agent(&ws.g_spec[g]) == maxcnt) best = max(best, NONE - ld_agent(&ws.g_specmin[g]));
+                }
+                best = block_max(best, red);
+                uint32_t sec = 0, gs = 0;
+                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                    uint32_t g = ws.touched[t];
+                    uint32_t c = ld_agent(&ws.g_spec[g]);
+                    if (c == maxcnt && NONE - ld_agent(&ws.g_specmin[g]) == best)
+                        gs = g + 1;
+                    else
+                        sec = max(sec, c);
+                }
+                gstar = block_max(gs, red) - 1;
+                sec = block_max(sec, red);
+                unique = nspec == 1 || (int64_t)maxcnt >= (int64_t)sec + a.prm.m;
+                if (unique && a.prm.p >= 0) {
+                    tstar = ld_agent(&ws.g_tot[gstar]);
+                    uint32_t mx = 0;
+                    for (uint32_t t = threadIdx.x; t < nt; t += kBlock)
+                        mx = max(mx, ld_agent(&ws.g_tot[ws.touched[t]]));
+                    mx = block_max(mx, red);
+                    demote = (int64_t)mx - (int64_t)tstar > a.prm.p;
+                }
+            }
+            // ---- emit genomes_mapped_to with list positions
+            if (unique && !demote) {
+                type = PA_UNIQUELY_MAPPED;
+                list_len = 1;
+                if (threadIdx.x == 0) {
+                    if (x.detail == 2) x.lists[x.list_off[r]] = gstar;
+                    if (!x.detail) {
+                        atomicAdd(&a.uniq[gstar], 1ull);
+                        atomicMin(&a.first[gstar], (unsigned long long)first_key(read_idx, 0));
+                    }
+                }
+            } else if (unique && demote) {
+                uint32_t nq = 0;
+                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) nq += ld_agent(&ws.g_tot[ws.touched[t]]) >= tstar;
+                nq = block_sum(nq, red);
+                list_len = 1 + nq;
+                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                    const uint32_t g = ws.touched[t];
+                    const uint32_t tg = ld_agent(&ws.g_tot[g]);
+                    if (tg < tstar) continue;
+                    const uint64_t me = ((uint64_t)ld_agent(&ws.g_totmin[g]) << 32) | g;
+                    uint32_t rank = 1;
+                    for (uint32_t u = 0; u < nt; u++) {
+                        const uint32_t h = ws.touched[u];
+                        if (ld_agent(&ws.g_tot[h]) >= tstar &&
+                            (((uint64_t)ld_agent(&ws.g_totmin[h]) << 32) | h) < me)
+                            rank++;
+                    }
+                    if (x.detail == 2) x.lists[x.list_off[r] + rank] = g;
+                    if (!x.detail) {
+                        atomicAdd(&a.amb[g], g == gstar ? 2ull : 1ull);
+                        atomicMin(&a.first[g], (unsigned long long)first_key(read_idx, g == gstar ? 0 : rank));
+                    }
+                }
+                if (threadIdx.x == 0 && x.detail == 2) x.lists[x.list_off[r]] = gstar;
+            } else if (nspec > 0) {
+                list_len = nspec;
+                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                    const uint32_t g = ws.touched[t];
+                    if (ld_agent(&ws.g_spec[g]) == 0) continue;
+                    const uint32_t mw = ld_agent(&ws.g_specmin[g]);
+                    uint32_t rank = 0;
+                    for (uint32_t u = 0; u < nt; u++) {
+                        const uint32_t h = ws.touched[u];
+                        if (ld_agent(&ws.g_spec[h]) > 0 && ld_agent(&ws.g_specmin[h]) < mw) rank++;
+                    }
+                    if (x.detail == 2) x.lists[x.list_off[r] + rank] = g;
+                    if (!x.detail) {
+                        atomicAdd(&a.amb[g], 1ull);
+                        atomicMin(&a.first[g], (unsigned long long)first_key(read_idx, rank));
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- restore the scratch invariant
+            for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                const uint32_t g = ws.touched[t];
+                st_agent(&ws.g_spec[g], 0u);
+                st_agent(&ws.g_specmin[g], NONE);
+                st_agent(&ws.g_tot[g], 0u);
+                st_agent(&ws.g_totmin[g], NONE);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) n_touched = 0;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            if (x.detail) {
+                x.type_out[r] = type;
+                x.qf_out[r] = qf;
+                x.hr_out[r] = hr;
+                x.len_out[r] = list_len;
+            } else {
+                atomicAdd(&a.stats[type == PA_UNMAPPED ? 2 : (type == PA_UNIQUELY_MAPPED ? 0 : 1)], 1ull);
+                if (has_mkq && qf) atomicAdd(&a.stats[4], (unsigned long long)qf);
+                if (has_mg && hr) atomicAdd(&a.stats[5], (unsigned long long)hr);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+
+template <int WPL>
+constexpr size_t wave_lds_bytes() {
+    return sizeof(WaveLds<WPL>);
+}
+
+size_t fast_lds_bytes(uint32_t G, int wpl) {
+    size_t cnt = G <= kLdsGenomeCap ? (((size_t)((G + 1) & ~1u) * 16 + 15) / 16 * 16) : 0;
+    size_t wl = wpl == 1 ? wave_lds_bytes<1>() : wpl == 2 ? wave_lds_bytes<2>() : wave_lds_bytes<4>();
+    return cnt + kWaves * wl;
+}
+
+template <int NW, int WPL>
+pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
+    auto kern = k_align_fast<NW, WPL>;
+    if (shm > 64 * 1024) PA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    int per_cu = 0;
+    PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, shm));
+    int dev = 0, cus = 256;
+    PA_HIP(hipGetDevice(&dev));
+    PA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    uint64_t want = (a.n + kWaves - 1) / kWaves;
+    uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)cus;
+    unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), shm, st, a);
+    PA_HIP(hipGetLastError());
+    return PA_OK;
+}
+
+template <int NW>
+pa_status launch_fast_wpl(const AlignArgs &a, int wpl, hipStream_t st) {
+    size_t shm = fast_lds_bytes(a.G, wpl);
+    switch (wpl) {
+        case 1: return launch_fast<NW, 1>(a, shm, st);
+        case 2: return launch_fast<NW, 2>(a, shm, st);
+        default: return launch_fast<NW, 4>(a, shm, st);
+    }
+}
+
+template <int NW>
+void launch_exact(const ExactArgs &x, unsigned grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_align_exact<NW>, dim3(grid), dim3(kBlock), 0, st, x);
+}
+
+void launch_exact_nw(int nw, const ExactArgs &x, unsigned grid, hipStream_t st) {
+    switch (nw) {
+        case 1: launch_exact<1>(x, grid, st); break;
+        case 2: launch_exact<2>(x, grid, st); break;
+        case 3: launch_exact<3>(x, grid, st); break;
+        case 4: launch_exact<4>(x, grid, st); break;
+        default: launch_exact<5>(x, grid, st); break;
+    }
+}
+
+constexpr unsigned kExactGrid = 512;
+
+AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams &p, uint64_t base) {
+    AlignArgs a{};
+    a.table = idx->table;
+    a.cap = idx->cap;
+    a.G = idx->n_genomes;
+    a.k = (int)std::max<int64_t>(idx->k, 0);
+    a.class_off = idx->class_off;
+    a.class_size = idx->class_size;
+    a.class_genomes = idx->class_genomes;
+    a.seq = r->seq;
+    a.qual = r->qual;
+    a.off = r->off;
+    a.n = r->n;
+    a.base = base;
+    a.prm = p;
+    return a;
+}
+
+pa_status prepare_exact(pa_index *idx, const pa_reads *r, ExactArgs &x, unsigned &grid) {
+    const uint32_t wcap = std::max<uint32_t>(1, r->max_len);
+    uint32_t dh = 64;
+    while (dh < 2 * wcap) dh <<= 1;
+    const uint64_t stride = exact_ws_stride(wcap, dh, idx->n_genomes);
+    grid = kExactGrid;
+    while (grid > 16 && (uint64_t)grid * stride > (1ull << 31)) grid >>= 1;
+    PA_TRY(pa::ensure_workspace(idx, (size_t)grid * stride));
+    x.ws = (unsigned char *)idx->ws.ptr;
+    x.ws_stride = stride;
+    x.wcap = wcap;
+    x.dh = dh;
+    return PA_OK;
+}
+
+}  // namespace
+
+namespace pa {
+
+pa_status ensure_workspace(pa_index *idx, size_t bytes) {
+    if (idx->ws.bytes >= bytes) return PA_OK;
+    hipFree(idx->ws.ptr);
+    idx->ws.ptr = nullptr;
+    idx->ws.bytes = 0;
+    hipError_t e = hipMalloc(&idx->ws.ptr, bytes);
+    if (e != hipSuccess) {
+        set_error(std::string("workspace allocation failed: ") + hipGetErrorString(e));
+        return PA_ENOMEM;
+    }
+    idx->ws.bytes = bytes;
+    return PA_OK;
+}
+
+pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t base, pa_result *acc,
+                hipStream_t st) {
+    if (r->n == 0) return PA_OK;
+    if (idx->queue_cap < r->n) {
+        hipFree(idx->queue);
+        idx->queue = nullptr;
+        idx->queue_cap = 0;
+        PA_HIP(hipMalloc(&idx->queue, r->n * 4));
+        idx->queue_cap = r->n;
+    }
+    AlignArgs a = make_args(idx, r, p, base);
+    const uint32_t G = idx->n_genomes;
+    a.stats = (unsigned long long *)acc->sum_block;
+    a.uniq = (unsigned long long *)acc->sum_block + 6;
+    a.amb = a.uniq + G;
+    a.first = (unsigned long long *)acc->min_block;
+    a.queue = idx->queue;
+    a.qcount = (unsigned long long *)idx->counters;
+    a.deferred_total = (unsigned long long *)idx->counters + 1;
+    PA_HIP(hipMemsetAsync(idx->counters, 0, 8, st));
+    ExactArgs x{};
+    unsigned egrid = 0;
+    PA_TRY(prepare_exact(idx, r, x, egrid));
+    x.a = a;
+    x.detail = 0;
+    const bool fast_ok = idx->k > 0 && idx->nw <= 2 && idx->n_kmers > 0;
+    if (fast_ok) {
+        const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
+        const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4
+        if (idx->profile) {
+            hipEvent_t e0, e1;
+            PA_HIP(hipEventCreate(&e0));
+            PA_HIP(hipEventCreate(&e1));
+            PA_HIP(hipEventRecord(e0, st));
+            idx->ev_start.push_back(e0);
+            PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
+            PA_HIP(hipEventRecord(e1, st));
+            idx->ev_stop.push_back(e1);
+        } else {
+            PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
+        }
+        x.use_queue = 1;
+    } else {
+        x.use_queue = 0;
+    }
+    launch_exact_nw(idx->nw, x, egrid, st);
+    PA_HIP(hipGetLastError());
+    return PA_OK;
+}
+
+pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uint8_t *type, uint32_t *qf,
+                       uint32_t *hr, uint64_t *list_off, uint32_t *lists, uint64_t list_cap, uint64_t *list_total,
+                       hipStream_t st) {
+    const uint64_t n = r->n;
+    if (list_off) list_off[0] = 0;
+    if (list_total) *list_total = 0;
+    if (n == 0) return PA_OK;
+    ExactArgs x{};
+    unsigned egrid = 0;
+    PA_TRY(prepare_exact(idx, r, x, egrid));
+    x.a = make_args(idx, r, p, 0);
+    x.use_queue = 0;
+    uint8_t *d_type = nullptr;
+    uint32_t *d_qf = nullptr, *d_hr = nullptr, *d_len = nullptr, *d_lists = nullptr;
+    uint64_t *d_off = nullptr;
+    PA_HIP(hipMalloc(&d_type, n));
+    PA_HIP(hipMalloc(&d_qf, n * 4));
+    PA_HIP(hipMalloc(&d_hr, n * 4));
+    PA_HIP(hipMalloc(&d_len, n * 4));
+    x.type_out = d_type;
+    x.qf_out = d_qf;
+    x.hr_out = d_hr;
+    x.len_out = d_len;
+    x.detail = 1;
+    launch_exact_nw(idx->nw, x, egrid, st);
+    PA_HIP(hipGetLastError());
+    std::vector<uint32_t> lens(n);
+    PA_HIP(hipMemcpyAsync(lens.data(), d_len, n * 4, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipMemcpyAsync(type, d_type, n, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipMemcpyAsync(qf, d_qf, n * 4, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipMemcpyAsync(hr, d_hr, n * 4, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipStreamSynchronize(st));
+    std::vector<uint64_t> offs(n + 1, 0);
+    for (uint64_t i = 0; i < n; i++) offs[i + 1] = offs[i] + lens[i];
+    const uint64_t total = offs[n];
+    if (list_total) *list_total = total;
+    if (list_off) std::memcpy(list_off, offs.data(), (n + 1) * 8);
+    pa_status rc = PA_OK;
+    if (lists && total > 0) {
+        if (list_cap < total) {
+            set_error("pa_align_detail: list_cap smaller than the required list length");
+            rc = PA_EINVAL;
+        } else {
+            PA_HIP(hipMalloc(&d_off, (n + 1) * 8));
+            PA_HIP(hipMalloc(&d_lists, total * 4));
+            PA_HIP(hipMemcpyAsync(d_off, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+            x.detail = 2;
+            x.list_off = d_off;
+            x.lists = d_lists;
+            launch_exact_nw(idx->nw, x, egrid, st);
+            PA_HIP(hipGetLastError());
+            PA_HIP(hipMemcpyAsync(lists, d_lists, total * 4, hipMemcpyDeviceToHost, st));
+            PA_HIP(hipStreamSynchronize(st));
+        }
+    }
+    hipFree(d_type); hipFree(d_qf); hipFree(d_hr); hipFree(d_len); hipFree(d_off); hipFree(d_lists);
+    return rc;
+}
+
+}  // namespace pa

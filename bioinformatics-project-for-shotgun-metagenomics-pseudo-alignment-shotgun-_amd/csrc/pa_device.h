@@ -1,0 +1,198 @@
+// Device-side building blocks shared by the index-build and align kernels.
+//
+// K-mer keys.  A k-mer is packed 2 bits per base (A=0 C=1 G=2 T=3), first base
+// in the most significant bits, into NW = k/32 + 1 64-bit words.  The top word
+// holds 2k - 64*(NW-1) < 64 bits, so an all-ones top word is never a key and
+// serves as the empty-slot sentinel of the hash table.  This is the HBM form of
+// the reference's `Dict[str, ...]` keys (src/kmer.py:130); bases other than
+// ACGT poison every window that contains them (the reference skips k-mers with
+// 'N' at src/kmer.py:145, and reads can only hold ACGT, src/records.py:262).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pad {
+
+constexpr uint64_t EMPTY = ~0ull;        // empty slot (top key word)
+constexpr uint64_t BUSY = ~0ull - 1;     // slot being written (multi-word inserts)
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+template <int NW>
+struct Key {
+    uint64_t w[NW];
+};
+
+// Hash-table slot: packed key + class id + class size (number of genomes).
+template <int NW>
+struct Slot {
+    uint64_t key[NW];
+    uint32_t cls;
+    uint32_t csize;
+};
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+template <int NW>
+__device__ __forceinline__ uint64_t key_hash(const Key<NW> &k) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+    for (int j = 0; j < NW; j++) h = fmix64(h ^ k.w[j]);
+    return h;
+}
+
+// Home slot by multiply-high range reduction (table size need not be 2^n).
+__device__ __forceinline__ uint64_t home_slot(uint64_t h, uint64_t cap) { return __umul64hi(h, cap); }
+
+__device__ __forceinline__ uint32_t base_code(uint32_t ch) {
+    return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : ch == 'T' ? 3u : 4u;
+}
+
+// Append one base (2-bit code) to a rolling key, keeping 2k bits.
+template <int NW>
+__device__ __forceinline__ void key_push(Key<NW> &k, uint32_t c, uint64_t mask0) {
+#pragma unroll
+    for (int j = 0; j < NW - 1; j++) k.w[j] = (k.w[j] << 2) | (k.w[j + 1] >> 62);
+    k.w[NW - 1] = (k.w[NW - 1] << 2) | (uint64_t)c;
+    k.w[0] &= mask0;
+}
+
+__device__ __forceinline__ uint64_t mask0_of(int k, int nw) {
+    int bits = 2 * k - 64 * (nw - 1);
+    return bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+}
+
+// 64 bits of a MSB-first 2-bit packed base array starting at bit `o`.
+__device__ __forceinline__ uint64_t get64(const uint64_t *p, uint32_t o) {
+    uint32_t q = o >> 6, r = o & 63;
+    uint64_t hi = p[q] << r;
+    return r ? (hi | (p[q + 1] >> (64 - r))) : hi;
+}
+
+// Key of the window starting at base w of a packed read.
+template <int NW>
+__device__ __forceinline__ Key<NW> extract_key(const uint64_t *packed, uint32_t w, int k) {
+    Key<NW> key;
+    const int w0bits = 2 * k - 64 * (NW - 1);
+    // k a multiple of 32 leaves the top word empty (a 64-bit shift would be undefined)
+    key.w[0] = w0bits ? (get64(packed, 2 * w) >> (64 - w0bits)) : 0;
+#pragma unroll
+    for (int j = 1; j < NW; j++) key.w[j] = get64(packed, 2 * w + w0bits + 64 * (j - 1));
+    return key;
+}
+
+// Bits [w, w+k) of a LSB-first position bitmap (k < 64).
+__device__ __forceinline__ uint64_t window_bits(const uint64_t *bm, uint32_t w, int k) {
+    uint32_t q = w >> 6, r = w & 63;
+    uint64_t v = bm[q] >> r;
+    if (r) v |= bm[q + 1] << (64 - r);
+    return v & ((1ull << k) - 1);
+}
+
+// Read-only probe (tables are immutable once built).
+template <int NW>
+__device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint64_t cap, const Key<NW> &k, uint64_t h,
+                                           uint64_t &slot, uint32_t &cls, uint32_t &csize) {
+    uint64_t pos = home_slot(h, cap);
+    for (;;) {
+        const Slot<NW> s = t[pos];
+        if (s.key[0] == EMPTY) return false;
+        bool eq = true;
+#pragma unroll
+        for (int j = 0; j < NW; j++) eq &= (s.key[j] == k.w[j]);
+        if (eq) {
+            slot = pos;
+            cls = s.cls;
+            csize = s.csize;
+            return true;
+        }
+        pos = (pos + 1 == cap) ? 0 : pos + 1;
+    }
+}
+
+// ---- wavefront (64-lane) helpers ------------------------------------------
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    uint32_t lo = __shfl_xor((unsigned)(uint32_t)v, m);
+    uint32_t hi = __shfl_xor((unsigned)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor(v, m));
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t o = shfl_xor64(v, m);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor64(v, m);
+    return v;
+}
+
+// OR across each 32-lane half of the wave.
+__device__ __forceinline__ uint64_t half_or64(uint64_t v) {
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) v |= shfl_xor64(v, m);
+    return v;
+}
+
+// Inclusive prefix sum across the 64 lanes.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(v, d);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) { return wave_incl_scan(v) - v; }
+
+// ---- coherent scratch access (bypass the per-CU L1) ------------------------
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace pad

@@ -1,0 +1,741 @@
+// GPU k-mer index build (KmerReference, src/kmer.py:113-150), lookups, EXTSIM
+// statistics (src/kmer.py:152-230) and device-side synthetic reads.
+//
+// Index layout in HBM
+//   table          open addressing, linear probing, `cap` slots of
+//                  {uint64 key[NW]; uint32 cls; uint32 csize} (16 B for k <= 31),
+//                  load factor <= 0.5 (cap = 2 x genome windows).
+//   classes        the genome SET of a k-mer (the keys of kmers[kmer] in the
+//                  reference) is a "class": cls < G means the singleton {cls};
+//                  cls >= G indexes a deduplicated multi-genome set whose
+//                  ascending genome list lives in class_genomes[class_off[c]..]
+//                  with class_size[c] entries.  csize caches the set size in
+//                  the slot so --max-genomes and the specific/unspecific test
+//                  need no second memory access.
+//
+// Build pipeline (all stream-ordered, one host sync at the end)
+//   1. ASCII -> 2-bit codes (4 = anything else, e.g. 'N').
+//   2. per genome in FASTA order: insert every N-free window (atomicCAS claim),
+//      count distinct genomes per slot with a per-slot "last genome" atomicMax
+//      (launch order = FASTA order makes this exact), remember the first genome.
+//   3. singletons get cls = genome; multi slots get a bump-allocated list.
+//   4. per genome again: append g to the list of every multi slot it touches
+//      (ascending order for free, again from launch order).
+//   5. hash every multi list, dedup lists through a second hash table, verify
+//      each list against its class representative element by element (a hash
+//      collision is reported as PA_EINTERNAL, never merged silently), assign
+//      class ids and copy representative lists into class_genomes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "pa_device.h"
+#include "pa_internal.h"
+
+using namespace pad;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kRun = 16;  // windows per thread in the genome scans
+
+inline unsigned grid_for(uint64_t n, unsigned block = kBlock) {
+    uint64_t g = (n + block - 1) / block;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, 1u << 30));
+}
+
+__global__ void k_encode(const uint8_t *__restrict__ ascii, uint8_t *__restrict__ codes, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) codes[i] = (uint8_t)base_code(ascii[i]);
+}
+
+__global__ void k_fill_u64(uint64_t *p, uint64_t n, uint64_t v) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) p[i] = v;
+}
+
+// Insert (or find) a key; returns its slot.  Slots only go EMPTY -> key, so a
+// stale plain load can only show EMPTY, which the CAS then corrects.
+template <int NW>
+__device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, uint64_t h,
+                                 unsigned long long *n_kmers, uint32_t *err) {
+    uint64_t pos = home_slot(h, cap);
+    if constexpr (NW == 1) {
+        for (uint64_t it = 0; it < cap; it++) {
+            uint64_t cur = t[pos].key[0];
+            if (cur == k.w[0]) return pos;
+            if (cur == EMPTY) {
+                uint64_t old = atomicCAS((unsigned long long *)&t[pos].key[0], EMPTY, k.w[0]);
+                if (old == EMPTY) {
+                    atomicAdd(n_kmers, 1ull);
+                    return pos;
+                }
+                if (old == k.w[0]) return pos;
+            }
+            pos = (pos + 1 == cap) ? 0 : pos + 1;
+        }
+    } else {
+        // multi-word keys: the top word doubles as a lock (EMPTY -> BUSY -> key)
+        uint32_t spins = 0;
+        for (uint64_t it = 0; it < cap;) {
+            uint64_t cur = __hip_atomic_load(&t[pos].key[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == BUSY) {
+                if (++spins > (1u << 26)) break;
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            if (cur == EMPTY) {
+                uint64_t old = atomicCAS((unsigned long long *)&t[pos].key[0], EMPTY, BUSY);
+                if (old == EMPTY) {
+#pragma unroll
+                    for (int j = 1; j < NW; j++) st_agent(&t[pos].key[j], k.w[j]);
+                    __hip_atomic_store(&t[pos].key[0], k.w[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicAdd(n_kmers, 1ull);
+                    return pos;
+                }
+                continue;  // someone claimed it: look again
+            }
+            if (cur == k.w[0]) {
+                bool eq = true;
+#pragma unroll
+                for (int j = 1; j < NW; j++) eq &= (ld_agent(&t[pos].key[j]) == k.w[j]);
+                if (eq) return pos;
+            }
+            pos = (pos + 1 == cap) ? 0 : pos + 1;
+            it++;
+        }
+    }
+    atomicOr(err, 1u);
+    return ~0ull;
+}
+
+// Pass 1 over one genome: insert windows, count distinct genomes per slot.
+template <int NW>
+__global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
+                               uint64_t mask0, uint32_t g, Slot<NW> *table, uint64_t cap, uint32_t *deg,
+                               uint32_t *last_g, uint32_t *first_g, unsigned long long *n_kmers, uint32_t *err) {
+    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+    if (w0 >= nwin) return;
+    uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
+    const uint8_t *s = codes + gstart + w0;
+    Key<NW> key;
+#pragma unroll
+    for (int j = 0; j < NW; j++) key.w[j] = 0;
+    int run = 0;
+    for (int i = 0; i < k - 1; i++) {
+        uint32_t c = s[i];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+    }
+    for (uint64_t w = w0; w < w1; w++) {
+        uint32_t c = s[w - w0 + k - 1];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+        if (run < k) continue;  // window contains a non-ACGT base (src/kmer.py:145)
+        uint64_t slot = table_insert<NW>(table, cap, key, key_hash(key), n_kmers, err);
+        if (slot == ~0ull) return;
+        uint32_t old = atomicMax(&last_g[slot], g + 1);
+        if (old < g + 1) {
+            uint32_t d = atomicAdd(&deg[slot], 1u);
+            if (d == 0) first_g[slot] = g;
+        }
+    }
+}
+
+// Singletons -> final slot values; multi slots -> list storage.
+template <int NW>
+__global__ void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg, uint32_t *aux,
+                             uint64_t *off, unsigned long long *bump, unsigned long long *n_multi) {
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; s < cap; s += stride) {
+        if (table[s].key[0] == EMPTY) continue;
+        uint32_t d = deg[s];
+        if (d == 1) {
+            table[s].cls = aux[s];
+            table[s].csize = 1;
+        } else {
+            off[s] = atomicAdd(bump, (unsigned long long)d);
+            aux[s] = 0;
+            table[s].csize = d;
+            atomicAdd(n_multi, 1ull);
+        }
+    }
+}
+
+// Pass 2 over one genome: append g to the genome list of every multi slot.
+template <int NW>
+__global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
+                             uint64_t mask0, uint32_t g, const Slot<NW> *table, uint64_t cap, const uint32_t *deg,
+                             uint32_t *last_g, uint32_t *fill, const uint64_t *off, uint32_t *lists) {
+    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+    if (w0 >= nwin) return;
+    uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
+    const uint8_t *s = codes + gstart + w0;
+    Key<NW> key;
+#pragma unroll
+    for (int j = 0; j < NW; j++) key.w[j] = 0;
+    int run = 0;
+    for (int i = 0; i < k - 1; i++) {
+        uint32_t c = s[i];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+    }
+    for (uint64_t w = w0; w < w1; w++) {
+        uint32_t c = s[w - w0 + k - 1];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+        if (run < k) continue;
+        uint64_t slot;
+        uint32_t cls, csize;
+        if (!table_find<NW>(table, cap, key, key_hash(key), slot, cls, csize)) continue;  // cannot happen
+        if (deg[slot] < 2) continue;
+        uint32_t old = atomicMax(&last_g[slot], g + 1);
+        if (old < g + 1) {
+            uint32_t p = atomicAdd(&fill[slot], 1u);
+            lists[off[slot] + p] = g;
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t list_hash(const uint32_t *l, uint32_t n) {
+    uint64_t h = fmix64(0x51ED27C3A9F0B1D5ull ^ n);
+    for (uint32_t i = 0; i < n; i++) h = fmix64(h ^ ((uint64_t)l[i] * 0x9E3779B97F4A7C15ull + i));
+    return h >> 1;  // < 2^63: never EMPTY
+}
+
+template <int NW>
+__global__ void k_class_insert(const Slot<NW> *table, uint64_t cap, const uint32_t *deg, const uint64_t *off,
+                               const uint32_t *lists, uint64_t *cs_key, uint64_t *cs_rep, uint64_t cs_cap,
+                               uint32_t *err) {
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; s < cap; s += stride) {
+        if (table[s].key[0] == EMPTY || deg[s] < 2) continue;
+        uint64_t h = list_hash(lists + off[s], deg[s]);
+        uint64_t pos = home_slot(fmix64(h), cs_cap);
+        uint64_t it = 0;
+        for (; it < cs_cap; it++) {
+            uint64_t old = atomicCAS((unsigned long long *)&cs_key[pos], EMPTY, h);
+            if (old == EMPTY) {
+                cs_rep[pos] = s;
+                break;
+            }
+            if (old == h) break;
+            pos = (pos + 1 == cs_cap) ? 0 : pos + 1;
+        }
+        if (it == cs_cap) atomicOr(err, 4u);
+    }
+}
+
+__global__ void k_class_number(const uint64_t *cs_key, const uint64_t *cs_rep, uint32_t *cs_id, uint64_t cs_cap,
+                               const uint32_t *deg, uint32_t *class_size, uint64_t *class_off, uint64_t *rep_of,
+                               unsigned long long *n_cls, unsigned long long *bump) {
+    uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; e < cs_cap; e += stride) {
+        if (cs_key[e] == EMPTY) continue;
+        uint64_t id = atomicAdd(n_cls, 1ull);
+        uint64_t rep = cs_rep[e];
+        uint32_t d = deg[rep];
+        cs_id[e] = (uint32_t)id;
+        class_size[id] = d;
+        class_off[id] = atomicAdd(bump, (unsigned long long)d);
+        rep_of[id] = rep;
+    }
+}
+
+__global__ void k_class_copy(uint64_t n_cls, const uint64_t *rep_of, const uint32_t *class_size,
+                             const uint64_t *class_off, const uint64_t *off, const uint32_t *lists,
+                             uint32_t *class_genomes) {
+    uint64_t c = blockIdx.x;
+    for (; c < n_cls; c += gridDim.x) {
+        const uint32_t *src = lists + off[rep_of[c]];
+        uint32_t *dst = class_genomes + class_off[c];
+        for (uint32_t i = threadIdx.x; i < class_size[c]; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
+template <int NW>
+__global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint32_t *deg, const uint64_t *off,
+                               const uint32_t *lists, const uint64_t *cs_key, const uint64_t *cs_rep,
+                               const uint32_t *cs_id, uint64_t cs_cap, uint32_t n_genomes, uint32_t *err) {
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; s < cap; s += stride) {
+        if (table[s].key[0] == EMPTY || deg[s] < 2) continue;
+        uint32_t d = deg[s];
+        const uint32_t *l = lists + off[s];
+        uint64_t h = list_hash(l, d);
+        uint64_t pos = home_slot(fmix64(h), cs_cap);
+        while (cs_key[pos] != h) pos = (pos + 1 == cs_cap) ? 0 : pos + 1;
+        uint64_t rep = cs_rep[pos];
+        bool same = deg[rep] == d;
+        const uint32_t *rl = lists + off[rep];
+        for (uint32_t i = 0; same && i < d; i++) same = (rl[i] == l[i]);
+        if (!same) atomicOr(err, 2u);  // 63-bit list-hash collision: refuse, never merge
+        table[s].cls = n_genomes + cs_id[pos];
+    }
+}
+
+template <int NW>
+__global__ void k_lookup(const Slot<NW> *table, uint64_t cap, const uint8_t *kmers, uint64_t n, int k, uint64_t mask0,
+                         int64_t *cls_out, uint32_t *size_out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *s = kmers + i * (uint64_t)k;
+    Key<NW> key;
+#pragma unroll
+    for (int j = 0; j < NW; j++) key.w[j] = 0;
+    bool ok = true;
+    for (int j = 0; j < k; j++) {
+        uint32_t c = base_code(s[j]);
+        ok &= c < 4;
+        key_push(key, c & 3, mask0);
+    }
+    uint64_t slot;
+    uint32_t cls = 0, csize = 0;
+    if (ok && table_find<NW>(table, cap, key, key_hash(key), slot, cls, csize)) {
+        cls_out[i] = cls;
+        size_out[i] = csize;
+    } else {
+        cls_out[i] = -1;
+        size_out[i] = 0;
+    }
+}
+
+// ---- EXTSIM statistics ------------------------------------------------------
+
+template <int NW>
+__global__ void k_extsim_slots(const Slot<NW> *table, uint64_t cap, uint32_t n_genomes, const uint32_t *group_of,
+                               uint32_t n_groups, unsigned long long *total, unsigned long long *uniq,
+                               unsigned long long *class_count, int use_lds) {
+    extern __shared__ unsigned long long sh[];  // [n_groups] totals (singletons: total == uniq increments)
+    if (use_lds) {
+        for (uint32_t i = threadIdx.x; i < n_groups; i += blockDim.x) sh[i] = 0;
+        __syncthreads();
+    }
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; s < cap; s += stride) {
+        if (table[s].key[0] == EMPTY) continue;
+        uint32_t c = table[s].cls;
+        if (c < n_genomes) {
+            uint32_t a = group_of[c];
+            if (use_lds)
+                atomicAdd(&sh[a], 1ull);
+            else {
+                atomicAdd(&total[a], 1ull);
+                atomicAdd(&uniq[a], 1ull);
+            }
+        } else {
+            atomicAdd(&class_count[c - n_genomes], 1ull);
+        }
+    }
+    if (use_lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n_groups; i += blockDim.x)
+            if (sh[i]) {
+                atomicAdd(&total[i], sh[i]);
+                atomicAdd(&uniq[i], sh[i]);
+            }
+    }
+}
+
+// One block per multi class: distinct groups of the class, then all ordered pairs.
+__global__ void k_extsim_classes(uint64_t n_cls, const uint64_t *class_off, const uint32_t *class_size,
+                                 const uint32_t *class_genomes, const uint32_t *group_of, uint32_t n_groups,
+                                 const unsigned long long *class_count, unsigned long long *total,
+                                 unsigned long long *inter, uint32_t *scratch, uint64_t scratch_stride) {
+    __shared__ uint32_t n_distinct;
+    for (uint64_t c = blockIdx.x; c < n_cls; c += gridDim.x) {
+        unsigned long long nc = class_count[c];
+        if (nc == 0) continue;
+        uint32_t sz = class_size[c];
+        const uint32_t *gl = class_genomes + class_off[c];
+        uint32_t *grp = scratch + blockIdx.x * scratch_stride;
+        if (threadIdx.x == 0) n_distinct = 0;
+        __syncthreads();
+        // keep the first occurrence of every group (lists are short; O(sz^2) is fine)
+        for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) {
+            uint32_t a = group_of[gl[i]];
+            bool first = true;
+            for (uint32_t j = 0; j < i && first; j++) first = group_of[gl[j]] != a;
+            if (first) grp[atomicAdd(&n_distinct, 1u)] = a;
+        }
+        __syncthreads();
+        uint32_t nd = n_distinct;
+        for (uint64_t t = threadIdx.x; t < (uint64_t)nd * nd; t += blockDim.x) {
+            uint32_t x = (uint32_t)(t / nd), y = (uint32_t)(t % nd);
+            if (x == y)
+                atomicAdd(&total[grp[x]], nc);
+            else
+                atomicAdd(&inter[(uint64_t)grp[x] * n_groups + grp[y]], nc);
+        }
+        __syncthreads();
+    }
+}
+
+// ---- synthetic reads --------------------------------------------------------
+
+__device__ __forceinline__ uint64_t rng(uint64_t seed, uint64_t a, uint64_t b) {
+    return fmix64(seed * 0xD1B54A32D192ED03ull ^ fmix64(a * 0x9E3779B97F4A7C15ull + b));
+}
+
+__global__ void k_synth_reads(const uint8_t *__restrict__ codes, const uint64_t *__restrict__ goff,
+                              const uint32_t *__restrict__ eligible, uint32_t n_eligible, uint64_t n_reads,
+                              uint32_t len, uint64_t first, uint64_t seed, uint32_t sub_thresh, uint8_t *seq,
+                              uint8_t *qual, uint64_t *off) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t total = n_reads * len;
+    const char acgt[4] = {'A', 'C', 'G', 'T'};
+    for (; i < total; i += stride) {
+        uint64_t r = i / len;
+        uint32_t j = (uint32_t)(i - r * len);
+        uint64_t gr = first + r;
+        uint64_t h0 = rng(seed, gr, 0xFFFFFFFFull);
+        uint32_t g = eligible[(uint32_t)((h0 >> 32) * n_eligible >> 32)];
+        uint64_t glen = goff[g + 1] - goff[g];
+        uint64_t start = __umul64hi(rng(seed, gr, 0xFFFFFFFEull), glen - len + 1);
+        uint32_t c = codes[goff[g] + start + j];
+        uint64_t h = rng(seed, gr, j);
+        if (c > 3) c = (uint32_t)(h & 3);                       // N in the genome -> random base
+        if ((uint32_t)(h >> 40) < sub_thresh) c = (c + 1 + (uint32_t)((h >> 8) % 3)) & 3;  // substitution
+        // raw-ASCII quality: clipped normal(60, 8) via an Irwin-Hall sum of four uniforms
+        float u = (float)((h >> 2) & 0xFFF) + (float)((h >> 14) & 0xFFF) + (float)((h >> 26) & 0xFFF) +
+                  (float)(rng(seed, gr, j + 0x100000000ull) & 0xFFF);
+        float z = (u / 4096.0f - 2.0f) * 1.7320508f;
+        int q = (int)rintf(60.0f + 8.0f * z);
+        q = q < 35 ? 35 : (q > 74 ? 74 : q);
+        seq[i] = (uint8_t)acgt[c];
+        qual[i] = (uint8_t)q;
+        if (j == 0) off[r] = r * len;
+        if (i == total - 1) off[n_reads] = total;
+    }
+}
+
+template <int NW>
+pa_status build_nw(pa_index *idx, hipStream_t st) {
+    const uint32_t G = idx->n_genomes;
+    const int k = (int)idx->k;
+    const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
+    const uint64_t cap = idx->cap;
+    Slot<NW> *table = (Slot<NW> *)idx->table;
+    uint32_t *deg = nullptr, *last_g = nullptr, *aux = nullptr, *lists = nullptr, *cs_id = nullptr, *err = nullptr;
+    uint64_t *off = nullptr, *cs_key = nullptr, *cs_rep = nullptr, *rep_of = nullptr;
+    unsigned long long *cnt = nullptr;  // [0] n_kmers [1] bump [2] n_multi [3] n_cls [4] bump2
+    pa_status rc = PA_OK;
+    auto cleanup = [&]() {
+        hipFree(deg); hipFree(last_g); hipFree(aux); hipFree(off); hipFree(lists);
+        hipFree(cs_key); hipFree(cs_rep); hipFree(cs_id); hipFree(rep_of); hipFree(cnt); hipFree(err);
+    };
+#define B_HIP(call)                                                                                 \
+    do {                                                                                            \
+        hipError_t e_ = (call);                                                                     \
+        if (e_ != hipSuccess) {                                                                     \
+            pa::set_error(std::string("HIP error in index build: ") + hipGetErrorString(e_) + " (" #call ")"); \
+            cleanup();                                                                              \
+            return e_ == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;                              \
+        }                                                                                           \
+    } while (0)
+    B_HIP(hipMalloc(&deg, cap * 4));
+    B_HIP(hipMalloc(&last_g, cap * 4));
+    B_HIP(hipMalloc(&aux, cap * 4));
+    B_HIP(hipMalloc(&off, cap * 8));
+    B_HIP(hipMalloc(&cnt, 8 * 8));
+    B_HIP(hipMalloc(&err, 4));
+    B_HIP(hipMemsetAsync(deg, 0, cap * 4, st));
+    B_HIP(hipMemsetAsync(last_g, 0, cap * 4, st));
+    B_HIP(hipMemsetAsync(cnt, 0, 8 * 8, st));
+    B_HIP(hipMemsetAsync(err, 0, 4, st));
+    // pass 1
+    for (uint32_t g = 0; g < G; g++) {
+        uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
+        if (k <= 0 || (uint64_t)k > len) continue;
+        uint64_t nwin = len - k + 1;
+        hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
+                           idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, cap, deg, last_g, aux, cnt + 0, err);
+    }
+    B_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_build_prep<NW>, dim3(grid_for(cap, kBlock) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0,
+                       st, table, cap, deg, aux, off, cnt + 1, cnt + 2);
+    B_HIP(hipGetLastError());
+    unsigned long long h_cnt[8];
+    uint32_t h_err = 0;
+    B_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+    B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
+    B_HIP(hipStreamSynchronize(st));
+    if (h_err) {
+        pa::set_error("index build: hash table overflow or insert livelock (internal error)");
+        cleanup();
+        return PA_EINTERNAL;
+    }
+    idx->n_kmers = h_cnt[0];
+    const uint64_t list_total = h_cnt[1], n_multi = h_cnt[2];
+    idx->n_multi = 0;
+    if (n_multi > 0) {
+        B_HIP(hipMalloc(&lists, list_total * 4));
+        B_HIP(hipMemsetAsync(last_g, 0, cap * 4, st));
+        for (uint32_t g = 0; g < G; g++) {
+            uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
+            if ((uint64_t)k > len) continue;
+            uint64_t nwin = len - k + 1;
+            hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
+                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, cap, deg, last_g, aux, off,
+                               lists);
+        }
+        B_HIP(hipGetLastError());
+        uint64_t cs_cap = 2 * n_multi + 64;
+        B_HIP(hipMalloc(&cs_key, cs_cap * 8));
+        B_HIP(hipMalloc(&cs_rep, cs_cap * 8));
+        B_HIP(hipMalloc(&cs_id, cs_cap * 4));
+        hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0, st,
+                           cs_key, cs_cap, EMPTY);
+        unsigned sgrid = grid_for(cap) > 65536 ? 65536 : grid_for(cap);
+        hipLaunchKernelGGL(k_class_insert<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists, cs_key,
+                           cs_rep, cs_cap, err);
+        // class ids: at most n_multi classes
+        B_HIP(hipMalloc(&idx->class_size, n_multi * 4));
+        B_HIP(hipMalloc(&idx->class_off, n_multi * 8));
+        B_HIP(hipMalloc(&rep_of, n_multi * 8));
+        hipLaunchKernelGGL(k_class_number, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0,
+                           st, cs_key, cs_rep, cs_id, cs_cap, deg, idx->class_size, idx->class_off, rep_of, cnt + 3,
+                           cnt + 4);
+        B_HIP(hipGetLastError());
+        B_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+        B_HIP(hipStreamSynchronize(st));
+        const uint64_t n_cls = h_cnt[3], entries = h_cnt[4];
+        if ((uint64_t)G + n_cls >= 0xFFFFFFFFull) {
+            pa::set_error("index build: too many distinct genome sets for 32-bit class ids");
+            cleanup();
+            return PA_EUNSUPPORTED;
+        }
+        B_HIP(hipMalloc(&idx->class_genomes, std::max<uint64_t>(entries, 1) * 4));
+        hipLaunchKernelGGL(k_class_copy, dim3((unsigned)std::min<uint64_t>(n_cls, 65536)), dim3(kBlock), 0, st, n_cls,
+                           rep_of, idx->class_size, idx->class_off, off, lists, idx->class_genomes);
+        hipLaunchKernelGGL(k_class_assign<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists, cs_key,
+                           cs_rep, cs_id, cs_cap, G, err);
+        B_HIP(hipGetLastError());
+        B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
+        B_HIP(hipStreamSynchronize(st));
+        if (h_err) {
+            pa::set_error(h_err & 2 ? "index build: genome-set hash collision detected (refusing to merge sets)"
+                                    : "index build: class table overflow (internal error)");
+            cleanup();
+            return PA_EINTERNAL;
+        }
+        idx->n_multi = n_cls;
+        idx->class_entries = entries;
+        idx->device_bytes += n_multi * 12 + std::max<uint64_t>(entries, 1) * 4;
+    }
+#undef B_HIP
+    cleanup();
+    return rc;
+}
+
+template <int NW>
+pa_status lookup_nw(const pa_index *idx, const uint8_t *d_kmers, uint64_t n, int64_t *d_cls, uint32_t *d_size,
+                    hipStream_t st) {
+    const int k = (int)idx->k;
+    const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
+    hipLaunchKernelGGL(k_lookup<NW>, dim3(grid_for(n)), dim3(kBlock), 0, st, (const Slot<NW> *)idx->table, idx->cap,
+                       d_kmers, n, k, mask0, d_cls, d_size);
+    PA_HIP(hipGetLastError());
+    return PA_OK;
+}
+
+template <int NW>
+void extsim_slots_nw(const pa_index *idx, const uint32_t *d_group, uint32_t n_groups, unsigned long long *total,
+                     unsigned long long *uniq, unsigned long long *ccount, hipStream_t st) {
+    int use_lds = n_groups <= 4096;
+    size_t shm = use_lds ? (size_t)n_groups * 8 : 0;
+    unsigned grid = grid_for(idx->cap) > 4096 ? 4096 : grid_for(idx->cap);
+    hipLaunchKernelGGL(k_extsim_slots<NW>, dim3(grid), dim3(kBlock), shm, st, (const Slot<NW> *)idx->table, idx->cap,
+                       idx->n_genomes, d_group, n_groups, total, uniq, ccount, use_lds);
+}
+
+}  // namespace
+
+namespace pa {
+
+void index_release(pa_index *idx) {
+    hipFree(idx->table);
+    hipFree(idx->class_off);
+    hipFree(idx->class_size);
+    hipFree(idx->class_genomes);
+    hipFree(idx->codes);
+    hipFree(idx->goff);
+    hipFree(idx->ws.ptr);
+    hipFree(idx->queue);
+    hipFree(idx->counters);
+    for (auto e : idx->ev_start) hipEventDestroy(e);
+    for (auto e : idx->ev_stop) hipEventDestroy(e);
+    idx->table = nullptr;
+}
+
+pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
+                      hipStream_t st) {
+    idx->k = k;
+    idx->nw = k > 0 ? key_words(k) : 1;
+    idx->n_genomes = n;
+    idx->h_goff.assign(goff, goff + n + 1);
+    const uint64_t total = goff[n] - goff[0];
+    uint64_t windows = 0;
+    for (uint32_t g = 0; g < n; g++) {
+        uint64_t len = goff[g + 1] - goff[g];
+        if (k > 0 && (uint64_t)k <= len) windows += len - (uint64_t)k + 1;
+    }
+    for (auto &o : idx->h_goff) o -= goff[0];
+    idx->total_windows = windows;
+    idx->cap = std::max<uint64_t>(64, 2 * windows + 64);
+    const int sb = slot_bytes(idx->nw);
+    PA_HIP(hipMalloc(&idx->table, idx->cap * sb));
+    PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
+    PA_HIP(hipMalloc(&idx->codes, std::max<uint64_t>(total, 1)));
+    PA_HIP(hipMalloc(&idx->goff, (n + 1) * 8));
+    PA_HIP(hipMalloc(&idx->counters, 8 * 8));
+    PA_HIP(hipMemsetAsync(idx->counters, 0, 8 * 8, st));
+    PA_HIP(hipMemcpyAsync(idx->goff, idx->h_goff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
+    if (total > 0) {
+        // stage the ASCII genomes through the table memory's tail? keep it simple: a temp buffer
+        uint8_t *ascii = nullptr;
+        PA_HIP(hipMalloc(&ascii, total));
+        hipError_t e = hipMemcpyAsync(ascii, genomes + goff[0], total, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_encode, dim3(grid_for(total) > 65536 ? 65536 : grid_for(total)), dim3(kBlock), 0, st,
+                               ascii, idx->codes, total);
+            e = hipStreamSynchronize(st);
+        }
+        hipFree(ascii);
+        PA_HIP(e);
+    }
+    if (k <= 0 || windows == 0) return PA_OK;
+    switch (idx->nw) {
+        case 1: return build_nw<1>(idx, st);
+        case 2: return build_nw<2>(idx, st);
+        case 3: return build_nw<3>(idx, st);
+        case 4: return build_nw<4>(idx, st);
+        case 5: return build_nw<5>(idx, st);
+    }
+    set_error("unsupported k");
+    return PA_EUNSUPPORTED;
+}
+
+pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
+                       uint32_t *size_out, hipStream_t st) {
+    if (n == 0) return PA_OK;
+    if ((int64_t)kmer_len != idx->k || idx->k <= 0 || idx->n_kmers == 0) {
+        for (uint64_t i = 0; i < n; i++) {
+            cls_out[i] = -1;
+            if (size_out) size_out[i] = 0;
+        }
+        return PA_OK;
+    }
+    uint8_t *d_k = nullptr;
+    int64_t *d_c = nullptr;
+    uint32_t *d_s = nullptr;
+    PA_HIP(hipMalloc(&d_k, n * kmer_len));
+    PA_HIP(hipMalloc(&d_c, n * 8));
+    PA_HIP(hipMalloc(&d_s, n * 4));
+    PA_HIP(hipMemcpyAsync(d_k, kmers, n * kmer_len, hipMemcpyHostToDevice, st));
+    pa_status rc = PA_OK;
+    switch (idx->nw) {
+        case 1: rc = lookup_nw<1>(idx, d_k, n, d_c, d_s, st); break;
+        case 2: rc = lookup_nw<2>(idx, d_k, n, d_c, d_s, st); break;
+        case 3: rc = lookup_nw<3>(idx, d_k, n, d_c, d_s, st); break;
+        case 4: rc = lookup_nw<4>(idx, d_k, n, d_c, d_s, st); break;
+        default: rc = lookup_nw<5>(idx, d_k, n, d_c, d_s, st); break;
+    }
+    if (rc == PA_OK) {
+        PA_HIP(hipMemcpyAsync(cls_out, d_c, n * 8, hipMemcpyDeviceToHost, st));
+        if (size_out) PA_HIP(hipMemcpyAsync(size_out, d_s, n * 4, hipMemcpyDeviceToHost, st));
+        PA_HIP(hipStreamSynchronize(st));
+    }
+    hipFree(d_k);
+    hipFree(d_c);
+    hipFree(d_s);
+    return rc;
+}
+
+pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint32_t n_groups, uint64_t *total,
+                             uint64_t *uniq, uint64_t *inter, hipStream_t st) {
+    const uint64_t ng2 = (uint64_t)n_groups * n_groups;
+    for (uint32_t i = 0; i < n_groups; i++) total[i] = uniq[i] = 0;
+    for (uint64_t i = 0; i < ng2; i++) inter[i] = 0;
+    if (idx->n_kmers == 0 || n_groups == 0) return PA_OK;
+    uint32_t *d_group = nullptr, *scratch = nullptr;
+    unsigned long long *d_tot = nullptr, *d_uniq = nullptr, *d_inter = nullptr, *d_cc = nullptr;
+    const uint64_t nm = std::max<uint64_t>(idx->n_multi, 1);
+    const unsigned cgrid = (unsigned)std::min<uint64_t>(nm, 1024);
+    PA_HIP(hipMalloc(&d_group, (uint64_t)idx->n_genomes * 4));
+    PA_HIP(hipMalloc(&d_tot, n_groups * 8));
+    PA_HIP(hipMalloc(&d_uniq, n_groups * 8));
+    PA_HIP(hipMalloc(&d_inter, ng2 * 8));
+    PA_HIP(hipMalloc(&d_cc, nm * 8));
+    PA_HIP(hipMalloc(&scratch, (uint64_t)cgrid * (idx->n_genomes + 1) * 4));
+    PA_HIP(hipMemcpyAsync(d_group, group_of, (uint64_t)idx->n_genomes * 4, hipMemcpyHostToDevice, st));
+    PA_HIP(hipMemsetAsync(d_tot, 0, n_groups * 8, st));
+    PA_HIP(hipMemsetAsync(d_uniq, 0, n_groups * 8, st));
+    PA_HIP(hipMemsetAsync(d_inter, 0, ng2 * 8, st));
+    PA_HIP(hipMemsetAsync(d_cc, 0, nm * 8, st));
+    switch (idx->nw) {
+        case 1: extsim_slots_nw<1>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        case 2: extsim_slots_nw<2>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        case 3: extsim_slots_nw<3>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        case 4: extsim_slots_nw<4>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        default: extsim_slots_nw<5>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+    }
+    if (idx->n_multi > 0)
+        hipLaunchKernelGGL(k_extsim_classes, dim3(cgrid), dim3(kBlock), 0, st, idx->n_multi, idx->class_off,
+                           idx->class_size, idx->class_genomes, d_group, n_groups, d_cc, d_tot, d_inter, scratch,
+                           (uint64_t)idx->n_genomes + 1);
+    PA_HIP(hipGetLastError());
+    PA_HIP(hipMemcpyAsync(total, d_tot, n_groups * 8, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipMemcpyAsync(uniq, d_uniq, n_groups * 8, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipMemcpyAsync(inter, d_inter, ng2 * 8, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipStreamSynchronize(st));
+    hipFree(d_group); hipFree(d_tot); hipFree(d_uniq); hipFree(d_inter); hipFree(d_cc); hipFree(scratch);
+    return PA_OK;
+}
+
+pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_t len, uint64_t first,
+                           uint64_t seed, double sub_rate, hipStream_t st) {
+    std::vector<uint32_t> elig;
+    for (uint32_t g = 0; g < idx->n_genomes; g++)
+        if (idx->h_goff[g + 1] - idx->h_goff[g] >= len) elig.push_back(g);
+    if (elig.empty()) {
+        set_error("pa_reads_synthesize: no genome is at least read_len long");
+        return PA_EINVAL;
+    }
+    r->device = idx->device;
+    r->n = n;
+    r->n_bases = n * len;
+    r->max_len = len;
+    uint32_t *d_elig = nullptr;
+    PA_HIP(hipMalloc(&r->seq, std::max<uint64_t>(r->n_bases, 1)));
+    PA_HIP(hipMalloc(&r->qual, std::max<uint64_t>(r->n_bases, 1)));
+    PA_HIP(hipMalloc(&r->off, (n + 1) * 8));
+    PA_HIP(hipMalloc(&d_elig, elig.size() * 4));
+    PA_HIP(hipMemcpyAsync(d_elig, elig.data(), elig.size() * 4, hipMemcpyHostToDevice, st));
+    if (n == 0 || len == 0) {
+        PA_HIP(hipMemsetAsync(r->off, 0, (n + 1) * 8, st));
+    } else {
+        double t = sub_rate < 0 ? 0 : (sub_rate > 1 ? 1 : sub_rate);
+        uint32_t thresh = (uint32_t)std::min(16777215.0, t * 16777216.0);
+        hipLaunchKernelGGL(k_synth_reads, dim3(grid_for(r->n_bases) > 65536 ? 65536 : grid_for(r->n_bases)),
+                           dim3(kBlock), 0, st, idx->codes, idx->goff, d_elig, (uint32_t)elig.size(), n, len, first,
+                           seed, thresh, r->seq, r->qual, r->off);
+    }
+    PA_HIP(hipGetLastError());
+    PA_HIP(hipStreamSynchronize(st));
+    hipFree(d_elig);
+    return PA_OK;
+}
+
+}  // namespace pa

@@ -1,0 +1,119 @@
+// Internal host-side structures of libpa.so (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/pa.h"
+
+namespace pa {
+
+// Last error, thread-local; set by the PA_* macros below.
+void set_error(const std::string &msg);
+
+#define PA_HIP(call)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            ::pa::set_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " __FILE__ ":" + \
+                            std::to_string(__LINE__) + " (" #call ")");                          \
+            return PA_EDEVICE;                                                                    \
+        }                                                                                         \
+    } while (0)
+
+#define PA_TRY(call)                         \
+    do {                                     \
+        pa_status s_ = (call);               \
+        if (s_ != PA_OK) return s_;          \
+    } while (0)
+
+// Number of 64-bit words of a packed k-mer key: 2k bits, top word < 64 bits
+// so that an all-ones top word can never be a key (empty-slot sentinel).
+inline int key_words(int64_t k) { return (int)(k / 32) + 1; }
+// Bytes per hash-table slot: key words + {uint32 class, uint32 class size}.
+inline int slot_bytes(int nw) { return 8 * nw + 8; }
+
+// Device arguments of the per-read kernels (clamped, see pa_api.cpp).
+struct DevParams {
+    int32_t m, p;          // m >= 0; p < 0 -> no validation
+    int32_t mrq, mkq, mg;  // already clamped to ranges where semantics are unchanged
+    uint32_t flags;
+};
+
+struct Workspace {  // grow-only device scratch owned by an index
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace pa
+
+struct pa_index {
+    int device = 0;
+    int64_t k = 0;
+    int nw = 1;
+    uint32_t n_genomes = 0;
+    // open-addressing table: slots of {uint64 key[nw]; uint32 cls; uint32 csize}
+    void *table = nullptr;
+    uint64_t cap = 0;
+    uint64_t n_kmers = 0;
+    // classes: cls < n_genomes means {cls}; cls >= n_genomes is multi class (cls - n_genomes)
+    uint64_t n_multi = 0;
+    uint64_t *class_off = nullptr;    // [n_multi]
+    uint32_t *class_size = nullptr;   // [n_multi]
+    uint32_t *class_genomes = nullptr;
+    uint64_t class_entries = 0;
+    // genome codes (0-3 ACGT, 4 other) kept for read synthesis
+    uint8_t *codes = nullptr;
+    uint64_t *goff = nullptr;          // device [n_genomes+1]
+    std::vector<uint64_t> h_goff;
+    uint64_t total_windows = 0;
+    uint64_t device_bytes = 0;
+    // align scratch
+    pa::Workspace ws;
+    uint32_t *queue = nullptr;         // deferred read indices
+    uint64_t queue_cap = 0;
+    uint64_t *counters = nullptr;      // [0] queue length, [1] deferred total, [2] error flags
+    // profiling
+    bool profile = false;
+    std::vector<hipEvent_t> ev_start, ev_stop;
+    double prof_ms = 0;
+    uint64_t prof_launches = 0;
+};
+
+struct pa_reads {
+    int device = 0;
+    uint64_t n = 0;
+    uint64_t n_bases = 0;
+    uint32_t max_len = 0;
+    uint8_t *seq = nullptr;
+    uint8_t *qual = nullptr;
+    uint64_t *off = nullptr;  // [n+1]
+};
+
+struct pa_result {
+    int device = 0;
+    uint32_t n_genomes = 0;
+    uint64_t *sum_block = nullptr;  // [6 + 2G]
+    uint64_t *min_block = nullptr;  // [G]
+};
+
+namespace pa {
+pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
+                      hipStream_t st);
+pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
+                       uint32_t *size_out, hipStream_t st);
+pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint32_t n_groups, uint64_t *total,
+                             uint64_t *uniq, uint64_t *inter, hipStream_t st);
+pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_t len, uint64_t first,
+                           uint64_t seed, double sub_rate, hipStream_t st);
+pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t base, pa_result *acc,
+                hipStream_t st);
+pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uint8_t *type, uint32_t *qf,
+                       uint32_t *hr, uint64_t *list_off, uint32_t *lists, uint64_t list_cap, uint64_t *list_total,
+                       hipStream_t st);
+pa_status ensure_workspace(pa_index *idx, size_t bytes);
+void index_release(pa_index *idx);
+}  // namespace pa

@@ -1,0 +1,548 @@
+"""K-mer reference and pseudo-alignment, backed by the MI355X engine (libpa.so).
+
+Drop-in for the reference's src/kmer.py: same names, constructor arguments,
+attributes, return values and exceptions.  What changes is where the work runs:
+
+* ``KmerReference`` builds a device-resident open-addressing hash table of
+  2-bit-packed k-mers and their genome sets (``pa_index_build``) instead of
+  ``Dict[str, Dict[Record, Set[int]]]`` (src/kmer.py:113-150).
+* ``PseudoAlignment.align_reads_from_container`` ships the reads column-wise to
+  HBM and classifies all of them in one kernel pass (``pa_align``,
+  src/kmer.py:482-620); only per-genome counters and filter statistics come
+  back.  ``PseudoAlignment.reads`` (per-read mapping types and genome lists)
+  is materialised on first access by the per-read kernel (``pa_align_detail``).
+* ``KmerReference.kmers`` -- positions included -- is an introspection view
+  built on the host on first access; nothing on the align path reads it.
+
+Results (per-genome unique/ambiguous counts, filtered_* counters, the Summary
+key order) are bit-exact to the reference; see DESIGN.md for the quirk list
+this reproduces.  Known deviations: k above 159 raises PaUnsupported; argument
+errors of a batch (TypeError / ValueError / AddingExistingRead) are raised
+before any read of the batch is counted rather than at the offending read.
+"""
+
+from __future__ import annotations
+
+import gzip
+import json
+import pickle
+from collections import defaultdict, namedtuple
+from enum import Enum
+from typing import Any, Dict, Iterator, List, Optional, Sequence, Set, Tuple, Union
+
+import numpy as np
+
+import constants
+import pa_native as N
+from records import FASTAQRecordContainer, FASTARecordContainer, Record
+
+IGNORE_AMBIGUOUS_THRESHOLD = 0
+M_THRESHOLD = 0
+_NO_KEY = int(N.NO_FIRST_KEY)
+_DROPPED = 0  # PA_DROPPED
+
+
+class NotValidatingUniqueMapping(Exception):
+    def __init__(self, message: str) -> None:
+        super().__init__(message)
+
+
+class AddingExistingRead(Exception):
+    def __init__(self, message: str) -> None:
+        super().__init__(message)
+
+
+class ReadMappingType(Enum):
+    UNMAPPED = 1
+    UNIQUELY_MAPPED = 2
+    AMBIGUOUSLY_MAPPED = 3
+
+
+class KmerSpecifity(Enum):
+    SPECIFIC = 1
+    UNSPECIFIC = 2
+
+
+ReadKmer = namedtuple("ReadKmer", ["specifity", "references"])
+ReadMapping = namedtuple("ReadMapping", ["type", "genomes_mapped_to"])
+
+
+def extract_k_max_value_keys_from_dict(d: Dict[str, int], k: int) -> List[str]:
+    if not isinstance(d, dict):
+        raise ValueError("Input must be a dictionary.")
+    return sorted(d, key=lambda x: d[x], reverse=True)[:k] if d else []
+
+
+def extract_kmers_from_genome(k: int, genome: str) -> Iterator[Tuple[int, str]]:
+    """All (position, k-mer) windows of ``genome`` (src/kmer.py:84-94).
+
+    Host helper kept for API compatibility; the engine extracts windows on
+    the GPU (2-bit rolling keys in the build, funnel shifts in the align)."""
+    if k > len(genome) or k <= 0:
+        return iter([])
+    return ((i, genome[i:i + k]) for i in range(len(genome) - k + 1))
+
+
+def reverse_complement(seq: str) -> str:
+    return seq.translate(str.maketrans("ACGT", "TGCA"))[::-1]
+
+
+def _kmer_positions(genome: str, kmer: str) -> Set[int]:
+    out, i = set(), genome.find(kmer)
+    while i >= 0:
+        out.add(i)
+        i = genome.find(kmer, i + 1)
+    return out
+
+
+def _check_align_args(kmer_reference, m, p, mrq, mkq, mg, debug=False) -> Optional[Exception]:
+    """The checks of Read.pseudo_align (src/kmer.py:501-510) as an exception, or None."""
+    if not (isinstance(kmer_reference, KmerReference) and isinstance(m, int) and isinstance(p, int)
+            and (mrq is None or isinstance(mrq, int)) and (mkq is None or isinstance(mkq, int))
+            and (mg is None or isinstance(mg, int)) and isinstance(debug, bool)):
+        return TypeError(f"Invalid types given to pseudo align: {type(kmer_reference)}, {type(p)}, {type(m)}, "
+                         f"{type(debug)}")
+    if m < M_THRESHOLD:
+        return ValueError(f"m must be bigger than or equal to {M_THRESHOLD}")
+    return None
+
+
+class KmerReference:
+    """Device-resident k-mer reference of a FASTA container (src/kmer.py:109-351)."""
+
+    def __init__(self, k: int, fasta_record_container: FASTARecordContainer, filter_similar: bool = False,
+                 similarity_threshold: float = 0.95, device: Optional[int] = None) -> None:
+        if filter_similar and not (0 <= similarity_threshold <= 1):
+            raise ValueError("similarity_threshold must be between 0 and 1")
+        if not isinstance(k, int):
+            raise TypeError(f"k must be an int, got {type(k)}")
+        self.genomes: List[Record] = list(fasta_record_container)
+        self.kmer_len: int = k
+        self._device = N.default_device() if device is None else int(device)
+        self._build()
+        if filter_similar:
+            self._filter_similar_genomes(similarity_threshold)
+
+    # -- device index -------------------------------------------------------
+
+    def _build(self) -> None:
+        self._index = N.Index([g["genome"] for g in self.genomes], self.kmer_len, device=self._device)
+        self._view: Optional[Dict[str, Dict[Record, Set[int]]]] = None
+
+    @property
+    def index(self) -> N.Index:
+        return self._index
+
+    @property
+    def n_kmers(self) -> int:
+        """Number of distinct k-mers (== len(self.kmers))."""
+        return self._index.n_kmers
+
+    # -- EXTSIM (src/kmer.py:152-263) --------------------------------------
+
+    def _filter_similar_genomes(self, similarity_threshold: float) -> None:
+        idents = [g.identifier for g in self.genomes]
+        gid: Dict[str, int] = {}
+        group_of = [gid.setdefault(i, len(gid)) for i in idents]
+        total, uniq, inter = self._index.extsim_stats(group_of, len(gid))
+        stats: Dict[str, Dict[str, int]] = {}
+        for order, genome in enumerate(self.genomes):  # later duplicates overwrite, as in the reference
+            a = gid[genome.identifier]
+            stats[genome.identifier] = {"unique_kmers": int(uniq[a]), "total_kmers": int(total[a]),
+                                        "genome_length": len(genome["genome"]), "order": order}
+        ordered = sorted(stats.items(), key=lambda x: (x[1]["unique_kmers"], x[1]["total_kmers"],
+                                                       x[1]["genome_length"], x[1]["order"]))
+        kept: List[str] = []
+        info: Dict[str, Dict[str, Union[str, int, float]]] = {}
+        for ident, st in ordered:
+            a = gid[ident]
+            similar_to = None
+            for kid in kept:
+                b = gid[kid]
+                min_count = min(int(total[a]), int(total[b]))
+                score = (int(inter[a, b]) / min_count) if min_count > 0 else 0
+                if score > similarity_threshold:  # overlap coefficient, strict (src/kmer.py:206-208)
+                    similar_to = (kid, score)
+                    break
+            base = {"unique_kmers": st["unique_kmers"], "total_kmers": st["total_kmers"],
+                    "genome_length": st["genome_length"]}
+            if similar_to is None:
+                info[ident] = {"kept": "yes", **base, "similar_to": "NA", "similarity_score": "NA"}
+                kept.append(ident)
+            else:
+                info[ident] = {"kept": "no", **base, "similar_to": similar_to[0], "similarity_score": similar_to[1]}
+        keep = set(kept)
+        if len(keep) != len(gid):
+            self._index.close()
+            self.genomes = [g for g in self.genomes if g.identifier in keep]
+            self._build()  # pruning dropped genomes == building from the kept ones
+        self.similarity_info = info
+
+    # -- persistence ----------------------------------------------------------
+
+    def __getstate__(self):
+        state = {k: v for k, v in self.__dict__.items() if k not in ("_index", "_view")}
+        return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self._build()
+
+    def save(self, ref_file: str) -> None:
+        with gzip.open(ref_file, "wb") as f:
+            pickle.dump(self, f)
+
+    @classmethod
+    def load(cls, ref_file: str) -> "KmerReference":
+        with gzip.open(ref_file, "rb") as f:
+            return pickle.load(f)
+
+    # -- lookups ----------------------------------------------------------------
+
+    @property
+    def kmers(self) -> Dict[str, Dict[Record, Set[int]]]:
+        """Introspection view ``{kmer: {Record: positions}}`` in the reference's
+        insertion order (built on the host on first access; not used to align)."""
+        if self._view is None:
+            view: Dict[str, Dict[Record, Set[int]]] = {}
+            for rec in self.genomes:
+                for pos, km in extract_kmers_from_genome(self.kmer_len, rec["genome"]):
+                    if constants.NULL_NUCLEOTIDES_CHAR not in km:
+                        view.setdefault(km, {}).setdefault(rec, set()).add(pos)
+            self._view = view
+        return self._view
+
+    def _genome_set(self, kmer: str) -> List[int]:
+        cls, _ = self._index.lookup([kmer])
+        return [] if cls[0] < 0 else self._index.class_genomes(int(cls[0]))
+
+    def get_kmer_references(self, kmer: str) -> Dict[Record, Set[int]]:
+        if self._view is not None:
+            return self._view.get(kmer, {})
+        return {self.genomes[g]: _kmer_positions(self.genomes[g]["genome"], kmer) for g in self._genome_set(kmer)}
+
+    def __getitem__(self, kmer: str) -> Optional[Dict[Record, Set[int]]]:
+        return self.get_kmer_references(kmer) or None
+
+    def get_kmer_and_reverse_references(self, kmer: str) -> Dict[Record, Set[int]]:
+        result: Dict[Record, Set[int]] = {g: set(p) for g, p in self.get_kmer_references(kmer).items()}
+        rev = reverse_complement(kmer)
+        if rev != kmer:
+            for g, p in self.get_kmer_references(rev).items():
+                result.setdefault(g, set()).update(p)
+        return result
+
+    def get_summary(self) -> Dict[str, Any]:
+        """dumpref summary (src/kmer.py:300-329), from the introspection view."""
+        kmers = self.kmers
+        details = {km: {g["description"]: sorted(p) for g, p in gs.items()} for km, gs in kmers.items()}
+        summary: Dict[str, Dict[str, int]] = defaultdict(
+            lambda: {"total_bases": 0, "unique_kmers": 0, "multi_mapping_kmers": 0})
+        per_genome: Dict[str, Set[str]] = defaultdict(set)
+        for km, gs in kmers.items():
+            for g in gs:
+                summary[g["description"]]["total_bases"] = len(g["genome"])
+                per_genome[g["description"]].add(km)
+        for desc, kms in per_genome.items():
+            uniq = sum(1 for km in kms if len(kmers[km]) == 1)
+            summary[desc]["unique_kmers"] = uniq
+            summary[desc]["multi_mapping_kmers"] = len(kms) - uniq
+        out = {"Kmers": details, "Summary": dict(summary)}
+        if hasattr(self, "similarity_info"):
+            out["Similarity"] = self.similarity_info
+        return out
+
+
+class Read:
+    """One FASTQ read (src/kmer.py:357-526); pseudo_align runs on the GPU."""
+
+    def __init__(self, fastaq_record: Record) -> None:
+        self.identifier = fastaq_record.identifier
+        self.mapping = ReadMapping(ReadMappingType.UNMAPPED, [])
+        self.__raw_read: str = fastaq_record["sequence"]
+        self.__quality_scores: str = fastaq_record["quality_sequence"]
+        self.num_quality_filtered_kmers: int = 0
+        self.num_redundant_kmers: int = 0
+        self._kmers: Dict[str, ReadKmer] = {}
+        self._kmer_args = None
+
+    def __str__(self) -> str:
+        rows = [f"Mapping: {self.mapping}"]
+        for kmer, rk in self.kmers.items():
+            rows += [f"k-mer: {kmer}", f"specifity: {rk.specifity}", "Genome References:"]
+            rows += [f"\t{ref}" for ref in rk.references]
+        return "\n".join(rows)
+
+    __repr__ = __str__
+
+    def mean_quality(self) -> float:
+        return sum(map(ord, self.__quality_scores)) / len(self.__quality_scores)
+
+    def kmer_quality(self, start: int, k: int) -> float:
+        return sum(map(ord, self.__quality_scores[start:start + k])) / k
+
+    @property
+    def kmers(self) -> Dict[str, ReadKmer]:
+        """The read's distinct indexed k-mers (src/kmer.py:410-429), from GPU lookups."""
+        if self._kmer_args is not None:
+            ref, mkq, mg = self._kmer_args
+            self._kmer_args = None
+            k = ref.kmer_len
+            windows = list(extract_kmers_from_genome(k, self.__raw_read))
+            cls, size = ref.index.lookup([w for _, w in windows]) if windows else ([], [])
+            for (start, km), c, s in zip(windows, cls, size):
+                if mkq is not None and self.kmer_quality(start, k) < mkq:
+                    continue
+                if c < 0 or (mg is not None and int(s) > mg):
+                    continue
+                refs = ref.get_kmer_references(km)
+                self._kmers[km] = ReadKmer(KmerSpecifity.SPECIFIC if int(s) == 1 else KmerSpecifity.UNSPECIFIC, refs)
+        return self._kmers
+
+    def _packed(self):
+        seq = np.frombuffer(self.__raw_read.encode("ascii", errors="replace"), dtype=np.uint8)
+        qual = np.frombuffer(self.__quality_scores.encode("latin-1", errors="replace"), dtype=np.uint8)
+        return seq, qual, np.array([0, seq.size], dtype=np.uint64)
+
+    def pseudo_align(self, kmer_reference: KmerReference, m: int = 1, p: int = 1,
+                     min_read_quality: Optional[int] = None, min_kmer_quality: Optional[int] = None,
+                     max_genomes: Optional[int] = None, debug: bool = False) -> ReadMappingType:
+        err = _check_align_args(kmer_reference, m, p, min_read_quality, min_kmer_quality, max_genomes, debug)
+        if err is not None:
+            raise err
+        if min_read_quality is not None and self.mean_quality() < min_read_quality:
+            return ReadMappingType.UNMAPPED
+        seq, qual, off = self._packed()
+        reads = N.Reads.upload(seq, qual, off, device=kmer_reference.index.device)
+        prm = N.Params.make(m, p, None, min_kmer_quality, max_genomes)
+        types, qf, hr, loff, lists = N.align_detail(kmer_reference.index, reads, prm)
+        reads.close()
+        self.num_quality_filtered_kmers += int(qf[0])
+        self.num_redundant_kmers += int(hr[0])
+        self._kmer_args = (kmer_reference, min_kmer_quality, max_genomes)
+        t = ReadMappingType(int(types[0]))
+        if t != ReadMappingType.UNMAPPED:
+            self.mapping = ReadMapping(t, [kmer_reference.genomes[int(g)] for g in lists[loff[0]:loff[1]]])
+        if debug:
+            print(f"[DEBUG pseudo_align]: self.mapping: {self.mapping.type}, mapped to: {self.mapping}")
+        return t
+
+
+class _Batch:
+    """A container batch aligned on the GPU, kept for lazy per-read results."""
+
+    __slots__ = ("base", "ids", "seq", "qual", "off", "params", "entries")
+
+    def __init__(self, base, ids, seq, qual, off, params):
+        self.base, self.ids, self.seq, self.qual, self.off, self.params = base, ids, seq, qual, off, params
+        self.entries = None
+
+
+def _columnar(container) -> Tuple[List[str], np.ndarray, np.ndarray, np.ndarray]:
+    if isinstance(container, FASTAQRecordContainer):
+        return container.ids, container.seq, container.qual, container.offsets
+    ids, seqs, quals = [], [], []
+    for rec in container:
+        ids.append(rec.identifier)
+        seqs.append(rec["sequence"])
+        quals.append(rec["quality_sequence"])
+    seq, off = N.concat(seqs)
+    qual, _ = N.concat(quals)
+    return ids, seq, qual, off
+
+
+class PseudoAlignment:
+    """Pseudo-alignment of reads against a KmerReference (src/kmer.py:532-699)."""
+
+    def __init__(self, kmer_reference: KmerReference) -> None:
+        self.kmer_reference: KmerReference = kmer_reference
+        self.filtered_quality_reads: int = 0
+        self.filtered_quality_kmers: int = 0
+        self.filtered_hr_kmers: int = 0
+        self.filter_read_quality_flag: bool = False
+        self.filter_kmer_quality_flag: bool = False
+        self.filter_max_genomes_flag: bool = False
+        self._next_index = 0
+        self._result: Optional[N.Result] = None
+        self._gpu_stats = np.zeros(6, dtype=np.uint64)
+        self._batches: List[_Batch] = []
+        self._host: List[Tuple[int, str, Dict[str, Any]]] = []  # (index, id, entry) of add_read()
+        self._ids: Optional[Set[str]] = None
+
+    # -- bookkeeping ------------------------------------------------------------
+
+    def _known_ids(self) -> Set[str]:
+        if self._ids is None:
+            ids: Set[str] = set()
+            for b in self._batches:
+                ids.update(b.ids)
+            ids.update(i for _, i, _ in self._host)
+            self._ids = ids
+        return self._ids
+
+    def _add_ids(self, ids: Sequence[str]) -> None:
+        if not self._batches and not self._host:
+            return  # the first batch comes from one container, whose ids the parser made unique
+        known = self._known_ids()
+        for rid in ids:
+            if rid in known:
+                raise AddingExistingRead(f"There already exists a read with identifier: {rid}")
+
+    def add_read(self, read: Read) -> None:
+        self._add_ids([read.identifier])
+        if self._ids is not None:
+            self._ids.add(read.identifier)
+        entry = {"mapping_type": read.mapping.type,
+                 "genomes_mapped_to": [g.identifier for g in read.mapping.genomes_mapped_to]}
+        self._host.append((self._next_index, read.identifier, entry))
+        self._next_index += 1
+
+    def add_read_from_read_record(self, read_record: Record, m: int = 1, p: int = 1,
+                                  min_read_quality: Optional[int] = None, min_kmer_quality: Optional[int] = None,
+                                  max_genomes: Optional[int] = None) -> None:
+        ids = [read_record.identifier]
+        seq, off = N.concat([read_record["sequence"]])
+        qual = np.frombuffer(read_record["quality_sequence"].encode("latin-1", errors="replace"), dtype=np.uint8)
+        self._align_columns(ids, seq, qual, off, m, p, min_read_quality, min_kmer_quality, max_genomes)
+
+    def align_reads_from_container(self, reads_container: FASTAQRecordContainer, m: int = 1, p: int = 1,
+                                   min_read_quality: Optional[int] = None, min_kmer_quality: Optional[int] = None,
+                                   max_genomes: Optional[int] = None) -> None:
+        ids, seq, qual, off = _columnar(reads_container)
+        self._align_columns(ids, seq, qual, off, m, p, min_read_quality, min_kmer_quality, max_genomes)
+
+    def _align_columns(self, ids, seq, qual, off, m, p, mrq, mkq, mg) -> None:
+        n = len(ids)
+        if n == 0:
+            return
+        if mrq is not None:
+            self.filter_read_quality_flag = True
+        if mkq is not None:
+            self.filter_kmer_quality_flag = True
+        if mg is not None:
+            self.filter_max_genomes_flag = True
+        err = _check_align_args(self.kmer_reference, m, p, mrq, mkq, mg)
+        if err is not None:
+            # the reference checks arguments only for reads that pass --min-read-quality
+            if mrq is None or not isinstance(mrq, (int, float)):
+                raise err
+            sums = np.add.reduceat(qual.astype(np.int64), off[:-1].astype(np.int64)) if qual.size else None
+            lens = np.diff(off).astype(np.int64)
+            if sums is None or np.any(sums >= mrq * lens):
+                raise err
+        self._add_ids(ids)
+        ref = self.kmer_reference
+        if self._result is None:
+            self._result = N.Result(ref.index)
+        prm = N.Params.make(m if err is None else 0, p if err is None else 0, mrq, mkq, mg)
+        reads = N.Reads.upload(seq, qual, off, device=ref.index.device)
+        N.align(ref.index, reads, prm, self._next_index, self._result)
+        stats, _, _, _ = self._result.fetch()
+        reads.close()
+        delta = stats - self._gpu_stats
+        self._gpu_stats = stats
+        self.filtered_quality_reads += int(delta[3])
+        self.filtered_quality_kmers += int(delta[4])
+        self.filtered_hr_kmers += int(delta[5])
+        self._batches.append(_Batch(self._next_index, ids, seq, qual, off, prm))
+        if self._ids is not None:
+            self._ids.update(ids)
+        self._next_index += n
+
+    # -- results ----------------------------------------------------------------
+
+    @property
+    def reads(self) -> Dict[str, Dict[str, Any]]:
+        """``{read id: {"mapping_type", "genomes_mapped_to"}}`` in insertion order;
+        reads dropped by --min-read-quality are absent (src/kmer.py:587-589)."""
+        ref = self.kmer_reference
+        items: List[Tuple[int, str, Dict[str, Any]]] = list(self._host)
+        for b in self._batches:
+            if b.entries is None:
+                reads = N.Reads.upload(b.seq, b.qual, b.off, device=ref.index.device)
+                types, _, _, loff, lists = N.align_detail(ref.index, reads, b.params)
+                reads.close()
+                names = [g.identifier for g in ref.genomes]
+                ent = []
+                for i, t in enumerate(types):
+                    if t == _DROPPED:  # filtered by --min-read-quality: not a read of the alignment
+                        continue
+                    gl = [names[int(g)] for g in lists[loff[i]:loff[i + 1]]]
+                    ent.append((b.base + i, b.ids[i], {"mapping_type": ReadMappingType(int(t)),
+                                                       "genomes_mapped_to": gl}))
+                b.entries = ent
+            items.extend(b.entries)
+        items.sort(key=lambda x: x[0])
+        return {rid: e for _, rid, e in items}
+
+    def get_summary(self) -> Dict[str, Dict[str, Union[int, Dict[str, int]]]]:
+        stats = self._gpu_stats.astype(np.int64)
+        summary: Dict[str, Union[int, Dict[str, int]]] = {
+            "unique_mapped_reads": int(stats[0]),
+            "ambiguous_mapped_reads": int(stats[1]),
+            "unmapped_reads": int(stats[2]),
+        }
+        if self.filter_read_quality_flag:
+            summary["filtered_quality_reads"] = self.filtered_quality_reads
+        if self.filter_kmer_quality_flag:
+            summary["filtered_quality_kmers"] = self.filtered_quality_kmers
+        if self.filter_max_genomes_flag:
+            summary["filtered_hr_kmers"] = self.filtered_hr_kmers
+        counts: Dict[str, List[int]] = {}
+        first: Dict[str, int] = {}
+        if self._result is not None:
+            _, uq, am, fk = self._result.fetch()
+            for g in np.flatnonzero(fk != N.NO_FIRST_KEY):
+                name = self.kmer_reference.genomes[int(g)].identifier
+                c = counts.setdefault(name, [0, 0])
+                c[0] += int(uq[g])
+                c[1] += int(am[g])
+                first[name] = min(first.get(name, _NO_KEY), int(fk[g]))
+        for idx, _, e in self._host:
+            t = e["mapping_type"]
+            if t == ReadMappingType.UNMAPPED:
+                summary["unmapped_reads"] += 1
+                continue
+            col = 0 if t == ReadMappingType.UNIQUELY_MAPPED else 1
+            summary["unique_mapped_reads" if col == 0 else "ambiguous_mapped_reads"] += 1
+            for pos, name in enumerate(e["genomes_mapped_to"]):
+                counts.setdefault(name, [0, 0])[col] += 1
+                first[name] = min(first.get(name, _NO_KEY), (idx << 20) | pos)
+        genome_mapping = {name: {"unique_reads": counts[name][0], "ambiguous_reads": counts[name][1]}
+                          for name in sorted(first, key=first.get)}
+        return {"Statistics": summary, "Summary": genome_mapping}
+
+    def get_reads_by_mapping_type(self, mapping_type: ReadMappingType) -> List[str]:
+        return [rid for rid, d in self.reads.items() if d["mapping_type"] == mapping_type]
+
+    def export_summary_to_json(self, json_file: str) -> None:
+        with open(json_file, "w") as f:
+            json.dump(self.get_summary(), f, indent=4)
+
+    def __repr__(self) -> str:
+        return json.dumps(self.get_summary(), indent=4)
+
+    # -- persistence: per-read results are materialised, device state dropped ----
+
+    def __getstate__(self):
+        reads = self.reads
+        state = {k: v for k, v in self.__dict__.items() if k not in ("_result", "_batches", "_host", "_ids")}
+        state["_host"] = [(i, rid, e) for i, (rid, e) in enumerate(reads.items())]
+        state["_next_index"] = len(reads)
+        state["_gpu_stats"] = np.zeros(6, dtype=np.uint64)
+        return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        self._result = None
+        self._batches = []
+        self._ids = None
+
+    def save(self, align_file: str) -> None:
+        with gzip.open(align_file, "wb") as f:
+            pickle.dump(self, f)
+
+    @classmethod
+    def load(cls, align_file: str) -> "PseudoAlignment":
+        with gzip.open(align_file, "rb") as f:
+            return pickle.load(f)

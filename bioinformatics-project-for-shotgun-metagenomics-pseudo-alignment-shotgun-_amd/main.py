@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Command-line interface, drop-in for the reference's src/main.py.
+
+    python3 main.py -t dumpalign -g GENOMES.fa -k 31 --reads READS.fq [-m M] [-p P]
+                    [--min-read-quality Q] [--min-kmer-quality QK] [--max-genomes MG]
+                    [--filter-similar [--similarity-threshold T]]
+
+Same tasks (reference | dumpref | align | dumpalign), flags, flag-combination
+checks, default coercions and error exits as src/main.py:61-402:
+
+* ``-m 0`` / ``-p 0`` / ``--similarity-threshold 0`` are falsy and coerced to
+  their defaults (1, 1, 0.95), exactly like src/main.py:337-342;
+* errors end the process with ``sys.exit(message)`` (non-zero, message on
+  stderr).
+
+The ``.kdb`` / ``.aln`` files are gzip pickles of this package's objects (the
+reference's files are pickles of its own classes, so neither side can read the
+other's); a loaded reference rebuilds its device index.
+"""
+
+from __future__ import annotations
+
+import argparse
+import gzip
+import json
+import os
+import sys
+from typing import List, Optional
+
+from constants import DEFAULT_AMBIGUOUS_THRESHOLD, DEFAULT_SIMILARITY_THRESHOLD, DEFAULT_UNIQUE_THRESHOLD
+from data_file import FASTAFile, FASTAQFile, InvalidExtensionError, NoRecordsInDataFile
+from kmer import AddingExistingRead, KmerReference, NotValidatingUniqueMapping, PseudoAlignment
+
+
+def validate_file_readable(filepath: str, description: str) -> None:
+    if not os.path.isfile(filepath):
+        sys.exit(f"Error: {description} file '{filepath}' does not exist or is not a file.")
+    if not os.access(filepath, os.R_OK):
+        sys.exit(f"Error: {description} file '{filepath}' is not readable.")
+
+
+def validate_file_writable(filepath: str, description: str) -> None:
+    dir_path = os.path.dirname(filepath) or "."
+    if os.path.exists(filepath) and not os.access(filepath, os.W_OK):
+        sys.exit(f"Error: {description} file '{filepath}' is not writable.")
+    if not os.path.exists(filepath) and not os.access(dir_path, os.W_OK):
+        sys.exit(f"Error: Directory '{dir_path}' is not writable to create {description} file '{filepath}'.")
+
+
+def parse_arguments(args: Optional[List[str]] = None) -> argparse.Namespace:
+    parser = argparse.ArgumentParser(prog="Biosequence project")
+    parser.add_argument("-t", "--task", required=True, help="Task to execute")
+    parser.add_argument("-g", "--genomefile", help="Genome FASTA file (multiple records)")
+    parser.add_argument("-k", "--kmer-size", type=int, help="Length of k-mers")
+    parser.add_argument("-r", "--referencefile", help="KDB file (input/output)")
+    parser.add_argument("-a", "--alignfile", help="aln file. Can be either input or name for output file")
+    parser.add_argument("--reads", help="FASTQ reads file")
+    parser.add_argument("-m", "--unique-threshold", help="unique k-mer threshold", type=int)
+    parser.add_argument("-p", "--ambiguous-threhold", help="ambiguous k-mer threshold", type=int)
+    parser.add_argument("--reverse-complement", action="store_true")  # parsed, unused (as in the reference)
+    parser.add_argument("--min-read-quality", type=int, default=None)
+    parser.add_argument("--min-kmer-quality", type=int, default=None)
+    parser.add_argument("--max-genomes", type=int, default=None)
+    parser.add_argument("--filter-similar", action="store_true")
+    parser.add_argument("--similarity-threshold", type=float)
+    return parser.parse_args(args)
+
+
+def _load_reference(reference_file: str) -> KmerReference:
+    try:
+        return KmerReference.load(reference_file)
+    except gzip.BadGzipFile:
+        sys.exit("Error: Incorrect format of input file.")
+
+
+def create_reference(fasta_file: str, kmer_size: int, filter_similar: bool = False,
+                     similarity_threshold: float = 0.95) -> KmerReference:
+    container = FASTAFile(fasta_file).container
+    return KmerReference(kmer_size, container, filter_similar=filter_similar,
+                         similarity_threshold=similarity_threshold)
+
+
+def create_alignment_from_reference(kmer_reference: KmerReference, reads_file: str, m: int, p: int,
+                                    min_read_quality, min_kmer_quality, max_genomes) -> PseudoAlignment:
+    reads = FASTAQFile(reads_file).container
+    alignment = PseudoAlignment(kmer_reference)
+    alignment.align_reads_from_container(reads, m, p, min_read_quality, min_kmer_quality, max_genomes)
+    return alignment
+
+
+def _print_json(obj) -> None:
+    print(json.dumps(obj, indent=4))
+
+
+def _check_task(args: argparse.Namespace) -> None:
+    """Flag combinations (src/main.py:321-334), truthiness-based like the reference."""
+    extra = (args.reads or args.alignfile or args.unique_threshold or args.ambiguous_threhold
+             or args.min_read_quality or args.min_kmer_quality or args.max_genomes)
+    if args.task == "reference":
+        if extra:
+            sys.exit("Error: For task 'reference', only -g, -k, -r, --filter-similar, and --similarity-threshold "
+                     "are allowed.")
+    elif args.task == "dumpref":
+        if extra:
+            sys.exit("Error: For task 'dumpref', only -r or (-g and -k) with --filter-similar and "
+                     "--similarity-threshold are allowed.")
+    elif args.task == "align":
+        if not ((args.referencefile and args.reads and args.alignfile)
+                or (args.genomefile and args.kmer_size and args.reads and args.alignfile)):
+            sys.exit("Error: For task 'align', provide either -r (reference file) or -g and -k (genome file and "
+                     "kmer size) along with --reads and -a.")
+    elif args.task == "dumpalign":
+        if not ((args.referencefile and args.reads) or (args.genomefile and args.kmer_size and args.reads)
+                or args.alignfile):
+            sys.exit("Error: For task 'dumpalign', provide either -r and --reads, or -g, -k, and --reads, or -a.")
+    else:
+        sys.exit("Error: Unsupported task.")
+
+
+def _run(args: argparse.Namespace) -> None:
+    filt = (args.unique_threshold, args.ambiguous_threhold, args.min_read_quality, args.min_kmer_quality,
+            args.max_genomes)
+    if args.task == "reference":
+        validate_file_readable(args.genomefile, "Genome FASTA")
+        validate_file_writable(args.referencefile, "Reference database output")
+        create_reference(args.genomefile, args.kmer_size, args.filter_similar,
+                         args.similarity_threshold).save(args.referencefile)
+    elif args.task == "dumpref":
+        if args.referencefile:
+            validate_file_readable(args.referencefile, "Reference database")
+            _print_json(_load_reference(args.referencefile).get_summary())
+        elif args.genomefile and args.kmer_size:
+            validate_file_readable(args.genomefile, "Genome FASTA")
+            _print_json(create_reference(args.genomefile, args.kmer_size, args.filter_similar,
+                                         args.similarity_threshold).get_summary())
+    elif args.task == "align":
+        validate_file_readable(args.reads, "FASTQ reads")
+        validate_file_writable(args.alignfile, "Alignment output")
+        if args.referencefile and args.reads and args.alignfile:
+            validate_file_readable(args.referencefile, "Reference database")
+            ref = _load_reference(args.referencefile)
+        else:
+            validate_file_readable(args.genomefile, "Genome FASTA")
+            ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
+            if args.referencefile:
+                ref.save(args.referencefile)
+        create_alignment_from_reference(ref, args.reads, *filt).save(args.alignfile)
+    elif args.task == "dumpalign":
+        if args.referencefile and args.reads:
+            validate_file_readable(args.reads, "FASTQ reads")
+            ref = _load_reference(args.referencefile)
+            _print_json(create_alignment_from_reference(ref, args.reads, *filt).get_summary())
+        elif args.genomefile and args.kmer_size and args.reads:
+            validate_file_readable(args.reads, "FASTQ reads")
+            validate_file_readable(args.genomefile, "Genome FASTA")
+            ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
+            _print_json(create_alignment_from_reference(ref, args.reads, *filt).get_summary())
+        elif args.alignfile:
+            validate_file_readable(args.alignfile, "Alignment output")
+            try:
+                alignment = PseudoAlignment.load(args.alignfile)
+            except gzip.BadGzipFile:
+                sys.exit("Error: Incorrect format of input file.")
+            _print_json(alignment.get_summary())
+        else:
+            sys.exit("Error: Provide either -g and -k with --reads, or -r with --reads, or -a.")
+    else:
+        sys.exit("Error: Unsupported task.")
+
+
+def main(argv: Optional[List[str]] = None) -> None:
+    args = parse_arguments(argv)
+    _check_task(args)
+    # falsy -> default, as src/main.py:337-342 (so -m 0 and -p 0 become 1)
+    if not args.unique_threshold:
+        args.unique_threshold = DEFAULT_UNIQUE_THRESHOLD
+    if not args.ambiguous_threhold:
+        args.ambiguous_threhold = DEFAULT_AMBIGUOUS_THRESHOLD
+    if not args.similarity_threshold:
+        args.similarity_threshold = DEFAULT_SIMILARITY_THRESHOLD
+    try:
+        _run(args)
+    except gzip.BadGzipFile:
+        sys.exit("Error: Incorrect format of input file.")
+    except (InvalidExtensionError, NoRecordsInDataFile, NotValidatingUniqueMapping, AddingExistingRead,
+            ValueError) as err:
+        sys.exit(err)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,378 @@
+"""ctypes binding of libpa.so (include/pa.h).
+
+This is the only module that talks to the native library.  There is no CPU
+fallback: if libpa.so is missing or no HIP device is visible, every call fails
+loudly (ImportError / PaDeviceError).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PA_LIBRARY", os.path.join(HERE, "libpa.so"))
+
+PA_OK, PA_EINVAL, PA_ETYPE, PA_ENOMEM, PA_EDEVICE, PA_EUNSUPPORTED, PA_EINTERNAL = range(7)
+PA_MAX_K = 159
+HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4
+NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
+
+# every symbol declared in include/pa.h
+EXPORTS = (
+    "pa_last_error", "pa_version", "pa_device_count",
+    "pa_index_build", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
+    "pa_index_extsim_stats",
+    "pa_reads_upload", "pa_reads_synthesize", "pa_reads_info", "pa_reads_download", "pa_reads_free",
+    "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_free",
+    "pa_align", "pa_align_detail", "pa_align_batch",
+    "pa_profile_enable", "pa_profile_read",
+)
+
+
+class PaError(RuntimeError):
+    pass
+
+
+class PaDeviceError(PaError):
+    pass
+
+
+class PaUnsupported(PaError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_int64), ("p", ctypes.c_int64), ("min_read_quality", ctypes.c_int64),
+                ("min_kmer_quality", ctypes.c_int64), ("max_genomes", ctypes.c_int64),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+    @classmethod
+    def make(cls, m=1, p=1, min_read_quality=None, min_kmer_quality=None, max_genomes=None) -> "Params":
+        flags = ((HAS_MRQ if min_read_quality is not None else 0) | (HAS_MKQ if min_kmer_quality is not None else 0)
+                 | (HAS_MG if max_genomes is not None else 0))
+
+        def clamp(v):  # Python ints are unbounded; the C side clamps again to semantic ranges
+            return max(min(int(v), 2 ** 62), -2 ** 62)
+        return cls(clamp(m), clamp(p), clamp(min_read_quality or 0), clamp(min_kmer_quality or 0),
+                   clamp(max_genomes or 0), flags, 0)
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("unique_mapped_reads", "ambiguous_mapped_reads", "unmapped_reads",
+                                               "filtered_quality_reads", "filtered_quality_kmers",
+                                               "filtered_hr_kmers")]
+
+
+class IndexInfo(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_uint32), ("n_genomes", ctypes.c_uint32), ("key_words", ctypes.c_uint32),
+                ("slot_bytes", ctypes.c_uint32)] + [
+        (n, ctypes.c_uint64) for n in ("n_kmers", "n_multi_classes", "class_genome_entries", "table_slots",
+                                       "table_bytes", "total_windows", "device_bytes")]
+
+
+_lib = None
+P = ctypes.c_void_p
+PP = ctypes.POINTER(ctypes.c_void_p)
+U64 = ctypes.c_uint64
+I64 = ctypes.c_int64
+U32 = ctypes.c_uint32
+I32 = ctypes.c_int32
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libpa.so not found at {LIB_PATH}; build it with `python build_native.py` "
+                          "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "pa_last_error": (ctypes.c_char_p, []),
+        "pa_version": (ctypes.c_char_p, []),
+        "pa_device_count": (I32, [ctypes.POINTER(I32)]),
+        "pa_index_build": (I32, [I32, ctypes.c_char_p, P, U32, I64, P, PP]),
+        "pa_index_free": (None, [P]),
+        "pa_index_get_info": (I32, [P, ctypes.POINTER(IndexInfo)]),
+        "pa_index_lookup": (I32, [P, ctypes.c_char_p, U64, U32, P, P, P]),
+        "pa_index_class_genomes": (I32, [P, I64, P, U32, ctypes.POINTER(U32), P]),
+        "pa_index_extsim_stats": (I32, [P, P, U32, P, P, P, P]),
+        "pa_reads_upload": (I32, [I32, P, P, P, U64, P, PP]),
+        "pa_reads_synthesize": (I32, [P, U64, U32, U64, U64, ctypes.c_double, P, PP]),
+        "pa_reads_info": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U32)]),
+        "pa_reads_download": (I32, [P, U64, U64, P, P, P, P]),
+        "pa_reads_free": (None, [P]),
+        "pa_result_create": (I32, [P, PP]),
+        "pa_result_reset": (I32, [P, P]),
+        "pa_result_fetch": (I32, [P, ctypes.POINTER(Stats), P, P, P, P]),
+        "pa_result_device_view": (I32, [P, PP, ctypes.POINTER(U64), PP, ctypes.POINTER(U64)]),
+        "pa_result_free": (None, [P]),
+        "pa_align": (I32, [P, P, ctypes.POINTER(Params), U64, P, P]),
+        "pa_align_detail": (I32, [P, P, ctypes.POINTER(Params), P, P, P, P, P, U64, ctypes.POINTER(U64), P]),
+        "pa_align_batch": (I32, [P, P, P, P, U64, U64, ctypes.POINTER(Params), ctypes.POINTER(Stats), P, P, P, P]),
+        "pa_profile_enable": (I32, [P, I32]),
+        "pa_profile_read": (I32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(status: int) -> None:
+    if status == PA_OK:
+        return
+    msg = lib().pa_last_error().decode(errors="replace")
+    if status == PA_EINVAL:
+        raise ValueError(msg)
+    if status == PA_ETYPE:
+        raise TypeError(msg)
+    if status == PA_ENOMEM:
+        raise MemoryError(msg)
+    if status == PA_EDEVICE:
+        raise PaDeviceError(msg)
+    if status == PA_EUNSUPPORTED:
+        raise PaUnsupported(msg)
+    raise PaError(msg)
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+def device_count() -> int:
+    n = I32(0)
+    try:
+        _check(lib().pa_device_count(ctypes.byref(n)))
+    except PaDeviceError:
+        return 0
+    return int(n.value)
+
+
+def default_device() -> int:
+    return int(os.environ.get("PA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def concat(chunks: Sequence) -> Tuple[np.ndarray, np.ndarray]:
+    """Concatenate str/bytes/uint8 chunks into (uint8 array, uint64 CSR offsets)."""
+    bs = [c.encode() if isinstance(c, str) else (c.tobytes() if isinstance(c, np.ndarray) else bytes(c))
+          for c in chunks]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(bs), dtype=np.uint8) if bs else np.zeros(0, dtype=np.uint8)
+    return buf, off
+
+
+class Index:
+    """A device-resident k-mer index (pa_index)."""
+
+    def __init__(self, genomes: Sequence, k: int, device: Optional[int] = None, stream=None):
+        buf, off = concat(genomes)
+        self.device = default_device() if device is None else int(device)
+        self.k = int(k)
+        h = P()
+        kk = max(min(self.k, 2 ** 62), -2 ** 62)
+        _check(lib().pa_index_build(self.device, buf.ctypes.data_as(ctypes.c_char_p) if buf.size else None,
+                                    _ptr(off), len(off) - 1, kk, _stream(stream), ctypes.byref(h)))
+        self._h = h
+        self.n_genomes = len(off) - 1
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pa_index_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def info(self) -> IndexInfo:
+        inf = IndexInfo()
+        _check(lib().pa_index_get_info(self._h, ctypes.byref(inf)))
+        return inf
+
+    @property
+    def n_kmers(self) -> int:
+        return int(self.info().n_kmers)
+
+    def lookup(self, kmers: Sequence[str], stream=None) -> Tuple[np.ndarray, np.ndarray]:
+        n = len(kmers)
+        cls = np.zeros(n, dtype=np.int64)
+        size = np.zeros(n, dtype=np.uint32)
+        if n == 0:
+            return cls, size
+        lens = {len(x) for x in kmers}
+        if len(lens) != 1:
+            for i, km in enumerate(kmers):
+                c, s = self.lookup([km], stream)
+                cls[i], size[i] = c[0], s[0]
+            return cls, size
+        kl = lens.pop()
+        blob = "".join(kmers).encode("utf-8", errors="replace") if kl else b""
+        if len(blob) != n * kl:  # non-ASCII text cannot be a k-mer
+            return np.full(n, -1, dtype=np.int64), size
+        _check(lib().pa_index_lookup(self._h, blob, n, kl, _ptr(cls), _ptr(size), _stream(stream)))
+        return cls, size
+
+    def class_genomes(self, cls: int) -> list:
+        n = U32(0)
+        _check(lib().pa_index_class_genomes(self._h, int(cls), None, 0, ctypes.byref(n), None))
+        out = np.zeros(max(n.value, 1), dtype=np.uint32)
+        _check(lib().pa_index_class_genomes(self._h, int(cls), _ptr(out), out.size, ctypes.byref(n), None))
+        return [int(x) for x in out[:n.value]]
+
+    def extsim_stats(self, group_of: Sequence[int], n_groups: int):
+        g = np.ascontiguousarray(group_of, dtype=np.uint32)
+        total = np.zeros(n_groups, dtype=np.uint64)
+        uniq = np.zeros(n_groups, dtype=np.uint64)
+        inter = np.zeros(n_groups * n_groups, dtype=np.uint64)
+        _check(lib().pa_index_extsim_stats(self._h, _ptr(g), n_groups, _ptr(total), _ptr(uniq), _ptr(inter), None))
+        return total, uniq, inter.reshape(n_groups, n_groups)
+
+    def profile_enable(self, on: bool = True):
+        _check(lib().pa_profile_enable(self._h, 1 if on else 0))
+
+    def profile_read(self) -> Tuple[float, int, int]:
+        ms = ctypes.c_double(0)
+        nl = U64(0)
+        dr = U64(0)
+        _check(lib().pa_profile_read(self._h, ctypes.byref(ms), ctypes.byref(nl), ctypes.byref(dr)))
+        return float(ms.value), int(nl.value), int(dr.value)
+
+
+class Reads:
+    """A device-resident read batch (pa_reads)."""
+
+    def __init__(self, handle, device: int):
+        self._h = handle
+        self.device = device
+        n = U64(0)
+        nb = U64(0)
+        ml = U32(0)
+        _check(lib().pa_reads_info(self._h, ctypes.byref(n), ctypes.byref(nb), ctypes.byref(ml)))
+        self.n, self.n_bases, self.max_len = int(n.value), int(nb.value), int(ml.value)
+
+    @classmethod
+    def upload(cls, seq: np.ndarray, qual: np.ndarray, off: np.ndarray, device: Optional[int] = None,
+               stream=None) -> "Reads":
+        device = default_device() if device is None else int(device)
+        seq = np.ascontiguousarray(seq, dtype=np.uint8).reshape(-1)
+        qual = np.ascontiguousarray(qual, dtype=np.uint8).reshape(-1)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        h = P()
+        _check(lib().pa_reads_upload(device, _ptr(seq), _ptr(qual), _ptr(off), len(off) - 1, _stream(stream),
+                                     ctypes.byref(h)))
+        return cls(h, device)
+
+    @classmethod
+    def synthesize(cls, index: Index, n_reads: int, read_len: int, first_read: int = 0, seed: int = 2,
+                   sub_rate: float = 0.005, stream=None) -> "Reads":
+        h = P()
+        _check(lib().pa_reads_synthesize(index.handle, n_reads, read_len, first_read, seed, sub_rate, _stream(stream),
+                                         ctypes.byref(h)))
+        return cls(h, index.device)
+
+    def download(self, first: int = 0, count: Optional[int] = None):
+        count = self.n - first if count is None else count
+        off = np.zeros(count + 1, dtype=np.uint64)
+        _check(lib().pa_reads_download(self._h, first, count, None, None, _ptr(off), None))
+        nb = int(off[-1])
+        seq = np.zeros(max(nb, 1), dtype=np.uint8)
+        qual = np.zeros(max(nb, 1), dtype=np.uint8)
+        _check(lib().pa_reads_download(self._h, first, count, _ptr(seq), _ptr(qual), _ptr(off), None))
+        return seq[:nb], qual[:nb], off
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pa_reads_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+
+class Result:
+    """Device accumulators of PseudoAlignment counters (pa_result)."""
+
+    def __init__(self, index: Index):
+        h = P()
+        _check(lib().pa_result_create(index.handle, ctypes.byref(h)))
+        self._h = h
+        self.n_genomes = index.n_genomes
+
+    @property
+    def handle(self):
+        return self._h
+
+    def reset(self, stream=None):
+        _check(lib().pa_result_reset(self._h, _stream(stream)))
+
+    def fetch(self, stream=None):
+        st = Stats()
+        G = self.n_genomes
+        u = np.zeros(max(G, 1), dtype=np.uint64)
+        a = np.zeros(max(G, 1), dtype=np.uint64)
+        f = np.zeros(max(G, 1), dtype=np.uint64)
+        _check(lib().pa_result_fetch(self._h, ctypes.byref(st), _ptr(u), _ptr(a), _ptr(f), _stream(stream)))
+        stats = np.array([st.unique_mapped_reads, st.ambiguous_mapped_reads, st.unmapped_reads,
+                          st.filtered_quality_reads, st.filtered_quality_kmers, st.filtered_hr_kmers],
+                         dtype=np.uint64)
+        return stats, u[:G], a[:G], f[:G]
+
+    def device_view(self):
+        s = P()
+        ns = U64(0)
+        m = P()
+        nm = U64(0)
+        _check(lib().pa_result_device_view(self._h, ctypes.byref(s), ctypes.byref(ns), ctypes.byref(m),
+                                           ctypes.byref(nm)))
+        return int(s.value or 0), int(ns.value), int(m.value or 0), int(nm.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pa_result_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+
+def align(index: Index, reads: Reads, params: Params, read_index_base: int, result: Result, stream=None) -> None:
+    _check(lib().pa_align(index.handle, reads.handle, ctypes.byref(params), int(read_index_base), result.handle,
+                          _stream(stream)))
+
+
+def align_detail(index: Index, reads: Reads, params: Params, stream=None):
+    n = reads.n
+    types = np.zeros(max(n, 1), dtype=np.uint8)
+    qf = np.zeros(max(n, 1), dtype=np.uint32)
+    hr = np.zeros(max(n, 1), dtype=np.uint32)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    total = U64(0)
+    _check(lib().pa_align_detail(index.handle, reads.handle, ctypes.byref(params), _ptr(types), _ptr(qf), _ptr(hr),
+                                 _ptr(off), None, 0, ctypes.byref(total), _stream(stream)))
+    lists = np.zeros(max(int(total.value), 1), dtype=np.uint32)
+    if total.value:
+        _check(lib().pa_align_detail(index.handle, reads.handle, ctypes.byref(params), _ptr(types), _ptr(qf),
+                                     _ptr(hr), _ptr(off), _ptr(lists), lists.size, ctypes.byref(total),
+                                     _stream(stream)))
+    return types[:n], qf[:n], hr[:n], off, lists[:int(total.value)]

@@ -1,0 +1,191 @@
+/*
+ * pa.h -- C ABI of libpa.so, the MI355X (gfx950) pseudo-alignment engine.
+ *
+ * The reference (nyenyu12/BioInformatics-project-for-Shotgun-Metagenomics-
+ * Pseudo-alignment-shotgun-, pure Python) has no FFI; its boundary for this
+ * path is the Python API of src/kmer.py plus the dumpalign CLI.  Each entry
+ * point below replaces one piece of that API (file:line in the reference):
+ *
+ *   pa_index_build           KmerReference.__init__ / _build_kmer_mapping   src/kmer.py:113-150
+ *   pa_index_lookup          KmerReference.get_kmer_references / __getitem__ src/kmer.py:284-298
+ *   pa_index_class_genomes   (genome set of a k-mer, i.e. the keys of kmers[kmer]) src/kmer.py:130
+ *   pa_index_extsim_stats    KmerReference._compute_genome_stats + the pairwise
+ *                            intersections of _apply_greedy_filter          src/kmer.py:152-230
+ *   pa_align                 PseudoAlignment.align_reads_from_container ->
+ *                            Read.pseudo_align (counters only)              src/kmer.py:482-620
+ *   pa_align_detail          the same, with per-read mapping type and
+ *                            genomes_mapped_to (PseudoAlignment.reads)      src/kmer.py:542, 551-561
+ *   pa_result_fetch          PseudoAlignment.get_summary inputs             src/kmer.py:622-657
+ *   pa_align_batch           one-shot host-buffer form of pa_align
+ *
+ * Conventions
+ *   - Every function returns PA_OK (0) or an error code; pa_last_error()
+ *     gives a thread-local message.  The Python layer maps PA_EINVAL to
+ *     ValueError and PA_ETYPE to TypeError, like src/kmer.py:501-510.
+ *   - Buffers named seq/qual/genomes/read_off/... are HOST pointers; the
+ *     library copies them.  Objects (pa_index, pa_reads, pa_result) own DEVICE
+ *     memory on the device they were created on.
+ *   - `stream` is a hipStream_t (NULL = the legacy default stream).  All work is
+ *     stream-ordered; functions that return host data synchronize that stream.
+ *   - Calls on one pa_index are not thread-safe with respect to each other.
+ *   - Genome text must be uppercase ACGTN (the FASTA grammar,
+ *     src/records.py:225-233); reads may contain any byte, but only ACGT
+ *     windows can match (the FASTQ grammar restricts reads to ACGT,
+ *     src/records.py:258-265).
+ *   - Mapping types use the reference's enum values (src/kmer.py:41-47):
+ *     1 UNMAPPED, 2 UNIQUELY_MAPPED, 3 AMBIGUOUSLY_MAPPED; 0 marks a read
+ *     dropped by --min-read-quality (src/kmer.py:587-589: not in `reads`).
+ */
+#ifndef PA_H
+#define PA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t pa_status;
+#define PA_OK 0
+#define PA_EINVAL 1        /* bad argument value (ValueError) */
+#define PA_ETYPE 2         /* bad argument kind (TypeError) */
+#define PA_ENOMEM 3        /* host or device allocation failed */
+#define PA_EDEVICE 4       /* HIP runtime error */
+#define PA_EUNSUPPORTED 5  /* e.g. k > PA_MAX_K */
+#define PA_EINTERNAL 6     /* invariant violated (reported, never silent) */
+
+#define PA_MAX_K 159       /* k-mers up to 159 bases: keys of up to 5 x 64-bit words */
+
+#define PA_DROPPED 0
+#define PA_UNMAPPED 1
+#define PA_UNIQUELY_MAPPED 2
+#define PA_AMBIGUOUSLY_MAPPED 3
+
+/* pa_params.flags: which optional EXTQUALITY arguments are set (not None) */
+#define PA_HAS_MIN_READ_QUALITY 1u
+#define PA_HAS_MIN_KMER_QUALITY 2u
+#define PA_HAS_MAX_GENOMES 4u
+
+#define PA_NO_FIRST_KEY INT64_MAX  /* first_key of a genome never counted; all keys are < 2^63 */
+
+typedef struct pa_index pa_index;
+typedef struct pa_reads pa_reads;
+typedef struct pa_result pa_result;
+
+/* Arguments of Read.pseudo_align / align_reads_from_container (src/kmer.py:482-489, 600-606). */
+typedef struct {
+    int64_t m;                 /* unique threshold; < 0 -> PA_EINVAL (src/kmer.py:509-510) */
+    int64_t p;                 /* ambiguity threshold; < 0 skips validation (src/kmer.py:469) */
+    int64_t min_read_quality;  /* raw-ASCII mean, strict < (src/kmer.py:399, 587) */
+    int64_t min_kmer_quality;  /* raw-ASCII window mean, strict < (src/kmer.py:408, 420) */
+    int64_t max_genomes;       /* genomes per k-mer, strict > (src/kmer.py:425) */
+    uint32_t flags;            /* PA_HAS_* */
+    uint32_t reserved;
+} pa_params;
+
+/* "Statistics" of get_summary (src/kmer.py:627-637). */
+typedef struct {
+    uint64_t unique_mapped_reads;
+    uint64_t ambiguous_mapped_reads;
+    uint64_t unmapped_reads;
+    uint64_t filtered_quality_reads;
+    uint64_t filtered_quality_kmers;   /* windows, repeats included (quirk 4) */
+    uint64_t filtered_hr_kmers;        /* windows, repeats included (quirk 4) */
+} pa_stats;
+
+typedef struct {
+    uint32_t k;
+    uint32_t n_genomes;
+    uint32_t key_words;            /* 64-bit words per packed k-mer key */
+    uint32_t slot_bytes;
+    uint64_t n_kmers;              /* distinct k-mers (len(KmerReference.kmers)) */
+    uint64_t n_multi_classes;      /* distinct genome sets with >= 2 genomes */
+    uint64_t class_genome_entries;
+    uint64_t table_slots;
+    uint64_t table_bytes;
+    uint64_t total_windows;        /* genome windows scanned by the build */
+    uint64_t device_bytes;         /* all device memory held by the index */
+} pa_index_info;
+
+const char *pa_last_error(void);
+const char *pa_version(void);
+pa_status pa_device_count(int32_t *n);
+
+/* ---- index (KmerReference) ---------------------------------------------- */
+
+/* genomes: concatenated ASCII; genome_off: n_genomes+1 offsets (CSR). */
+pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *genome_off, uint32_t n_genomes,
+                         int64_t k, void *stream, pa_index **out);
+void pa_index_free(pa_index *idx);
+pa_status pa_index_get_info(const pa_index *idx, pa_index_info *out);
+/* n k-mers of length kmer_len packed back to back; cls_out[i] = class id or -1
+ * if absent; size_out[i] = number of genomes containing it (0 if absent). */
+pa_status pa_index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len,
+                          int64_t *cls_out, uint32_t *size_out, void *stream);
+/* genome indices (ascending = FASTA order) of class `cls`; *n = class size. */
+pa_status pa_index_class_genomes(const pa_index *idx, int64_t cls, uint32_t *genomes, uint32_t cap, uint32_t *n,
+                                 void *stream);
+/* EXTSIM inputs at identifier-group granularity (group_of[n_genomes]):
+ * total[a] = distinct k-mers touching group a, uniq[a] = k-mers contained in
+ * exactly one genome which belongs to a, inter[a*n_groups+b] = k-mers touching
+ * both groups a != b. */
+pa_status pa_index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint32_t n_groups, uint64_t *total,
+                                uint64_t *uniq, uint64_t *inter, void *stream);
+
+/* ---- reads ------------------------------------------------------------------ */
+
+pa_status pa_reads_upload(int32_t device, const uint8_t *seq, const uint8_t *qual, const uint64_t *read_off,
+                          uint64_t n_reads, void *stream, pa_reads **out);
+/* Synthetic fixed-length forward-strand reads sampled on the device from the
+ * index's genomes (read i = global read first_read + i; deterministic in seed). */
+pa_status pa_reads_synthesize(const pa_index *idx, uint64_t n_reads, uint32_t read_len, uint64_t first_read,
+                              uint64_t seed, double sub_rate, void *stream, pa_reads **out);
+pa_status pa_reads_info(const pa_reads *reads, uint64_t *n_reads, uint64_t *n_bases, uint32_t *max_len);
+/* copy reads [first, first+count) back to the host (seq/qual: n_bases of that range) */
+pa_status pa_reads_download(const pa_reads *reads, uint64_t first, uint64_t count, uint8_t *seq, uint8_t *qual,
+                            uint64_t *read_off, void *stream);
+void pa_reads_free(pa_reads *reads);
+
+/* ---- results (PseudoAlignment counters) ------------------------------------- */
+
+pa_status pa_result_create(const pa_index *idx, pa_result **out);
+pa_status pa_result_reset(pa_result *res, void *stream);
+/* any output pointer may be NULL; per-genome arrays hold n_genomes entries */
+pa_status pa_result_fetch(const pa_result *res, pa_stats *stats, uint64_t *unique_reads, uint64_t *ambiguous_reads,
+                          uint64_t *first_key, void *stream);
+/* Device views for collectives: sum block = [6 stats][G unique][G ambiguous]
+ * (reduce with SUM), min block = [G first_key] (reduce with MIN). */
+pa_status pa_result_device_view(pa_result *res, uint64_t **sum_block, uint64_t *n_sum, uint64_t **min_block,
+                                uint64_t *n_min);
+void pa_result_free(pa_result *res);
+
+/* ---- alignment ---------------------------------------------------------------- */
+
+/* Accumulates into `acc`.  read_index_base = global index of reads[0] (orders
+ * the Summary keys by first appearance, quirk 9). */
+pa_status pa_align(const pa_index *idx, const pa_reads *reads, const pa_params *params, uint64_t read_index_base,
+                   pa_result *acc, void *stream);
+/* Per-read results.  read_type[n], filtered_kmers[n], redundant_kmers[n],
+ * list_off[n+1] (host).  lists may be NULL to query *list_total first. */
+pa_status pa_align_detail(const pa_index *idx, const pa_reads *reads, const pa_params *params, uint8_t *read_type,
+                          uint32_t *filtered_kmers, uint32_t *redundant_kmers, uint64_t *list_off, uint32_t *lists,
+                          uint64_t list_cap, uint64_t *list_total, void *stream);
+/* upload + pa_align + fetch for host buffers (stats and per-genome arrays accumulate: +=, min) */
+pa_status pa_align_batch(const pa_index *idx, const uint8_t *seq, const uint8_t *qual, const uint64_t *read_off,
+                         uint64_t n_reads, uint64_t read_index_base, const pa_params *params, pa_stats *stats,
+                         uint64_t *unique_reads, uint64_t *ambiguous_reads, uint64_t *first_key, void *stream);
+
+/* ---- profiling ------------------------------------------------------------------ */
+
+/* When enabled, pa_align records HIP events around its main kernel on the
+ * stream it launches on; pa_profile_read synchronizes and returns the summed
+ * main-kernel milliseconds, launch count, and the reads that took the exact
+ * (deferred) path since the last read. */
+pa_status pa_profile_enable(pa_index *idx, int32_t enable);
+pa_status pa_profile_read(pa_index *idx, double *main_ms, uint64_t *launches, uint64_t *deferred_reads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PA_H */

@@ -182,6 +182,8 @@ class OracleIndex:
                                  _ptr(stats), _ptr(uq), _ptr(am), _ptr(fk))
         if rc == -2:
             raise MemoryError("oracle align allocation failed")
+        if detail:
+            lists = lists[:int(lo[-1])]
         return AlignResult(types, qf, hr, lo, lists, stats, uq, am, fk)
 
 

@@ -1,0 +1,328 @@
+"""GPU parity tests: libpa.so (HIP kernels) against the reference's golden
+vectors and against the CPU restatement (oracle/) on seeded synthetic data.
+
+Everything here calls through the C ABI (pa_native -> libpa.so) and needs an
+MI355X; bit-exact equality is required everywhere (integer work).
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import pa_native as N
+import pa_oracle as O
+import synth
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "bioinformatics-project-for-shotgun-metagenomics-pseudo-alignment-shotgun-_amd")
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+UNIT = load("unit_cases.json")
+TYPE = {0: "DROPPED", 1: "UNMAPPED", 2: "UNIQUELY_MAPPED", 3: "AMBIGUOUSLY_MAPPED"}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if N.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on an MI355X (no CPU fallback exists)")
+
+
+def reads_of(reads):
+    seq, off = N.concat([r[1] for r in reads])
+    qual, _ = N.concat([r[2] for r in reads])
+    return seq, qual, off
+
+
+def summary_from_counters(idents, stats, uq, am, fk, ps):
+    """get_summary from per-genome counters + first-appearance keys (as kmer.py does)."""
+    st = {"unique_mapped_reads": int(stats[0]), "ambiguous_mapped_reads": int(stats[1]),
+          "unmapped_reads": int(stats[2])}
+    if ps["mrq"] is not None:
+        st["filtered_quality_reads"] = int(stats[3])
+    if ps["mkq"] is not None:
+        st["filtered_quality_kmers"] = int(stats[4])
+    if ps["mg"] is not None:
+        st["filtered_hr_kmers"] = int(stats[5])
+    counts, first = {}, {}
+    for g in np.flatnonzero(fk != N.NO_FIRST_KEY):
+        name = idents[g]
+        c = counts.setdefault(name, [0, 0])
+        c[0] += int(uq[g])
+        c[1] += int(am[g])
+        first[name] = min(first.get(name, 1 << 64), int(fk[g]))
+    return {"Statistics": st, "Summary": {n: {"unique_reads": counts[n][0], "ambiguous_reads": counts[n][1]}
+                                          for n in sorted(first, key=first.get)}}
+
+
+@pytest.mark.parametrize("case", UNIT, ids=[c["name"] for c in UNIT])
+def test_golden_unit_cases(case):
+    """Per-read results (exact kernel) and summaries (fast + exact kernels) vs the reference."""
+    idents = [g[0] for g in case["genomes"]]
+    index = N.Index([g[1] for g in case["genomes"]], case["k"])
+    assert index.n_kmers == case["n_kmers"]
+    # index: the genome set of every k-mer
+    kms = [km for km, _ in case["kmer_sets"]]
+    if kms:
+        cls, size = index.lookup(kms)
+        for (km, gl), c, s in zip(case["kmer_sets"], cls, size):
+            assert c >= 0 and int(s) == len(gl), km
+            assert index.class_genomes(int(c)) == gl, km
+    seq, qual, off = reads_of(case["reads"])
+    reads = N.Reads.upload(seq, qual, off)
+    for res in case["results"]:
+        ps = res["params"]
+        prm = N.Params.make(ps["m"], ps["p"], ps["mrq"], ps["mkq"], ps["mg"])
+        types, qf, hr, loff, lists = N.align_detail(index, reads, prm)
+        for r, (rid, tname, glist, eqf, ehr) in enumerate(res["reads"]):
+            assert TYPE[int(types[r])] == tname, (rid, ps)
+            assert [idents[g] for g in lists[loff[r]:loff[r + 1]]] == glist, (rid, ps)
+            assert (int(qf[r]), int(hr[r])) == (eqf, ehr), (rid, ps)
+        result = N.Result(index)
+        N.align(index, reads, prm, 0, result)
+        stats, uq, am, fk = result.fetch()
+        summ = summary_from_counters(idents, stats, uq, am, fk, ps)
+        assert json.dumps(summ, indent=4) == res["summary_text"], ps
+
+
+def test_dropin_api_on_reference_fixtures():
+    """The reference's own test_kmer.py scenarios through the drop-in classes."""
+    from kmer import KmerReference, PseudoAlignment, Read, ReadMappingType
+    from records import FASTAQRecordContainer, FASTARecordContainer
+
+    def fa(text):
+        c = FASTARecordContainer()
+        c.parse_records(text)
+        return c
+
+    def fq(text):
+        c = FASTAQRecordContainer()
+        c.parse_records(text)
+        return c
+
+    ref = KmerReference(4, fa(">Genome1\nATGCCTTTTCGGGG\n>Genome2\nGCCGTTTTCGGGGCTA\n>Genome3\nCCGG\n"
+                              ">Genome4\nAAAAAAAAGGGCT\n>Genome5\nTTTTTTTTGCTAA\n"))
+    rec = list(fq("@Read4\nATGCCGGGGCTAA\n+\nIIIIIIIIIIIII\n"))[0]
+    assert Read(rec).pseudo_align(ref) == ReadMappingType.AMBIGUOUSLY_MAPPED
+    assert Read(rec).pseudo_align(ref, p=5) == ReadMappingType.UNIQUELY_MAPPED
+    r = Read(rec)
+    r.pseudo_align(ref)
+    assert [g.identifier for g in r.mapping.genomes_mapped_to] == ["Genome1", "Genome1", "Genome2"]
+    with pytest.raises(ValueError):
+        Read(rec).pseudo_align(ref, m=-1)
+    with pytest.raises(TypeError):
+        Read(rec).pseudo_align(ref, m=1.5)
+
+    sample = fa(">Genome1\nAGCTAGCTAGCTAGCTAGCT\n>Genome2\nTGCATGCATGCATGCATGCA\n"
+                ">Genome3\nAGCTTGCATGCAGCTAGCTA\n>Genome4\nCCGGAAGCTTGCATGCAGCTA\n")
+    kref = KmerReference(3, sample)
+    assert kref.get_kmer_references("AGC") and not kref.get_kmer_references("GGG")
+    assert kref.n_kmers == len(kref.kmers)
+    reads = fq("@Read1\nAGCTAGCT\n+\nIIIIIIII\n@Read2\nTGCATGCA\n+\n!!!!!!!!\n@Read3\nGGGGGGGG\n+\n!!IIIIII\n")
+    pa = PseudoAlignment(kref)
+    pa.align_reads_from_container(reads, min_read_quality=40, min_kmer_quality=50, max_genomes=2)
+    s = pa.get_summary()["Statistics"]
+    assert (s["filtered_quality_reads"], s["filtered_quality_kmers"], s["filtered_hr_kmers"]) == (1, 1, 5)
+    pa = PseudoAlignment(kref)
+    pa.align_reads_from_container(reads, min_read_quality=30, min_kmer_quality=30, max_genomes=3)
+    s = pa.get_summary()["Statistics"]
+    assert (s["unique_mapped_reads"], s["ambiguous_mapped_reads"], s["unmapped_reads"]) == (0, 2, 1)
+    assert set(pa.reads) == {"Read1", "Read2", "Read3"}
+    pa = PseudoAlignment(kref)
+    pa.align_reads_from_container(reads, min_read_quality=40)
+    assert "Read2" not in pa.reads  # dropped, not unmapped
+    from kmer import AddingExistingRead
+    with pytest.raises(AddingExistingRead):
+        pa.align_reads_from_container(reads)
+
+
+def test_config1_cli_stdout():
+    """BASELINE config 1 through the drop-in CLI: stdout identical to the reference's."""
+    for case in load("config1_cli.json"):
+        cmd = [sys.executable, os.path.join(PKG, "main.py"), "-t", "dumpalign", "-g",
+               os.path.join(GOLD, "config1.fa"), "-k", "21", "--reads", os.path.join(GOLD, "config1.fq")] + case["flags"]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout == case["stdout"], case["flags"]
+
+
+@pytest.mark.parametrize("case", load("extsim_cases.json"), ids=lambda c: c["name"])
+def test_extsim_golden(case):
+    from kmer import KmerReference, PseudoAlignment
+    from records import FASTAQRecordContainer, FASTARecordContainer
+    fa = FASTARecordContainer()
+    fa.parse_records("".join(f">{h}\n{s}\n" for h, s in case["genomes"]))
+    ref = KmerReference(case["k"], fa, filter_similar=True, similarity_threshold=case["threshold"])
+    assert json.dumps(ref.similarity_info, indent=4) == case["similarity_text"]
+    assert [g.identifier for g in ref.genomes] == case["kept"]
+    assert ref.n_kmers == case["n_kmers"]
+    fq = FASTAQRecordContainer()
+    fq.parse_records("".join(f"@{i}\n{s}\n+\n{q}\n" for i, s, q in case["reads"]))
+    pa = PseudoAlignment(ref)
+    pa.align_reads_from_container(fq)
+    assert json.dumps(pa.get_summary(), indent=4) == case["summary_text"]
+
+
+# ---------------------------------------------------------------------------
+# fast kernel vs the oracle on synthetic data
+# ---------------------------------------------------------------------------
+
+SYNTH = [
+    # (n_genomes, genome_len, family, sub, k, n_reads, read_len, err, param sets)
+    (12, 20000, 4, 0.02, 31, 6000, 150, 0.01, [dict(), dict(m=0, p=0), dict(p=-1), dict(m=3, p=4),
+                                                dict(mrq=58, mkq=59, mg=3), dict(mrq=20, mkq=25, mg=10),
+                                                dict(mg=1), dict(mg=0)]),
+    (6, 8000, 3, 0.03, 21, 4000, 100, 0.02, [dict(), dict(m=0, p=0), dict(mkq=60), dict(mg=2)]),
+    (8, 6000, 4, 0.05, 25, 3000, 60, 0.01, [dict(), dict(m=2, p=0)]),
+    (10, 9000, 5, 0.02, 31, 2000, 250, 0.01, [dict(), dict(m=0, p=0), dict(mkq=58)]),
+    (5, 7000, 5, 0.01, 32, 2000, 120, 0.01, [dict(), dict(m=0, p=0)]),  # 2-word keys, fast path
+    (5, 7000, 5, 0.01, 45, 1500, 150, 0.01, [dict(), dict(m=0, p=0)]),
+    (4, 5000, 2, 0.02, 64, 800, 150, 0.005, [dict(), dict(m=0, p=0)]),  # 3-word keys, exact path
+    (3, 4000, 1, 0.0, 17, 1500, 40, 0.02, [dict(), dict(mkq=55)]),
+    (70, 3000, 10, 0.01, 15, 3000, 80, 0.01, [dict(), dict(m=0, p=0)]),  # many genomes per class
+]
+
+
+def _synthetic_case(ng, glen, fam, sub, k, nr, rl, err, seed):
+    gens = synth.family_genomes(ng, glen, seed=seed, family_size=fam, sub_rate=sub,
+                                conserved_len=min(500, glen // 4), n_rate=2e-4, n_run=5)
+    seq, qual, _ = synth.sample_reads(gens, nr, rl, seed=seed + 1, err_rate=err)
+    # ragged tail: some shorter reads (and a few shorter than k)
+    lens = np.full(nr, rl, dtype=np.int64)
+    lens[::7] = np.maximum(1, rl - 1 - (np.arange(len(lens[::7])) % (rl - 1)))
+    off = np.zeros(nr + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    s = np.concatenate([seq[i, :lens[i]] for i in range(nr)])
+    q = np.concatenate([qual[i, :lens[i]] for i in range(nr)])
+    return gens, s, q, off
+
+
+@pytest.mark.parametrize("cfg", SYNTH, ids=[f"G{c[0]}_k{c[4]}_L{c[6]}" for c in SYNTH])
+def test_fast_kernel_vs_oracle(cfg):
+    ng, glen, fam, sub, k, nr, rl, err, psets = cfg
+    gens, s, q, off = _synthetic_case(ng, glen, fam, sub, k, nr, rl, err, seed=k * 101 + ng)
+    index = N.Index(gens, k)
+    oix = O.OracleIndex(gens, k)
+    assert index.n_kmers == oix.n_kmers
+    reads = N.Reads.upload(s, q, off)
+    idents = [f"g{i}" for i in range(ng)]
+    for ps in psets:
+        full = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None}
+        full.update(ps)
+        base = 12345
+        ores = oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"],
+                         mkq=full["mkq"], mg=full["mg"], read_base=base, detail=False)
+        prm = N.Params.make(full["m"], full["p"], full["mrq"], full["mkq"], full["mg"])
+        result = N.Result(index)
+        N.align(index, reads, prm, base, result)
+        stats, uq, am, fk = result.fetch()
+        assert stats.tolist() == ores.stats.tolist(), ps
+        assert uq.tolist() == ores.unique.tolist(), ps
+        assert am.tolist() == ores.ambiguous.tolist(), ps
+        ofk = np.where(ores.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, ores.first_key)
+        assert fk.tolist() == ofk.tolist(), ps
+        # summaries identical, key order included
+        assert summary_from_counters(idents, stats, uq, am, fk, full) == \
+            O.summary_by_walk(oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"],
+                                        mkq=full["mkq"], mg=full["mg"]), idents, full["mrq"], full["mkq"], full["mg"])
+
+
+def test_detail_kernel_vs_oracle_per_read():
+    gens, s, q, off = _synthetic_case(9, 6000, 3, 0.02, 27, 2500, 130, 0.01, seed=77)
+    index = N.Index(gens, 27)
+    oix = O.OracleIndex(gens, 27)
+    reads = N.Reads.upload(s, q, off)
+    for ps in (dict(m=1, p=1), dict(m=0, p=0, mrq=56, mkq=57, mg=4)):
+        prm = N.Params.make(ps.get("m", 1), ps.get("p", 1), ps.get("mrq"), ps.get("mkq"), ps.get("mg"))
+        types, qf, hr, loff, lists = N.align_detail(index, reads, prm)
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=ps.get("m", 1), p=ps.get("p", 1), mrq=ps.get("mrq"),
+                      mkq=ps.get("mkq"), mg=ps.get("mg"))
+        assert types.tolist() == o.types.tolist()
+        assert qf.tolist() == o.qf.tolist() and hr.tolist() == o.hr.tolist()
+        assert loff.tolist() == o.list_off.tolist()
+        assert lists.tolist() == o.lists.tolist()
+
+
+def test_batches_and_determinism():
+    """Two half batches == one batch; repeated runs identical."""
+    gens, s, q, off = _synthetic_case(8, 10000, 4, 0.02, 31, 4000, 150, 0.01, seed=5)
+    index = N.Index(gens, 31)
+    prm = N.Params.make(1, 1, None, None, None)
+    full = N.Result(index)
+    N.align(index, N.Reads.upload(s, q, off), prm, 0, full)
+    a = full.fetch()
+    N.align(index, N.Reads.upload(s, q, off), prm, 0, full)  # accumulate twice: counts double, keys same
+    b = full.fetch()
+    assert (b[0] == 2 * a[0]).all() and (b[1] == 2 * a[1]).all() and (b[3] == a[3]).all()
+    half = N.Result(index)
+    h = len(off) // 2
+    N.align(index, N.Reads.upload(s[:int(off[h])], q[:int(off[h])], off[:h + 1]), prm, 0, half)
+    N.align(index, N.Reads.upload(s[int(off[h]):], q[int(off[h]):], off[h:] - off[h]), prm, h, half)
+    c = half.fetch()
+    for x, y in zip(a, c):
+        assert x.tolist() == y.tolist()
+
+
+def test_synthesized_reads_parity():
+    """Device-synthesized reads (bench workload) against the oracle on the downloaded bytes."""
+    gens = synth.family_genomes(10, 30000, seed=3, family_size=5, sub_rate=0.01, conserved_len=1000)
+    index = N.Index(gens, 31)
+    reads = N.Reads.synthesize(index, 20000, 150, first_read=0, seed=2, sub_rate=0.005)
+    s, q, off = reads.download()
+    assert set(np.unique(s).tolist()) <= set(b"ACGT")
+    assert q.min() >= 35 and q.max() <= 74
+    oix = O.OracleIndex(gens, 31)
+    for ps in (dict(), dict(mrq=58, mkq=59, mg=3)):
+        full = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+        result = N.Result(index)
+        N.align(index, reads, N.Params.make(full["m"], full["p"], full["mrq"], full["mkq"], full["mg"]), 0, result)
+        stats, uq, am, fk = result.fetch()
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"], mkq=full["mkq"],
+                      mg=full["mg"], detail=False)
+        assert stats.tolist() == o.stats.tolist()
+        assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist()
+
+
+def test_edge_cases():
+    # k <= 0 and k longer than every genome: empty index, every read unmapped
+    for k in (0, -3, 50):
+        index = N.Index(["ACGTACGTAC", "GGGGCCCC"], k)
+        assert index.n_kmers == 0
+        s, off = N.concat(["ACGTACGT", "A"])
+        q, _ = N.concat(["IIIIIIII", "I"])
+        res = N.Result(index)
+        N.align(index, N.Reads.upload(s, q, off), N.Params.make(), 0, res)
+        assert res.fetch()[0].tolist() == [0, 0, 2, 0, 0, 0]
+    # k > PA_MAX_K fails loudly
+    with pytest.raises(N.PaUnsupported):
+        N.Index(["A" * 200], 160)
+    # invalid genome characters are rejected, like the FASTA grammar
+    with pytest.raises(ValueError):
+        N.Index(["ACGTX"], 3)
+    # m < 0 is a ValueError at the ABI too
+    index = N.Index(["ACGTACGT"], 3)
+    s, off = N.concat(["ACGT"])
+    with pytest.raises(ValueError):
+        N.align(index, N.Reads.upload(s, s, off), N.Params.make(m=-1), 0, N.Result(index))
+    # the largest supported k
+    g = synth.family_genomes(3, 2000, seed=9, family_size=3, sub_rate=0.01, conserved_len=0, n_rate=0)
+    index = N.Index(g, 159)
+    oix = O.OracleIndex(g, 159)
+    assert index.n_kmers == oix.n_kmers
+    seq, qual, _ = synth.sample_reads(g, 300, 170, seed=10, err_rate=0.002)
+    off = np.arange(301, dtype=np.uint64) * 170
+    res = N.Result(index)
+    N.align(index, N.Reads.upload(seq, qual, off), N.Params.make(), 0, res)
+    o = oix.align(seq.tobytes(), qual.tobytes(), off, detail=False)
+    assert res.fetch()[0].tolist() == o.stats.tolist()
