@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the MI355X pseudo-alignment engine.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3raw|c1]
+    torchrun --nproc-per-node N bench.py --gpus N ...            (one rank per GPU)
+
+Metric (BASELINE.json): reads/s pseudo-aligned, k=31, 150 bp reads, plus the
+achieved fraction of the HBM roofline.  Workload (SURVEY.md section 8d,
+config C2 = BASELINE.json configs[1]): 50 synthetic 2 Mbp genomes in families
+of 5 (1% substitutions within a family, a 5 kb segment shared by all, N runs),
+k=31, and per GPU 10M x 150 bp forward-strand reads with 0.5% substitution
+errors and raw-ASCII qualities, synthesized ON the device (they are resident in
+HBM before the timed region; nothing crosses PCIe while timing).
+
+A step = one pass of the align kernels over the rank's 10M reads (counters
+reset, pa_align, and for N > 1 the RCCL SUM/MIN all-reduce of the counter
+blocks).  Scaling is weak: every rank aligns its own 10M reads (global read
+indices rank*10M ...), and value = all ranks' reads / max-over-ranks time.
+
+roofline: algorithmic bytes per read B = L + q*L + (L-k+1)*16 (ASCII bases,
+qualities when a quality filter is on, one 8-B key + 8-B value slot per
+window) x reads per launch / the fast kernel's average
+duration, measured with HIP events recorded by libpa on the stream it launches
+on.  traffic: HBM bytes per launch from rocprofv3 PMC counters when a summary
+for this config is committed under profiles/ (else null).
+
+cpu_baseline (rank 0, N=1): the C restatement oracle/pa_oracle.c (single
+thread) timed on a bounded prefix of the same device-generated reads; the same
+prefix is aligned on the GPU and compared bit-for-bit.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "bioinformatics-project-for-shotgun-metagenomics-pseudo-alignment-shotgun-_amd")
+sys.path.insert(0, PKG)
+
+import pa_dist  # noqa: E402
+import pa_native as N  # noqa: E402
+import synth  # noqa: E402
+
+METRIC = "reads/sec pseudo-aligned (k=31, 150bp) at 1/2/4/8 GPUs; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+BASE = dict(n_genomes=50, genome_len=2_000_000, family=5, sub=0.01, conserved=5000, n_rate=1e-4, n_run=10, k=31,
+            reads_per_gpu=10_000_000, read_len=150, read_err=0.005, params={})
+CONFIGS = {
+    "c2": dict(BASE, name="C2: 50 x 2 Mbp synthetic genomes, 10M x 150 bp reads per GPU, k=31"),
+    "c3": dict(BASE, name="C3: C2 + --min-read-quality 20 --min-kmer-quality 25 --max-genomes 10",
+               params=dict(mrq=20, mkq=25, mg=10)),
+    "c3raw": dict(BASE, name="C3 raw-ASCII variant: C2 + --min-read-quality 53 --min-kmer-quality 58 "
+                             "--max-genomes 10", params=dict(mrq=53, mkq=58, mg=10)),
+    "c1": dict(BASE, n_genomes=3, genome_len=5000, family=3, sub=0.02, conserved=300, k=21, reads_per_gpu=1000,
+               read_len=100, read_err=0.01, name="C1: 3 x 5 kb genomes, 1k x 100 bp reads, k=21"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def bytes_per_read(cfg) -> int:
+    L, k = cfg["read_len"], cfg["k"]
+    q = 1 if (cfg["params"].get("mrq") is not None or cfg["params"].get("mkq") is not None) else 0
+    return L + q * L + (L - k + 1) * 16
+
+
+def traffic_from_profiles(config: str):
+    path = os.path.join(REPO, "profiles", f"traffic_{config}.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+def cpu_baseline(cfg, genomes, index, reads, prm_kw, target_s: float):
+    """Time the oracle on a prefix of the reads; check GPU == oracle on it."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pa_oracle as O
+    t0 = time.perf_counter()
+    oix = O.OracleIndex(genomes, cfg["k"])
+    build_s = time.perf_counter() - t0
+    kw = dict(m=prm_kw.get("m", 1), p=prm_kw.get("p", 1), mrq=prm_kw.get("mrq"), mkq=prm_kw.get("mkq"),
+              mg=prm_kw.get("mg"))
+    n = min(reads.n, 20000)
+    s, q, off = reads.download(0, n)
+    t0 = time.perf_counter()
+    oix.align(s.tobytes(), q.tobytes(), off, detail=False, **kw)
+    rate = n / max(time.perf_counter() - t0, 1e-9)
+    n = int(min(reads.n, max(n, rate * target_s), 4_000_000))
+    s, q, off = reads.download(0, n)
+    t0 = time.perf_counter()
+    o = oix.align(s.tobytes(), q.tobytes(), off, detail=False, **kw)
+    dt = time.perf_counter() - t0
+    # GPU on the same sample
+    sample = N.Reads.upload(s, q, off, device=index.device)
+    res = N.Result(index)
+    N.align(index, sample, N.Params.make(kw["m"], kw["p"], kw["mrq"], kw["mkq"], kw["mg"]), 0, res)
+    stats, uq, am, fk = res.fetch()
+    ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+    exact = (stats.tolist() == o.stats.tolist() and uq.tolist() == o.unique.tolist()
+             and am.tolist() == o.ambiguous.tolist() and fk.tolist() == ofk.tolist())
+    return ({"value": n / dt, "unit": "reads/s", "cores": 1, "kind": "port",
+             "sample": f"first {n} of the benchmark's device-generated reads, oracle/pa_oracle.c single thread "
+                       f"({dt:.1f} s; oracle index build {build_s:.1f} s not included)"},
+            {"reads": n, "bit_exact": bool(exact), "stats": [int(x) for x in stats]})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--reads-per-gpu", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.reads_per_gpu:
+        cfg["reads_per_gpu"] = args.reads_per_gpu
+
+    import torch
+    rank, world, local = pa_dist.init_process_group()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    t0 = time.perf_counter()
+    genomes = synth.family_genomes(cfg["n_genomes"], cfg["genome_len"], seed=1, family_size=cfg["family"],
+                                   sub_rate=cfg["sub"], conserved_len=cfg["conserved"], n_rate=cfg["n_rate"],
+                                   n_run=cfg["n_run"])
+    gen_s = time.perf_counter() - t0
+    stream = torch.cuda.current_stream(dev)
+    t0 = time.perf_counter()
+    index = N.Index(genomes, cfg["k"], device=local, stream=stream)
+    torch.cuda.synchronize(dev)
+    build_s = time.perf_counter() - t0
+    info = index.info()
+    npg = cfg["reads_per_gpu"]
+    reads = N.Reads.synthesize(index, npg, cfg["read_len"], first_read=rank * npg, seed=2, sub_rate=cfg["read_err"],
+                               stream=stream)
+    result = N.Result(index)
+    pk = cfg["params"]
+    prm = N.Params.make(pk.get("m", 1), pk.get("p", 1), pk.get("mrq"), pk.get("mkq"), pk.get("mg"))
+    log(f"[rank {rank}] genomes {gen_s:.1f}s, index build {build_s:.2f}s: {info.n_kmers} k-mers, "
+        f"{info.n_multi_classes} multi-genome sets, table {info.table_bytes / 2**30:.2f} GiB; {npg} reads")
+
+    def step():
+        result.reset(stream)
+        N.align(index, reads, prm, rank * npg, result, stream)
+        if world > 1:
+            pa_dist.reduce_result(result, dev, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    index.profile_read()  # drop warmup events
+    index.profile_enable(True)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms, launches, deferred = index.profile_read()
+    index.profile_enable(False)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    total_reads = world * npg * args.steps
+    value = total_reads / elapsed
+    kern_s = kern_ms / max(launches, 1) / 1e3
+    b_read = bytes_per_read(cfg)
+    achieved = b_read * npg / kern_s / 1e9 if kern_s > 0 else 0.0
+    traffic = traffic_from_profiles(args.config)
+    out = {
+        "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: seeded numpy genomes, reads sampled on the device (resident in HBM before timing)",
+        "config": {"workload": cfg["name"], "genomes": cfg["n_genomes"], "genome_len": cfg["genome_len"],
+                   "k": cfg["k"], "reads_per_gpu": npg, "read_len": cfg["read_len"],
+                   "filters": cfg["params"] or None, "parallelism": f"read-sharded x{world}, index replicated"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_align_fast", "kernel_ms": kern_s * 1e3, "bytes_per_read": b_read},
+        "deferred_read_fraction": deferred / max(npg * args.steps, 1),
+        "index": {"build_s": build_s, "n_kmers": int(info.n_kmers), "multi_genome_sets": int(info.n_multi_classes),
+                  "table_bytes": int(info.table_bytes)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        torch.cuda.synchronize(dev)
+        base, parity = cpu_baseline(cfg, genomes, index, reads, pk, args.cpu_seconds)
+        out["cpu_baseline"] = base
+        out["parity_sample"] = parity
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

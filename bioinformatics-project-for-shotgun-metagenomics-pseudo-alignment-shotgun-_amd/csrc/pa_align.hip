@@ -980,9 +980,25 @@ pa_status prepare_exact(pa_index *idx, const pa_reads *r, ExactArgs &x, unsigned
     return PA_OK;
 }
 
+__global__ void k_fill_first(unsigned long long *p, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = (unsigned long long)PA_NO_FIRST_KEY;
+}
+
 }  // namespace
 
 namespace pa {
+
+pa_status result_reset(pa_result *res, hipStream_t st) {
+    const uint64_t G = res->n_genomes;
+    PA_HIP(hipMemsetAsync(res->sum_block, 0, (6 + 2 * G) * 8, st));
+    if (G) {
+        hipLaunchKernelGGL(k_fill_first, dim3((unsigned)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           (unsigned long long *)res->min_block, G);
+        PA_HIP(hipGetLastError());
+    }
+    return PA_OK;
+}
 
 pa_status ensure_workspace(pa_index *idx, size_t bytes) {
     if (idx->ws.bytes >= bytes) return PA_OK;

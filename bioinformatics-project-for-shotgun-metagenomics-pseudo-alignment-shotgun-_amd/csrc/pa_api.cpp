@@ -306,6 +306,7 @@ pa_status pa_result_create(const pa_index *idx, pa_result **out) {
         return PA_ENOMEM;
     }
     pa_status rc = pa_result_reset(r, nullptr);
+    if (rc == PA_OK && hipStreamSynchronize(nullptr) != hipSuccess) rc = PA_EDEVICE;
     if (rc != PA_OK) {
         pa_result_free(r);
         return rc;
@@ -317,12 +318,26 @@ pa_status pa_result_create(const pa_index *idx, pa_result **out) {
 pa_status pa_result_reset(pa_result *res, void *stream) {
     PA_CHECK(res != nullptr, PA_EINVAL, "NULL argument");
     PA_HIP(hipSetDevice(res->device));
+    return pa::result_reset(res, as_stream(stream));  // async: memset + fill kernel
+}
+
+pa_status pa_result_copy_out(const pa_result *res, void *sum_dst, void *min_dst, void *stream) {
+    PA_CHECK(res != nullptr, PA_EINVAL, "NULL argument");
+    PA_HIP(hipSetDevice(res->device));
     hipStream_t st = as_stream(stream);
     const uint64_t G = res->n_genomes;
-    PA_HIP(hipMemsetAsync(res->sum_block, 0, (6 + 2 * G) * 8, st));
-    std::vector<uint64_t> none(std::max<uint64_t>(G, 1), (uint64_t)PA_NO_FIRST_KEY);
-    PA_HIP(hipMemcpyAsync(res->min_block, none.data(), none.size() * 8, hipMemcpyHostToDevice, st));
-    PA_HIP(hipStreamSynchronize(st));
+    if (sum_dst) PA_HIP(hipMemcpyAsync(sum_dst, res->sum_block, (6 + 2 * G) * 8, hipMemcpyDeviceToDevice, st));
+    if (min_dst && G) PA_HIP(hipMemcpyAsync(min_dst, res->min_block, G * 8, hipMemcpyDeviceToDevice, st));
+    return PA_OK;
+}
+
+pa_status pa_result_copy_in(pa_result *res, const void *sum_src, const void *min_src, void *stream) {
+    PA_CHECK(res != nullptr, PA_EINVAL, "NULL argument");
+    PA_HIP(hipSetDevice(res->device));
+    hipStream_t st = as_stream(stream);
+    const uint64_t G = res->n_genomes;
+    if (sum_src) PA_HIP(hipMemcpyAsync(res->sum_block, sum_src, (6 + 2 * G) * 8, hipMemcpyDeviceToDevice, st));
+    if (min_src && G) PA_HIP(hipMemcpyAsync(res->min_block, min_src, G * 8, hipMemcpyDeviceToDevice, st));
     return PA_OK;
 }
 

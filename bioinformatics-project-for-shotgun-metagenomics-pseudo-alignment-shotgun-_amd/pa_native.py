@@ -27,7 +27,8 @@ EXPORTS = (
     "pa_index_build", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
     "pa_index_extsim_stats",
     "pa_reads_upload", "pa_reads_synthesize", "pa_reads_info", "pa_reads_download", "pa_reads_free",
-    "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_free",
+    "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
+    "pa_result_copy_in", "pa_result_free",
     "pa_align", "pa_align_detail", "pa_align_batch",
     "pa_profile_enable", "pa_profile_read",
 )
@@ -110,6 +111,8 @@ def lib():
         "pa_result_reset": (I32, [P, P]),
         "pa_result_fetch": (I32, [P, ctypes.POINTER(Stats), P, P, P, P]),
         "pa_result_device_view": (I32, [P, PP, ctypes.POINTER(U64), PP, ctypes.POINTER(U64)]),
+        "pa_result_copy_out": (I32, [P, P, P, P]),
+        "pa_result_copy_in": (I32, [P, P, P, P]),
         "pa_result_free": (None, [P]),
         "pa_align": (I32, [P, P, ctypes.POINTER(Params), U64, P, P]),
         "pa_align_detail": (I32, [P, P, ctypes.POINTER(Params), P, P, P, P, P, U64, ctypes.POINTER(U64), P]),
@@ -347,6 +350,17 @@ class Result:
         _check(lib().pa_result_device_view(self._h, ctypes.byref(s), ctypes.byref(ns), ctypes.byref(m),
                                            ctypes.byref(nm)))
         return int(s.value or 0), int(ns.value), int(m.value or 0), int(nm.value)
+
+    @property
+    def n_sum(self) -> int:
+        return 6 + 2 * self.n_genomes
+
+    def copy_out(self, sum_dst_ptr: int, min_dst_ptr: int, stream=None) -> None:
+        """D2D copy of [stats|unique|ambiguous] and [first_key] into caller device buffers."""
+        _check(lib().pa_result_copy_out(self._h, sum_dst_ptr or None, min_dst_ptr or None, _stream(stream)))
+
+    def copy_in(self, sum_src_ptr: int, min_src_ptr: int, stream=None) -> None:
+        _check(lib().pa_result_copy_in(self._h, sum_src_ptr or None, min_src_ptr or None, _stream(stream)))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -157,6 +157,11 @@ pa_status pa_result_fetch(const pa_result *res, pa_stats *stats, uint64_t *uniqu
  * (reduce with SUM), min block = [G first_key] (reduce with MIN). */
 pa_status pa_result_device_view(pa_result *res, uint64_t **sum_block, uint64_t *n_sum, uint64_t **min_block,
                                 uint64_t *n_min);
+/* Stream-ordered device-to-device copies of the two blocks to / from caller
+ * device buffers (e.g. torch tensors reduced with RCCL); either pointer may be
+ * NULL.  Values fit int64: counts < 2^63, first keys < 2^63 (PA_NO_FIRST_KEY). */
+pa_status pa_result_copy_out(const pa_result *res, void *sum_dst, void *min_dst, void *stream);
+pa_status pa_result_copy_in(pa_result *res, const void *sum_src, const void *min_src, void *stream);
 void pa_result_free(pa_result *res);
 
 /* ---- alignment ---------------------------------------------------------------- */
