@@ -56,9 +56,7 @@ struct AlignArgs {
     uint64_t cap;
     uint32_t G;
     int k;
-    const uint64_t *class_off;
-    const uint32_t *class_size;
-    const uint32_t *class_genomes;
+    const uint32_t *class_genomes;  // multi-genome set records [size, genomes...], id = G + offset
     const uint8_t *seq;
     const uint8_t *qual;
     const uint64_t *off;
@@ -82,75 +80,6 @@ __device__ __forceinline__ uint64_t first_key(uint64_t read, uint32_t rank) { re
 // fast kernel
 // ---------------------------------------------------------------------------
 
-template <int WPL>
-struct FastCfg {
-    static constexpr int HS = 128 * WPL;        // LDS hash entries per wave (>= 2 x windows)
-    static constexpr int E = HS / 64;           // entries owned per lane
-    static constexpr int LCAP = 64 * WPL + 64;  // longest read (k <= 63)
-    static constexpr int PW = LCAP / 32 + 2;    // packed words
-    static constexpr int BW = LCAP / 64 + 2;    // poison bitmap words
-};
-
-template <int WPL>
-struct __align__(16) WaveLds {
-    using C = FastCfg<WPL>;
-    uint64_t packed[C::PW];
-    uint64_t poison[C::BW];
-    uint64_t hA_key[C::HS];   // dedup: table slot; p-check: genome id
-    uint64_t lst[C::HS];      // compaction scratch
-    uint32_t hA_v[C::HS];     // dedup: first window; p-check: total count
-    uint32_t hA_v2[C::HS];    // p-check: first window
-    uint32_t hB_key[C::HS];   // class id
-    uint32_t hB_cnt[C::HS];   // distinct k-mers of the class
-    uint32_t hB_min[C::HS];   // first window of the class
-    uint32_t pref[C::LCAP + 4];
-    uint32_t claims;
-};
-
-__device__ __forceinline__ uint32_t lds_hash_slot(uint64_t key, uint32_t mask) {
-    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & mask;
-}
-
-// Insert into an LDS open-addressing set of 64-bit keys; returns the entry.
-__device__ __forceinline__ uint32_t lds_insert64(uint64_t *keys, uint32_t hs, uint64_t key) {
-    uint32_t p = lds_hash_slot(key, hs - 1);
-    for (;;) {
-        uint64_t old = atomicCAS((unsigned long long *)&keys[p], (unsigned long long)EMPTY, (unsigned long long)key);
-        if (old == EMPTY || old == key) return p;
-        p = (p + 1) & (hs - 1);
-    }
-}
-
-__device__ __forceinline__ uint32_t lds_find64(const uint64_t *keys, uint32_t hs, uint64_t key) {
-    uint32_t p = lds_hash_slot(key, hs - 1);
-    while (keys[p] != key) p = (p + 1) & (hs - 1);
-    return p;
-}
-
-__device__ __forceinline__ uint32_t lds_insert32(uint32_t *keys, uint32_t hs, uint32_t key) {
-    uint32_t p = lds_hash_slot(key, hs - 1);
-    for (;;) {
-        uint32_t old = atomicCAS(&keys[p], NONE, key);
-        if (old == NONE || old == key) return p;
-        p = (p + 1) & (hs - 1);
-    }
-}
-
-// Bounded insert for the p-check genome hash; returns HS on overflow.
-__device__ __forceinline__ uint32_t lds_insert64_bounded(uint64_t *keys, uint32_t hs, uint64_t key, uint32_t *claims) {
-    uint32_t p = lds_hash_slot(key, hs - 1);
-    for (uint32_t it = 0; it < hs; it++) {
-        uint64_t old = atomicCAS((unsigned long long *)&keys[p], (unsigned long long)EMPTY, (unsigned long long)key);
-        if (old == EMPTY) {
-            atomicAdd(claims, 1u);
-            return p;
-        }
-        if (old == key) return p;
-        p = (p + 1) & (hs - 1);
-    }
-    return hs;
-}
-
 struct WgCounters {
     uint32_t *uniq;
     uint32_t *amb;
@@ -169,395 +98,8 @@ __device__ __forceinline__ void count_genome(const AlignArgs &a, const WgCounter
     }
 }
 
-template <int NW, int WPL>
-__global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
-    using C = FastCfg<WPL>;
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int lane = lane_id();
-    const int wid = threadIdx.x >> 6;
-    const uint32_t G = a.G;
-    const int k = a.k;
-    const uint64_t mask_hs = C::HS - 1;
-    (void)mask_hs;
+#include "pa_fast.h"
 
-    WgCounters wc;
-    wc.lds = G <= kLdsGenomeCap;
-    const uint32_t Gl = wc.lds ? ((G + 1) & ~1u) : 0;
-    wc.first = (unsigned long long *)smem;
-    wc.uniq = (uint32_t *)(wc.first + Gl);
-    wc.amb = wc.uniq + Gl;
-    WaveLds<WPL> *waves = (WaveLds<WPL> *)(smem + ((size_t)Gl * 16 + 15) / 16 * 16);
-    WaveLds<WPL> &L = waves[wid];
-    for (uint32_t i = threadIdx.x; i < Gl; i += kBlock) {
-        wc.first[i] = (unsigned long long)PA_NO_FIRST_KEY;
-        wc.uniq[i] = 0;
-        wc.amb[i] = 0;
-    }
-    __syncthreads();
-
-    const Slot<NW> *table = (const Slot<NW> *)a.table;
-    const bool has_mrq = a.prm.flags & F_MRQ, has_mkq = a.prm.flags & F_MKQ, has_mg = a.prm.flags & F_MG;
-    const bool need_q = has_mrq || has_mkq;
-    const int64_t mkq_k = (int64_t)a.prm.mkq * k;
-
-    uint32_t l_qf = 0, l_hr = 0;                     // per-lane window counters (committed reads only)
-    uint32_t w_unique = 0, w_amb = 0, w_unm = 0, w_drop = 0;  // lane 0 only
-
-    for (uint64_t r = (uint64_t)blockIdx.x * kWaves + wid; r < a.n; r += (uint64_t)gridDim.x * kWaves) {
-        const uint64_t off = a.off[r];
-        const uint32_t len = (uint32_t)(a.off[r + 1] - off);
-        const uint32_t W = (len >= (uint32_t)k) ? len - k + 1 : 0;
-        if (W > 64u * WPL || len > (uint32_t)(C::LCAP - 2)) {
-            if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;
-            continue;
-        }
-        // ---- raw-ASCII quality prefix sums (src/kmer.py:399, 408)
-        if (need_q) {
-            uint32_t carry = 0;
-            for (uint32_t c0 = 0; c0 < len; c0 += 64) {
-                uint32_t i = c0 + lane;
-                uint32_t q = i < len ? (uint32_t)a.qual[off + i] : 0u;
-                uint32_t s = wave_incl_scan(q) + carry;
-                L.pref[i + 1] = s;
-                carry = __shfl(s, 63);
-            }
-            if (lane == 0) L.pref[0] = 0;
-            wave_sync();
-            if (has_mrq && (int64_t)L.pref[len] < (int64_t)a.prm.mrq * (int64_t)len) {
-                if (lane == 0) w_drop++;  // dropped, not unmapped (src/kmer.py:587-589)
-                continue;
-            }
-        }
-        // ---- 2-bit pack + non-ACGT bitmap
-        for (uint32_t c0 = 0; c0 < len; c0 += 64) {
-            uint32_t i = c0 + lane;
-            uint32_t code = i < len ? base_code(a.seq[off + i]) : 0u;
-            uint64_t bad = __ballot(code > 3);
-            uint64_t v = (uint64_t)(code & 3) << (62 - 2 * (lane & 31));
-            v = half_or64(v);
-            if ((lane & 31) == 0) L.packed[c0 / 32 + (lane >> 5)] = v;
-            if (lane == 0) L.poison[c0 / 64] = bad;
-        }
-        if (lane < 2) {
-            uint32_t nc = (len + 63) / 64;
-            L.packed[nc * 2 + lane] = 0;
-            if (lane == 0) L.poison[nc] = 0;
-        }
-        // clear the dedup / class hashes
-#pragma unroll
-        for (int e = 0; e < C::E; e++) {
-            const int i = lane + 64 * e;
-            L.hA_key[i] = EMPTY;
-            L.hA_v[i] = NONE;
-            L.hB_key[i] = NONE;
-            L.hB_cnt[i] = 0;
-            L.hB_min[i] = NONE;
-        }
-        wave_sync();
-        // ---- windows: quality gate, key, probe (src/kmer.py:419-429)
-        Key<NW> key[WPL];
-        uint64_t hsh[WPL], pos[WPL], slot[WPL];
-        uint32_t cls[WPL], csz[WPL];
-        bool pend[WPL], inc[WPL];
-        uint32_t qf = 0, hr = 0;
-#pragma unroll
-        for (int j = 0; j < WPL; j++) {
-            const uint32_t w = lane + 64 * j;
-            bool ok = w < W;
-            if (ok && has_mkq) {
-                uint32_t s = L.pref[w + k] - L.pref[w];
-                if ((int64_t)s < mkq_k) {
-                    qf++;
-                    ok = false;
-                }
-            }
-            if (ok) ok = window_bits(L.poison, w, k) == 0;
-            pend[j] = ok;
-            inc[j] = false;
-            if (ok) {
-                key[j] = extract_key<NW>(L.packed, w, k);
-                hsh[j] = key_hash(key[j]);
-                pos[j] = home_slot(hsh[j], a.cap);
-            }
-        }
-        // batched linear probing: all pending probes of the lane in flight together
-        for (;;) {
-            bool any = false;
-#pragma unroll
-            for (int j = 0; j < WPL; j++) any |= pend[j];
-            if (!__ballot(any)) break;
-            Slot<NW> s[WPL];
-#pragma unroll
-            for (int j = 0; j < WPL; j++)
-                if (pend[j]) s[j] = table[pos[j]];
-#pragma unroll
-            for (int j = 0; j < WPL; j++) {
-                if (!pend[j]) continue;
-                if (s[j].key[0] == EMPTY) {
-                    pend[j] = false;
-                    continue;
-                }
-                bool eq = true;
-#pragma unroll
-                for (int t = 0; t < NW; t++) eq &= (s[j].key[t] == key[j].w[t]);
-                if (eq) {
-                    pend[j] = false;
-                    slot[j] = pos[j];
-                    cls[j] = s[j].cls;
-                    csz[j] = s[j].csize;
-                    if (has_mg && (int64_t)csz[j] > (int64_t)a.prm.mg)
-                        hr++;  // highly redundant k-mer (src/kmer.py:425-427)
-                    else
-                        inc[j] = true;
-                } else {
-                    pos[j] = (pos[j] + 1 == a.cap) ? 0 : pos[j] + 1;
-                }
-            }
-        }
-        bool any_inc = false;
-#pragma unroll
-        for (int j = 0; j < WPL; j++) any_inc |= inc[j];
-        if (!__ballot(any_inc)) {
-            l_qf += qf;
-            l_hr += hr;
-            if (lane == 0) w_unm++;  // no k-mer references -> UNMAPPED (src/kmer.py:516-517)
-            continue;
-        }
-        // ---- distinct k-mers: first window per table slot (quirk 3)
-        uint32_t hp[WPL];
-#pragma unroll
-        for (int j = 0; j < WPL; j++)
-            if (inc[j]) {
-                hp[j] = lds_insert64(L.hA_key, C::HS, slot[j]);
-                atomicMin(&L.hA_v[hp[j]], (uint32_t)(lane + 64 * j));
-            }
-        wave_sync();
-        // ---- group distinct k-mers by genome set
-#pragma unroll
-        for (int j = 0; j < WPL; j++)
-            if (inc[j] && L.hA_v[hp[j]] == (uint32_t)(lane + 64 * j)) {
-                uint32_t p = lds_insert32(L.hB_key, C::HS, cls[j]);
-                atomicAdd(&L.hB_cnt[p], 1u);
-                atomicMin(&L.hB_min[p], (uint32_t)(lane + 64 * j));
-            }
-        wave_sync();
-        // ---- specific counts: singleton classes (src/kmer.py:431-462)
-        uint32_t nspec_l = 0, nmulti_l = 0;
-        uint64_t top_l = 0;
-#pragma unroll
-        for (int e = 0; e < C::E; e++) {
-            const int i = lane + 64 * e;
-            uint32_t c = L.hB_key[i];
-            if (c == NONE) continue;
-            if (c < G) {
-                nspec_l++;
-                uint64_t t = ((uint64_t)L.hB_cnt[i] << 48) | ((uint64_t)(0xFFFFu - L.hB_min[i]) << 32) | c;
-                top_l = t > top_l ? t : top_l;
-            } else {
-                nmulti_l++;
-            }
-        }
-        const uint32_t nspec = wave_sum(nspec_l);
-        const uint32_t nmulti = wave_sum(nmulti_l);
-        const uint64_t read_idx = a.base + r;
-        l_qf += qf;  // from here on the read is committed by this kernel unless deferred below
-        l_hr += hr;
-        if (nspec == 0) {
-            if (lane == 0) w_amb++;  // AMBIGUOUS with an empty genome list
-            continue;
-        }
-        const uint64_t top = wave_max64(top_l);
-        const uint32_t gstar = (uint32_t)top, topcnt = (uint32_t)(top >> 48);
-        uint32_t sec_l = 0;
-#pragma unroll
-        for (int e = 0; e < C::E; e++) {
-            const int i = lane + 64 * e;
-            uint32_t c = L.hB_key[i];
-            if (c != NONE && c < G && c != gstar) sec_l = max(sec_l, L.hB_cnt[i]);
-        }
-        const uint32_t second = wave_max(sec_l);
-        const bool unique = nspec == 1 || (int64_t)topcnt >= (int64_t)second + a.prm.m;
-        if (!unique) {
-            // AMBIGUOUS: every specific genome, in first-insertion order
-            uint32_t mine = 0;
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                uint32_t c = L.hB_key[lane + 64 * e];
-                mine += (c != NONE && c < G);
-            }
-            uint32_t at = wave_excl_scan(mine);
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                const int i = lane + 64 * e;
-                uint32_t c = L.hB_key[i];
-                if (c != NONE && c < G) L.lst[at++] = ((uint64_t)L.hB_min[i] << 32) | c;
-            }
-            wave_sync();
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                const int i = lane + 64 * e;
-                uint32_t c = L.hB_key[i];
-                if (c == NONE || c >= G) continue;
-                uint64_t me = ((uint64_t)L.hB_min[i] << 32) | c;
-                uint32_t rank = 0;
-                for (uint32_t t = 0; t < nspec; t++) rank += L.lst[t] < me;
-                count_genome(a, wc, c, false, 1, first_key(read_idx, rank));
-            }
-            if (lane == 0) w_amb++;
-            continue;
-        }
-        if (a.prm.p < 0 || nmulti == 0) {
-            // UNIQUE; with only specific k-mers the p-check cannot demote
-            if (lane == 0) {
-                count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
-                w_unique++;
-            }
-            continue;
-        }
-        // ---- p-validation (src/kmer.py:464-480): total counts over all genomes
-        wave_sync();
-#pragma unroll
-        for (int e = 0; e < C::E; e++) {
-            const int i = lane + 64 * e;
-            L.hA_key[i] = EMPTY;
-            L.hA_v[i] = 0;
-            L.hA_v2[i] = NONE;
-        }
-        if (lane == 0) L.claims = 0;
-        // compact the multi classes into lst: (class << 32 | cnt << 16 | first window)
-        {
-            uint32_t mine = 0;
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                uint32_t c = L.hB_key[lane + 64 * e];
-                mine += (c != NONE && c >= G);
-            }
-            uint32_t at = wave_excl_scan(mine);
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                const int i = lane + 64 * e;
-                uint32_t c = L.hB_key[i];
-                if (c != NONE && c >= G)
-                    L.lst[at++] = ((uint64_t)c << 32) | ((uint64_t)L.hB_cnt[i] << 16) | L.hB_min[i];
-            }
-        }
-        wave_sync();
-        bool ovf = false;
-        const uint32_t limit = (C::HS * 3) / 4;
-#pragma unroll
-        for (int e = 0; e < C::E; e++) {
-            const int i = lane + 64 * e;
-            uint32_t c = L.hB_key[i];
-            if (c != NONE && c < G) {
-                uint32_t p = lds_insert64_bounded(L.hA_key, C::HS, c, &L.claims);
-                if (p >= (uint32_t)C::HS) {
-                    ovf = true;
-                } else {
-                    atomicAdd(&L.hA_v[p], L.hB_cnt[i]);
-                    atomicMin(&L.hA_v2[p], L.hB_min[i]);
-                }
-            }
-        }
-        for (uint32_t t = 0; t < nmulti; t++) {
-            const uint64_t ent = L.lst[t];
-            const uint32_t c = (uint32_t)(ent >> 32) - G;
-            const uint32_t cnt = (uint32_t)(ent >> 16) & 0xFFFFu, mw = (uint32_t)ent & 0xFFFFu;
-            const uint32_t sz = a.class_size[c];
-            if (sz > limit) {
-                ovf = true;
-                break;
-            }
-            const uint32_t *gl = a.class_genomes + a.class_off[c];
-            for (uint32_t j = lane; j < sz; j += 64) {
-                uint32_t g = gl[j];
-                uint32_t p = lds_insert64_bounded(L.hA_key, C::HS, g, &L.claims);
-                if (p >= (uint32_t)C::HS) {
-                    ovf = true;
-                } else {
-                    atomicAdd(&L.hA_v[p], cnt);
-                    atomicMin(&L.hA_v2[p], mw);
-                }
-            }
-            wave_sync();
-            if (L.claims > limit) break;
-        }
-        wave_sync();
-        if (__ballot(ovf) || L.claims > limit) {
-            // genome union too large for the wave's LDS: exact kernel takes over
-            l_qf -= qf;
-            l_hr -= hr;
-            if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;
-            continue;
-        }
-        uint32_t ts_l = 0, mx_l = 0;
-#pragma unroll
-        for (int e = 0; e < C::E; e++) {
-            const int i = lane + 64 * e;
-            uint64_t g = L.hA_key[i];
-            if (g == EMPTY) continue;
-            mx_l = max(mx_l, L.hA_v[i]);
-            if (g == gstar) ts_l = L.hA_v[i];
-        }
-        const uint32_t tstar = wave_max(ts_l), maxtot = wave_max(mx_l);
-        if ((int64_t)maxtot - (int64_t)tstar > a.prm.p) {
-            // demoted: [G*] + every genome with total >= total[G*], first-appearance order
-            uint32_t mine = 0;
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                const int i = lane + 64 * e;
-                mine += (L.hA_key[i] != EMPTY && L.hA_v[i] >= tstar);
-            }
-            uint32_t at = wave_excl_scan(mine);
-            const uint32_t nq = wave_sum(mine);
-            wave_sync();
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                const int i = lane + 64 * e;
-                if (L.hA_key[i] != EMPTY && L.hA_v[i] >= tstar)
-                    L.lst[at++] = ((uint64_t)L.hA_v2[i] << 32) | (uint32_t)L.hA_key[i];
-            }
-            wave_sync();
-#pragma unroll
-            for (int e = 0; e < C::E; e++) {
-                const int i = lane + 64 * e;
-                if (L.hA_key[i] == EMPTY || L.hA_v[i] < tstar) continue;
-                const uint32_t g = (uint32_t)L.hA_key[i];
-                if (g == gstar) {
-                    count_genome(a, wc, g, false, 2, first_key(read_idx, 0));
-                } else {
-                    uint64_t me = ((uint64_t)L.hA_v2[i] << 32) | g;
-                    uint32_t rank = 1;
-                    for (uint32_t t = 0; t < nq; t++) rank += L.lst[t] < me;
-                    count_genome(a, wc, g, false, 1, first_key(read_idx, rank));
-                }
-            }
-            if (lane == 0) w_amb++;
-        } else {
-            if (lane == 0) {
-                count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
-                w_unique++;
-            }
-        }
-    }
-    // ---- flush
-    const uint32_t qf_w = wave_sum(l_qf), hr_w = wave_sum(l_hr);
-    if (lane == 0) {
-        if (w_unique) atomicAdd(&a.stats[0], (unsigned long long)w_unique);
-        if (w_amb) atomicAdd(&a.stats[1], (unsigned long long)w_amb);
-        if (w_unm) atomicAdd(&a.stats[2], (unsigned long long)w_unm);
-        if (w_drop) atomicAdd(&a.stats[3], (unsigned long long)w_drop);
-        if (qf_w && has_mkq) atomicAdd(&a.stats[4], (unsigned long long)qf_w);
-        if (hr_w && has_mg) atomicAdd(&a.stats[5], (unsigned long long)hr_w);
-    }
-    if (wc.lds) {
-        __syncthreads();
-        for (uint32_t g = threadIdx.x; g < G; g += kBlock) {
-            if (wc.uniq[g]) atomicAdd(&a.uniq[g], (unsigned long long)wc.uniq[g]);
-            if (wc.amb[g]) atomicAdd(&a.amb[g], (unsigned long long)wc.amb[g]);
-            if (wc.first[g] != (unsigned long long)PA_NO_FIRST_KEY) atomicMin(&a.first[g], wc.first[g]);
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // exact kernel (one workgroup per read, dense per-genome scratch)
@@ -753,8 +295,9 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
                     gl = &single;
                     sz = 1;
                 } else {
-                    gl = a.class_genomes + a.class_off[c - G];
-                    sz = a.class_size[c - G];
+                    const uint32_t *rec = a.class_genomes + (c - G);  // [size, genomes...]
+                    gl = rec + 1;
+                    sz = rec[0];
                 }
                 for (uint32_t j = 0; j < sz; j++) {
                     const uint32_t g = gl[j];
@@ -892,14 +435,9 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
 // host side
 // ---------------------------------------------------------------------------
 
-template <int WPL>
-constexpr size_t wave_lds_bytes() {
-    return sizeof(WaveLds<WPL>);
-}
-
-size_t fast_lds_bytes(uint32_t G, int wpl) {
+size_t fast_lds_bytes(uint32_t G, int wpl, bool need_q) {
     size_t cnt = G <= kLdsGenomeCap ? (((size_t)((G + 1) & ~1u) * 16 + 15) / 16 * 16) : 0;
-    size_t wl = wpl == 1 ? wave_lds_bytes<1>() : wpl == 2 ? wave_lds_bytes<2>() : wave_lds_bytes<4>();
+    size_t wl = wpl == 1 ? fast_wave_bytes<1>(need_q) : wpl == 2 ? fast_wave_bytes<2>(need_q) : fast_wave_bytes<4>(need_q);
     return cnt + kWaves * wl;
 }
 
@@ -922,7 +460,7 @@ pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
 
 template <int NW>
 pa_status launch_fast_wpl(const AlignArgs &a, int wpl, hipStream_t st) {
-    size_t shm = fast_lds_bytes(a.G, wpl);
+    size_t shm = fast_lds_bytes(a.G, wpl, (a.prm.flags & (F_MRQ | F_MKQ)) != 0);
     switch (wpl) {
         case 1: return launch_fast<NW, 1>(a, shm, st);
         case 2: return launch_fast<NW, 2>(a, shm, st);
@@ -953,8 +491,6 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.cap = idx->cap;
     a.G = idx->n_genomes;
     a.k = (int)std::max<int64_t>(idx->k, 0);
-    a.class_off = idx->class_off;
-    a.class_size = idx->class_size;
     a.class_genomes = idx->class_genomes;
     a.seq = r->seq;
     a.qual = r->qual;

@@ -152,23 +152,24 @@ pa_status pa_index_lookup(const pa_index *idx, const char *kmers, uint64_t n, ui
 pa_status pa_index_class_genomes(const pa_index *idx, int64_t cls, uint32_t *genomes, uint32_t cap, uint32_t *n,
                                  void *stream) {
     PA_CHECK(idx && n, PA_EINVAL, "NULL argument");
-    PA_CHECK(cls >= 0 && (uint64_t)cls < (uint64_t)idx->n_genomes + idx->n_multi, PA_EINVAL, "class id out of range");
+    PA_CHECK(cls >= 0 && (uint64_t)cls < (uint64_t)idx->n_genomes + idx->class_entries, PA_EINVAL,
+             "class id out of range");
     if ((uint64_t)cls < idx->n_genomes) {
         *n = 1;
         if (genomes && cap >= 1) genomes[0] = (uint32_t)cls;
         return PA_OK;
     }
+    // multi-genome class: id = G + word offset of its [size, genomes...] record
     PA_HIP(hipSetDevice(idx->device));
-    const uint64_t c = (uint64_t)cls - idx->n_genomes;
+    const uint64_t rec = (uint64_t)cls - idx->n_genomes;
     uint32_t size = 0;
-    uint64_t off = 0;
     hipStream_t st = as_stream(stream);
-    PA_HIP(hipMemcpyAsync(&size, idx->class_size + c, 4, hipMemcpyDeviceToHost, st));
-    PA_HIP(hipMemcpyAsync(&off, idx->class_off + c, 8, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipMemcpyAsync(&size, idx->class_genomes + rec, 4, hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
+    PA_CHECK(rec + 1 + size <= idx->class_entries, PA_EINVAL, "not a class id");
     *n = size;
     if (genomes && cap > 0) {
-        PA_HIP(hipMemcpyAsync(genomes, idx->class_genomes + off, (uint64_t)std::min(cap, size) * 4,
+        PA_HIP(hipMemcpyAsync(genomes, idx->class_genomes + rec + 1, (uint64_t)std::min(cap, size) * 4,
                               hipMemcpyDeviceToHost, st));
         PA_HIP(hipStreamSynchronize(st));
     }
@@ -212,8 +213,8 @@ pa_status pa_reads_upload(int32_t device, const uint8_t *seq, const uint8_t *qua
         return e == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;
     };
     hipError_t e;
-    if ((e = hipMalloc(&r->seq, std::max<uint64_t>(nb, 1))) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&r->qual, std::max<uint64_t>(nb, 1))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&r->seq, nb + pa::kReadPad)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&r->qual, nb + pa::kReadPad)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&r->off, (n_reads + 1) * 8)) != hipSuccess) return fail(e);
     if (nb) {
         if ((e = hipMemcpyAsync(r->seq, seq + read_off[0], nb, hipMemcpyHostToDevice, st)) != hipSuccess) return fail(e);

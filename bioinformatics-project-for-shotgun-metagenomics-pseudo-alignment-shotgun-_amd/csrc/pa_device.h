@@ -137,6 +137,12 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    uint32_t lo = __shfl((unsigned)(uint32_t)v, src);
+    uint32_t hi = __shfl((unsigned)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);

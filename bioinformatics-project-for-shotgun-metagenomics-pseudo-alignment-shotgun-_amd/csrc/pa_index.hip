@@ -7,11 +7,11 @@
 //                  load factor <= 0.5 (cap = 2 x genome windows).
 //   classes        the genome SET of a k-mer (the keys of kmers[kmer] in the
 //                  reference) is a "class": cls < G means the singleton {cls};
-//                  cls >= G indexes a deduplicated multi-genome set whose
-//                  ascending genome list lives in class_genomes[class_off[c]..]
-//                  with class_size[c] entries.  csize caches the set size in
-//                  the slot so --max-genomes and the specific/unspecific test
-//                  need no second memory access.
+//                  cls >= G is a deduplicated multi-genome set stored as the
+//                  record class_genomes[cls - G] = [size, ascending genomes...]
+//                  (one contiguous read in the align kernels).  csize caches
+//                  the set size in the slot so --max-genomes and the
+//                  specific/unspecific test need no second memory access.
 //
 // Build pipeline (all stream-ordered, one host sync at the end)
 //   1. ASCII -> 2-bit codes (4 = anything else, e.g. 'N').
@@ -150,19 +150,30 @@ __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstar
 template <int NW>
 __global__ void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg, uint32_t *aux,
                              uint64_t *off, unsigned long long *bump, unsigned long long *n_multi) {
-    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (; s < cap; s += stride) {
-        if (table[s].key[0] == EMPTY) continue;
-        uint32_t d = deg[s];
-        if (d == 1) {
-            table[s].cls = aux[s];
-            table[s].csize = 1;
-        } else {
-            off[s] = atomicAdd(bump, (unsigned long long)d);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int lane = lane_id();
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < cap; base += stride) {  // uniform trip count
+        const uint64_t s = base + threadIdx.x;
+        uint32_t d = 0;
+        if (s < cap && table[s].key[0] != EMPTY) {
+            d = deg[s];
+            if (d == 1) {
+                table[s].cls = aux[s];
+                table[s].csize = 1;
+                d = 0;
+            }
+        }
+        // one bump allocation per wave (a single global counter would serialise ~10^7 atomics)
+        const uint32_t incl = wave_incl_scan(d);
+        const uint64_t multi = __ballot(d >= 2);
+        uint64_t wbase = 0;
+        if (lane == 63 && incl) wbase = atomicAdd(bump, (unsigned long long)incl);
+        wbase = shfl64(wbase, 63);
+        if (lane == 0 && multi) atomicAdd(n_multi, (unsigned long long)__popcll(multi));
+        if (d >= 2) {
+            off[s] = wbase + incl - d;
             aux[s] = 0;
             table[s].csize = d;
-            atomicAdd(n_multi, 1ull);
         }
     }
 }
@@ -244,7 +255,7 @@ __global__ void k_class_number(const uint64_t *cs_key, const uint64_t *cs_rep, u
         uint32_t d = deg[rep];
         cs_id[e] = (uint32_t)id;
         class_size[id] = d;
-        class_off[id] = atomicAdd(bump, (unsigned long long)d);
+        class_off[id] = atomicAdd(bump, (unsigned long long)d + 1);  // record = [size, genomes...]
         rep_of[id] = rep;
     }
 }
@@ -256,14 +267,16 @@ __global__ void k_class_copy(uint64_t n_cls, const uint64_t *rep_of, const uint3
     for (; c < n_cls; c += gridDim.x) {
         const uint32_t *src = lists + off[rep_of[c]];
         uint32_t *dst = class_genomes + class_off[c];
-        for (uint32_t i = threadIdx.x; i < class_size[c]; i += blockDim.x) dst[i] = src[i];
+        if (threadIdx.x == 0) dst[0] = class_size[c];
+        for (uint32_t i = threadIdx.x; i < class_size[c]; i += blockDim.x) dst[1 + i] = src[i];
     }
 }
 
 template <int NW>
 __global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint32_t *deg, const uint64_t *off,
                                const uint32_t *lists, const uint64_t *cs_key, const uint64_t *cs_rep,
-                               const uint32_t *cs_id, uint64_t cs_cap, uint32_t n_genomes, uint32_t *err) {
+                               const uint32_t *cs_id, uint64_t cs_cap, const uint64_t *class_off,
+                               uint32_t n_genomes, uint32_t *err) {
     uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; s < cap; s += stride) {
@@ -278,7 +291,8 @@ __global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint32_t *de
         const uint32_t *rl = lists + off[rep];
         for (uint32_t i = 0; same && i < d; i++) same = (rl[i] == l[i]);
         if (!same) atomicOr(err, 2u);  // 63-bit list-hash collision: refuse, never merge
-        table[s].cls = n_genomes + cs_id[pos];
+        // a multi-genome class id is G + the word offset of its [size, genomes...] record
+        table[s].cls = n_genomes + (uint32_t)class_off[cs_id[pos]];
     }
 }
 
@@ -333,7 +347,7 @@ __global__ void k_extsim_slots(const Slot<NW> *table, uint64_t cap, uint32_t n_g
                 atomicAdd(&uniq[a], 1ull);
             }
         } else {
-            atomicAdd(&class_count[c - n_genomes], 1ull);
+            atomicAdd(&class_count[c - n_genomes], 1ull);  // indexed by record offset
         }
     }
     if (use_lds) {
@@ -353,10 +367,10 @@ __global__ void k_extsim_classes(uint64_t n_cls, const uint64_t *class_off, cons
                                  unsigned long long *inter, uint32_t *scratch, uint64_t scratch_stride) {
     __shared__ uint32_t n_distinct;
     for (uint64_t c = blockIdx.x; c < n_cls; c += gridDim.x) {
-        unsigned long long nc = class_count[c];
+        unsigned long long nc = class_count[class_off[c]];
         if (nc == 0) continue;
         uint32_t sz = class_size[c];
-        const uint32_t *gl = class_genomes + class_off[c];
+        const uint32_t *gl = class_genomes + class_off[c] + 1;
         uint32_t *grp = scratch + blockIdx.x * scratch_stride;
         if (threadIdx.x == 0) n_distinct = 0;
         __syncthreads();
@@ -510,7 +524,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         B_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
         B_HIP(hipStreamSynchronize(st));
         const uint64_t n_cls = h_cnt[3], entries = h_cnt[4];
-        if ((uint64_t)G + n_cls >= 0xFFFFFFFFull) {
+        if ((uint64_t)G + entries >= 0xFFFFFFFFull) {
             pa::set_error("index build: too many distinct genome sets for 32-bit class ids");
             cleanup();
             return PA_EUNSUPPORTED;
@@ -519,7 +533,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         hipLaunchKernelGGL(k_class_copy, dim3((unsigned)std::min<uint64_t>(n_cls, 65536)), dim3(kBlock), 0, st, n_cls,
                            rep_of, idx->class_size, idx->class_off, off, lists, idx->class_genomes);
         hipLaunchKernelGGL(k_class_assign<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists, cs_key,
-                           cs_rep, cs_id, cs_cap, G, err);
+                           cs_rep, cs_id, cs_cap, idx->class_off, G, err);
         B_HIP(hipGetLastError());
         B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
         B_HIP(hipStreamSynchronize(st));
@@ -672,18 +686,19 @@ pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint
     uint32_t *d_group = nullptr, *scratch = nullptr;
     unsigned long long *d_tot = nullptr, *d_uniq = nullptr, *d_inter = nullptr, *d_cc = nullptr;
     const uint64_t nm = std::max<uint64_t>(idx->n_multi, 1);
+    const uint64_t n_rec = std::max<uint64_t>(idx->class_entries, 1);
     const unsigned cgrid = (unsigned)std::min<uint64_t>(nm, 1024);
     PA_HIP(hipMalloc(&d_group, (uint64_t)idx->n_genomes * 4));
     PA_HIP(hipMalloc(&d_tot, n_groups * 8));
     PA_HIP(hipMalloc(&d_uniq, n_groups * 8));
     PA_HIP(hipMalloc(&d_inter, ng2 * 8));
-    PA_HIP(hipMalloc(&d_cc, nm * 8));
+    PA_HIP(hipMalloc(&d_cc, n_rec * 8));
     PA_HIP(hipMalloc(&scratch, (uint64_t)cgrid * (idx->n_genomes + 1) * 4));
     PA_HIP(hipMemcpyAsync(d_group, group_of, (uint64_t)idx->n_genomes * 4, hipMemcpyHostToDevice, st));
     PA_HIP(hipMemsetAsync(d_tot, 0, n_groups * 8, st));
     PA_HIP(hipMemsetAsync(d_uniq, 0, n_groups * 8, st));
     PA_HIP(hipMemsetAsync(d_inter, 0, ng2 * 8, st));
-    PA_HIP(hipMemsetAsync(d_cc, 0, nm * 8, st));
+    PA_HIP(hipMemsetAsync(d_cc, 0, n_rec * 8, st));
     switch (idx->nw) {
         case 1: extsim_slots_nw<1>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
         case 2: extsim_slots_nw<2>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
@@ -718,8 +733,8 @@ pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_
     r->n_bases = n * len;
     r->max_len = len;
     uint32_t *d_elig = nullptr;
-    PA_HIP(hipMalloc(&r->seq, std::max<uint64_t>(r->n_bases, 1)));
-    PA_HIP(hipMalloc(&r->qual, std::max<uint64_t>(r->n_bases, 1)));
+    PA_HIP(hipMalloc(&r->seq, r->n_bases + kReadPad));
+    PA_HIP(hipMalloc(&r->qual, r->n_bases + kReadPad));
     PA_HIP(hipMalloc(&r->off, (n + 1) * 8));
     PA_HIP(hipMalloc(&d_elig, elig.size() * 4));
     PA_HIP(hipMemcpyAsync(d_elig, elig.data(), elig.size() * 4, hipMemcpyHostToDevice, st));

@@ -35,6 +35,9 @@ void set_error(const std::string &msg);
 inline int key_words(int64_t k) { return (int)(k / 32) + 1; }
 // Bytes per hash-table slot: key words + {uint32 class, uint32 class size}.
 inline int slot_bytes(int nw) { return 8 * nw + 8; }
+// Read buffers are over-allocated so a wave may fetch a whole staging window
+// (up to 512 B) past any read start without a bounds check.
+constexpr uint64_t kReadPad = 1024;
 
 // Device arguments of the per-read kernels (clamped, see pa_api.cpp).
 struct DevParams {
