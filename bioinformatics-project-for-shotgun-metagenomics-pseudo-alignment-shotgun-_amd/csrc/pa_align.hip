@@ -54,9 +54,11 @@ enum : uint32_t { F_MRQ = 1, F_MKQ = 2, F_MG = 4 };
 struct AlignArgs {
     const void *table;
     uint64_t cap;
+    HomeCfg home;
     uint32_t G;
     int k;
     const uint32_t *class_genomes;  // multi-genome set records [size, genomes...], id = G + offset
+    const uint64_t *class_mask;     // G <= 64: membership mask of each record (same offsets)
     const uint8_t *seq;
     const uint8_t *qual;
     const uint64_t *off;
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
             if (!clean) continue;
             uint64_t slot;
             uint32_t cls, csize;
-            if (!table_find<NW>(table, a.cap, key, key_hash(key), slot, cls, csize)) continue;
+            if (!table_find<NW>(table, a.cap, key, home_of(key, key_hash(key), a.home), slot, cls, csize)) continue;
             if (has_mg && (int64_t)csize > (int64_t)a.prm.mg) {
                 hr++;
                 continue;
@@ -441,9 +443,9 @@ size_t fast_lds_bytes(uint32_t G, int wpl, bool need_q) {
     return cnt + kWaves * wl;
 }
 
-template <int NW, int WPL>
+template <int NW, int WPL, bool DENSE>
 pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
-    auto kern = k_align_fast<NW, WPL>;
+    auto kern = k_align_fast<NW, WPL, DENSE>;
     if (shm > 64 * 1024) PA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     int per_cu = 0;
     PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, shm));
@@ -461,10 +463,11 @@ pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
 template <int NW>
 pa_status launch_fast_wpl(const AlignArgs &a, int wpl, hipStream_t st) {
     size_t shm = fast_lds_bytes(a.G, wpl, (a.prm.flags & (F_MRQ | F_MKQ)) != 0);
+    const bool dense = a.G <= 64;  // membership masks exist (k_class_masks)
     switch (wpl) {
-        case 1: return launch_fast<NW, 1>(a, shm, st);
-        case 2: return launch_fast<NW, 2>(a, shm, st);
-        default: return launch_fast<NW, 4>(a, shm, st);
+        case 1: return dense ? launch_fast<NW, 1, true>(a, shm, st) : launch_fast<NW, 1, false>(a, shm, st);
+        case 2: return dense ? launch_fast<NW, 2, true>(a, shm, st) : launch_fast<NW, 2, false>(a, shm, st);
+        default: return dense ? launch_fast<NW, 4, true>(a, shm, st) : launch_fast<NW, 4, false>(a, shm, st);
     }
 }
 
@@ -489,9 +492,11 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     AlignArgs a{};
     a.table = idx->table;
     a.cap = idx->cap;
+    a.home = idx->home;
     a.G = idx->n_genomes;
     a.k = (int)std::max<int64_t>(idx->k, 0);
     a.class_genomes = idx->class_genomes;
+    a.class_mask = idx->class_mask;
     a.seq = r->seq;
     a.qual = r->qual;
     a.off = r->off;

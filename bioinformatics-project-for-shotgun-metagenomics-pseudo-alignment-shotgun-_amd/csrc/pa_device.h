@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pa_home.h"
+
 namespace pad {
 
 constexpr uint64_t EMPTY = ~0ull;        // empty slot (top key word)
@@ -96,11 +98,47 @@ __device__ __forceinline__ uint64_t window_bits(const uint64_t *bm, uint32_t w, 
     return v & ((1ull << k) - 1);
 }
 
-// Read-only probe (tables are immutable once built).
+// Where a key starts probing.  With m > 0 (k <= 31), the home slot lies in a
+// region of R slots chosen by the key's MINIMIZER -- the m-mer of the k-mer with
+// the smallest hash -- and the key's own hash picks the slot inside the region.
+// Consecutive windows of a read share their minimizer most of the time (a
+// "super-k-mer"), so their probes land in the same few cache lines and one wave
+// load instruction coalesces them into a handful of HBM requests.  Any key's
+// home is a pure function of the key, so build and lookup agree exactly.
+// (HomeCfg: pa_home.h)
+
+__device__ __forceinline__ uint32_t mmer_hash(uint32_t x) {
+    x *= 0x9E3779B1u;
+    x ^= x >> 15;
+    x *= 0x85EBCA77u;
+    x ^= x >> 13;
+    return x;
+}
+
+// Minimizer hash of a single-word k-mer key (m <= 16).
+__device__ __forceinline__ uint32_t minimizer_hash(uint64_t K, int k, int m) {
+    const uint32_t mask = m >= 16 ? 0xFFFFFFFFu : ((1u << (2 * m)) - 1);
+    uint32_t best = 0xFFFFFFFFu;
+    for (int sh = 2 * (k - m); sh >= 0; sh -= 2) best = min(best, mmer_hash((uint32_t)(K >> sh) & mask));
+    return best;
+}
+
 template <int NW>
-__device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint64_t cap, const Key<NW> &k, uint64_t h,
-                                           uint64_t &slot, uint32_t &cls, uint32_t &csize) {
-    uint64_t pos = home_slot(h, cap);
+__device__ __forceinline__ uint64_t home_of(const Key<NW> &key, uint64_t h, const HomeCfg &c) {
+    if constexpr (NW == 1) {
+        if (c.m > 0) {
+            const uint32_t mh = mmer_hash(minimizer_hash(key.w[0], c.k, c.m) ^ 0x5BD1E995u);
+            return (((uint64_t)mh * c.nreg) >> 32) * c.R + (h & (c.R - 1));
+        }
+    }
+    return home_slot(h, c.cap);
+}
+
+// Read-only probe from a home slot (tables are immutable once built).
+template <int NW>
+__device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint64_t cap, const Key<NW> &k,
+                                           uint64_t home, uint64_t &slot, uint32_t &cls, uint32_t &csize) {
+    uint64_t pos = home;
     for (;;) {
         const Slot<NW> s = t[pos];
         if (s.key[0] == EMPTY) return false;
@@ -143,37 +181,70 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Wave reductions on DPP (VALU lane moves; no LDS round trips).  row_shr 1/2/4/8
+// leave each 16-lane row's total in its lane 15, row_bcast 15/31 carry row
+// totals up to lane 63, which readlane broadcasts.  Callers must have all 64
+// lanes active (every call site is in wave-uniform control flow).
+#define PA_DPP(old, v, ctrl, rmask) __builtin_amdgcn_update_dpp((old), (v), (ctrl), (rmask), 0xf, false)
+#define PA_DPP_STEPS(OP, IDENT, v)                          \
+    v = OP(v, (uint32_t)PA_DPP(IDENT, (int)v, 0x111, 0xf)); \
+    v = OP(v, (uint32_t)PA_DPP(IDENT, (int)v, 0x112, 0xf)); \
+    v = OP(v, (uint32_t)PA_DPP(IDENT, (int)v, 0x114, 0xf)); \
+    v = OP(v, (uint32_t)PA_DPP(IDENT, (int)v, 0x118, 0xf)); \
+    v = OP(v, (uint32_t)PA_DPP(IDENT, (int)v, 0x142, 0xa)); \
+    v = OP(v, (uint32_t)PA_DPP(IDENT, (int)v, 0x143, 0xc));
+
+__device__ __forceinline__ uint32_t op_add(uint32_t a, uint32_t b) { return a + b; }
+__device__ __forceinline__ uint32_t op_max(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-    return v;
+    PA_DPP_STEPS(op_add, 0, v);
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor(v, m));
-    return v;
+    PA_DPP_STEPS(op_max, 0, v);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ uint64_t dpp64(uint64_t v, int ctrl_sel) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    switch (ctrl_sel) {  // constant-folded: the DPP control must be an immediate
+        case 0: lo = PA_DPP(0, (int)lo, 0x111, 0xf); hi = PA_DPP(0, (int)hi, 0x111, 0xf); break;
+        case 1: lo = PA_DPP(0, (int)lo, 0x112, 0xf); hi = PA_DPP(0, (int)hi, 0x112, 0xf); break;
+        case 2: lo = PA_DPP(0, (int)lo, 0x114, 0xf); hi = PA_DPP(0, (int)hi, 0x114, 0xf); break;
+        case 3: lo = PA_DPP(0, (int)lo, 0x118, 0xf); hi = PA_DPP(0, (int)hi, 0x118, 0xf); break;
+        case 4: lo = PA_DPP(0, (int)lo, 0x142, 0xa); hi = PA_DPP(0, (int)hi, 0x142, 0xa); break;
+        default: lo = PA_DPP(0, (int)lo, 0x143, 0xc); hi = PA_DPP(0, (int)hi, 0x143, 0xc); break;
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+    uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+    uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint64_t o = shfl_xor64(v, m);
+    for (int s = 0; s < 6; s++) {
+        const uint64_t o = dpp64(v, s);
         v = o > v ? o : v;
     }
-    return v;
+    return readlane64(v, 63);
 }
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor64(v, m);
-    return v;
+    for (int s = 0; s < 6; s++) v += dpp64(v, s);
+    return readlane64(v, 63);
 }
 
-// OR across each 32-lane half of the wave.
+// OR across each 32-lane half of the wave; the result is valid in lanes 31 and 63.
 __device__ __forceinline__ uint64_t half_or64(uint64_t v) {
 #pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) v |= shfl_xor64(v, m);
+    for (int s = 0; s < 5; s++) v |= dpp64(v, s);
     return v;
 }
 

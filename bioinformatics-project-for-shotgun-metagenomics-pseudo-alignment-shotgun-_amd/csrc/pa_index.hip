@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -61,9 +63,9 @@ __global__ void k_fill_u64(uint64_t *p, uint64_t n, uint64_t v) {
 // Insert (or find) a key; returns its slot.  Slots only go EMPTY -> key, so a
 // stale plain load can only show EMPTY, which the CAS then corrects.
 template <int NW>
-__device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, uint64_t h,
+__device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, uint64_t home,
                                  unsigned long long *n_kmers, uint32_t *err) {
-    uint64_t pos = home_slot(h, cap);
+    uint64_t pos = home;
     if constexpr (NW == 1) {
         for (uint64_t it = 0; it < cap; it++) {
             uint64_t cur = t[pos].key[0];
@@ -116,8 +118,9 @@ __device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, ui
 // Pass 1 over one genome: insert windows, count distinct genomes per slot.
 template <int NW>
 __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
-                               uint64_t mask0, uint32_t g, Slot<NW> *table, uint64_t cap, uint32_t *deg,
+                               uint64_t mask0, uint32_t g, Slot<NW> *table, HomeCfg hc, uint32_t *deg,
                                uint32_t *last_g, uint32_t *first_g, unsigned long long *n_kmers, uint32_t *err) {
+    const uint64_t cap = hc.cap;
     uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
     if (w0 >= nwin) return;
     uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
@@ -136,7 +139,7 @@ __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstar
         run = c > 3 ? 0 : run + 1;
         key_push(key, c & 3, mask0);
         if (run < k) continue;  // window contains a non-ACGT base (src/kmer.py:145)
-        uint64_t slot = table_insert<NW>(table, cap, key, key_hash(key), n_kmers, err);
+        uint64_t slot = table_insert<NW>(table, cap, key, home_of(key, key_hash(key), hc), n_kmers, err);
         if (slot == ~0ull) return;
         uint32_t old = atomicMax(&last_g[slot], g + 1);
         if (old < g + 1) {
@@ -181,8 +184,9 @@ __global__ void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg,
 // Pass 2 over one genome: append g to the genome list of every multi slot.
 template <int NW>
 __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
-                             uint64_t mask0, uint32_t g, const Slot<NW> *table, uint64_t cap, const uint32_t *deg,
+                             uint64_t mask0, uint32_t g, const Slot<NW> *table, HomeCfg hc, const uint32_t *deg,
                              uint32_t *last_g, uint32_t *fill, const uint64_t *off, uint32_t *lists) {
+    const uint64_t cap = hc.cap;
     uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
     if (w0 >= nwin) return;
     uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
@@ -203,7 +207,7 @@ __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart,
         if (run < k) continue;
         uint64_t slot;
         uint32_t cls, csize;
-        if (!table_find<NW>(table, cap, key, key_hash(key), slot, cls, csize)) continue;  // cannot happen
+        if (!table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, csize)) continue;
         if (deg[slot] < 2) continue;
         uint32_t old = atomicMax(&last_g[slot], g + 1);
         if (old < g + 1) {
@@ -272,6 +276,18 @@ __global__ void k_class_copy(uint64_t n_cls, const uint64_t *rep_of, const uint3
     }
 }
 
+// G <= 64: one 64-bit membership mask per multi-genome set (dense align path).
+__global__ void k_class_masks(uint64_t n_cls, const uint64_t *class_off, const uint32_t *class_genomes,
+                              uint64_t *class_mask) {
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; c < n_cls; c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t *rec = class_genomes + class_off[c];
+        uint64_t m = 0;
+        for (uint32_t i = 0; i < rec[0]; i++) m |= 1ull << rec[1 + i];
+        class_mask[class_off[c]] = m;
+    }
+}
+
 template <int NW>
 __global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint32_t *deg, const uint64_t *off,
                                const uint32_t *lists, const uint64_t *cs_key, const uint64_t *cs_rep,
@@ -297,8 +313,9 @@ __global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint32_t *de
 }
 
 template <int NW>
-__global__ void k_lookup(const Slot<NW> *table, uint64_t cap, const uint8_t *kmers, uint64_t n, int k, uint64_t mask0,
+__global__ void k_lookup(const Slot<NW> *table, HomeCfg hc, const uint8_t *kmers, uint64_t n, int k, uint64_t mask0,
                          int64_t *cls_out, uint32_t *size_out) {
+    const uint64_t cap = hc.cap;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t *s = kmers + i * (uint64_t)k;
@@ -313,7 +330,7 @@ __global__ void k_lookup(const Slot<NW> *table, uint64_t cap, const uint8_t *kme
     }
     uint64_t slot;
     uint32_t cls = 0, csize = 0;
-    if (ok && table_find<NW>(table, cap, key, key_hash(key), slot, cls, csize)) {
+    if (ok && table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, csize)) {
         cls_out[i] = cls;
         size_out[i] = csize;
     } else {
@@ -473,7 +490,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         if (k <= 0 || (uint64_t)k > len) continue;
         uint64_t nwin = len - k + 1;
         hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
-                           idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, cap, deg, last_g, aux, cnt + 0, err);
+                           idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, deg, last_g, aux, cnt + 0,
+                           err);
     }
     B_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_build_prep<NW>, dim3(grid_for(cap, kBlock) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0,
@@ -500,8 +518,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             if ((uint64_t)k > len) continue;
             uint64_t nwin = len - k + 1;
             hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
-                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, cap, deg, last_g, aux, off,
-                               lists);
+                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, deg, last_g, aux,
+                               off, lists);
         }
         B_HIP(hipGetLastError());
         uint64_t cs_cap = 2 * n_multi + 64;
@@ -532,6 +550,11 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         B_HIP(hipMalloc(&idx->class_genomes, std::max<uint64_t>(entries, 1) * 4));
         hipLaunchKernelGGL(k_class_copy, dim3((unsigned)std::min<uint64_t>(n_cls, 65536)), dim3(kBlock), 0, st, n_cls,
                            rep_of, idx->class_size, idx->class_off, off, lists, idx->class_genomes);
+        if (G <= 64) {
+            B_HIP(hipMalloc(&idx->class_mask, std::max<uint64_t>(entries, 1) * 8));
+            hipLaunchKernelGGL(k_class_masks, dim3((unsigned)std::min<uint64_t>((n_cls + kBlock - 1) / kBlock, 4096)),
+                               dim3(kBlock), 0, st, n_cls, idx->class_off, idx->class_genomes, idx->class_mask);
+        }
         hipLaunchKernelGGL(k_class_assign<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists, cs_key,
                            cs_rep, cs_id, cs_cap, idx->class_off, G, err);
         B_HIP(hipGetLastError());
@@ -557,7 +580,7 @@ pa_status lookup_nw(const pa_index *idx, const uint8_t *d_kmers, uint64_t n, int
                     hipStream_t st) {
     const int k = (int)idx->k;
     const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
-    hipLaunchKernelGGL(k_lookup<NW>, dim3(grid_for(n)), dim3(kBlock), 0, st, (const Slot<NW> *)idx->table, idx->cap,
+    hipLaunchKernelGGL(k_lookup<NW>, dim3(grid_for(n)), dim3(kBlock), 0, st, (const Slot<NW> *)idx->table, idx->home,
                        d_kmers, n, k, mask0, d_cls, d_size);
     PA_HIP(hipGetLastError());
     return PA_OK;
@@ -582,6 +605,7 @@ void index_release(pa_index *idx) {
     hipFree(idx->class_off);
     hipFree(idx->class_size);
     hipFree(idx->class_genomes);
+    hipFree(idx->class_mask);
     hipFree(idx->codes);
     hipFree(idx->goff);
     hipFree(idx->ws.ptr);
@@ -606,7 +630,27 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     }
     for (auto &o : idx->h_goff) o -= goff[0];
     idx->total_windows = windows;
-    idx->cap = std::max<uint64_t>(64, 2 * windows + 64);
+    // Home slots: plain hashing by default.  PA_MINIMIZER_M=m (single-word keys)
+    // places keys in R-slot regions chosen by their minimizer instead; measured
+    // on C2 it is 1.7-3x SLOWER (regions that collect several minimizers
+    // overflow into long linear-probing chains, and a wave waits for its
+    // slowest lane), so it stays an experiment.
+    int m = 0;
+    uint32_t R = 1;
+    if (std::getenv("PA_MINIMIZER_M") && k >= 20 && idx->nw == 1) {
+        R = 32;
+        if (const char *e = std::getenv("PA_MINIMIZER_M")) m = std::atoi(e);
+        if (const char *e = std::getenv("PA_REGION_SLOTS")) R = (uint32_t)std::atoi(e);
+        if (m < 0 || m > 16 || m > k || R == 0 || (R & (R - 1))) {
+            set_error("invalid PA_MINIMIZER_M / PA_REGION_SLOTS");
+            return PA_EINVAL;
+        }
+        if (m == 0) R = 1;
+    }
+    uint64_t cap = std::max<uint64_t>(64, 2 * windows + 64);
+    if (m > 0) cap = (cap + R - 1) / R * R;
+    idx->cap = cap;
+    idx->home = pad::HomeCfg{cap, m > 0 ? cap / R : 0, R, (int)std::max<int64_t>(k, 0), m};
     const int sb = slot_bytes(idx->nw);
     PA_HIP(hipMalloc(&idx->table, idx->cap * sb));
     PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));

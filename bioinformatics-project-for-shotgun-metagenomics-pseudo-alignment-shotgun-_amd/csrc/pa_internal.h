@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/pa.h"
+#include "pa_home.h"
 
 namespace pa {
 
@@ -61,6 +62,7 @@ struct pa_index {
     // open-addressing table: slots of {uint64 key[nw]; uint32 cls; uint32 csize}
     void *table = nullptr;
     uint64_t cap = 0;
+    pad::HomeCfg home{};               // home-slot function (minimizer regions for k <= 31)
     uint64_t n_kmers = 0;
     // classes: cls < n_genomes means {cls}; cls >= n_genomes is multi class (cls - n_genomes)
     uint64_t n_multi = 0;
@@ -68,6 +70,7 @@ struct pa_index {
     uint32_t *class_size = nullptr;   // [n_multi]
     uint32_t *class_genomes = nullptr;
     uint64_t class_entries = 0;
+    uint64_t *class_mask = nullptr;     // G <= 64: membership mask per set, indexed like class_genomes
     // genome codes (0-3 ACGT, 4 other) kept for read synthesis
     uint8_t *codes = nullptr;
     uint64_t *goff = nullptr;          // device [n_genomes+1]
