@@ -121,12 +121,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--reads-per-gpu", type=int, default=None)
+    ap.add_argument("--genome-len", type=int, default=None, help="override the genome length (experiments)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.reads_per_gpu:
         cfg["reads_per_gpu"] = args.reads_per_gpu
+    if args.genome_len:
+        cfg["genome_len"] = args.genome_len
+        cfg["name"] += f" [genome_len overridden: {args.genome_len}]"
 
     import torch
     rank, world, local = pa_dist.init_process_group()

@@ -1,9 +1,12 @@
 """Build libpa.so (HIP, gfx950) in-tree with hipcc.
 
-    python build_native.py [--force]
+    python build_native.py [--force] [--stats]
 
 Objects go to ./build/, the shared library to ./libpa.so next to this file
 (both git-ignored; the .so travels to the GPU box with the repo snapshot).
+--stats builds the diagnostic variant libpa_stats.so (-DPA_STATS: the fast
+kernel counts windows / probes / walk-resolved windows / anchors and pa_align
+prints them to stderr); load it with PA_LIBRARY=<path>.
 """
 
 from __future__ import annotations
@@ -39,21 +42,24 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, stats: bool = False) -> str:
+    build_dir = BUILD + ("_stats" if stats else "")
+    lib = os.path.join(HERE, "libpa_stats.so") if stats else LIB
+    flags = FLAGS + (["-DPA_STATS"] if stats else [])
+    os.makedirs(build_dir, exist_ok=True)
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "pa.h")]
     jobs = []
     objs = []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+        obj = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
         if force or _stale(obj, [path, __file__] + headers):
             if src.endswith(".hip"):
-                cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, "-x", "hip", "-c", path, "-o", obj]
+                cmd = [hipcc, f"--offload-arch={ARCH}", *flags, "-x", "hip", "-c", path, "-o", obj]
             else:
-                cmd = [hipcc, *FLAGS, "-c", path, "-o", obj]
+                cmd = [hipcc, *flags, "-c", path, "-o", obj]
             jobs.append(cmd)
 
     def run(cmd):
@@ -66,10 +72,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), 4))) as ex:
         list(ex.map(run, jobs))
-    if force or jobs or _stale(LIB, objs):
-        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
-    return LIB
+    if force or jobs or _stale(lib, objs):
+        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs])
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, stats="--stats" in sys.argv))

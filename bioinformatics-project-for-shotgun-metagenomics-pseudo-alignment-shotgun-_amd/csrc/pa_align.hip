@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -59,6 +61,11 @@ struct AlignArgs {
     int k;
     const uint32_t *class_genomes;  // multi-genome set records [size, genomes...], id = G + offset
     const uint64_t *class_mask;     // G <= 64: membership mask of each record (same offsets)
+    const uint32_t *tile_cls;       // genome tiling (pa_index.hip); tile_n == 0: none
+    const uint64_t *tile_pk;
+    uint64_t tile_n;
+    int walk_rounds;
+    int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
     const uint8_t *seq;
     const uint8_t *qual;
     const uint64_t *off;
@@ -74,6 +81,7 @@ struct AlignArgs {
     uint32_t *queue;
     unsigned long long *qcount;
     unsigned long long *deferred_total;
+    unsigned long long *dbg;  // PA_STATS builds: [0] windows [1] probed [2] walk-resolved [3] anchors
 };
 
 __device__ __forceinline__ uint64_t first_key(uint64_t read, uint32_t rank) { return (read << 20) | rank; }
@@ -257,9 +265,9 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
             }
             if (!clean) continue;
             uint64_t slot;
-            uint32_t cls, csize;
-            if (!table_find<NW>(table, a.cap, key, home_of(key, key_hash(key), a.home), slot, cls, csize)) continue;
-            if (has_mg && (int64_t)csize > (int64_t)a.prm.mg) {
+            uint32_t cls, tpos;
+            if (!table_find<NW>(table, a.cap, key, home_of(key, key_hash(key), a.home), slot, cls, tpos)) continue;
+            if (has_mg && (int64_t)class_size_of(cls, G, a.class_genomes) > (int64_t)a.prm.mg) {
                 hr++;
                 continue;
             }
@@ -497,6 +505,12 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.k = (int)std::max<int64_t>(idx->k, 0);
     a.class_genomes = idx->class_genomes;
     a.class_mask = idx->class_mask;
+    a.tile_cls = idx->tile_cls;
+    a.tile_pk = idx->tile_pk;
+    a.tile_n = idx->tile_cls ? idx->tile_n : 0;
+    a.walk_rounds = 1;
+    if (const char *e = std::getenv("PA_WALK_ROUNDS")) a.walk_rounds = std::atoi(e);
+    if (const char *e = std::getenv("PA_DBG_MODE")) a.dbg_mode = std::atoi(e);
     a.seq = r->seq;
     a.qual = r->qual;
     a.off = r->off;
@@ -574,7 +588,11 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     a.queue = idx->queue;
     a.qcount = (unsigned long long *)idx->counters;
     a.deferred_total = (unsigned long long *)idx->counters + 1;
+    a.dbg = (unsigned long long *)idx->counters + 4;
     PA_HIP(hipMemsetAsync(idx->counters, 0, 8, st));
+#ifdef PA_STATS
+    PA_HIP(hipMemsetAsync(a.dbg, 0, 32, st));
+#endif
     ExactArgs x{};
     unsigned egrid = 0;
     PA_TRY(prepare_exact(idx, r, x, egrid));
@@ -602,6 +620,13 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     }
     launch_exact_nw(idx->nw, x, egrid, st);
     PA_HIP(hipGetLastError());
+#ifdef PA_STATS
+    unsigned long long d[4];
+    PA_HIP(hipMemcpyAsync(d, a.dbg, 32, hipMemcpyDeviceToHost, st));
+    PA_HIP(hipStreamSynchronize(st));
+    fprintf(stderr, "[pa_stats] reads %llu windows %llu probed %llu walk %llu anchors %llu\n",
+            (unsigned long long)r->n, d[0], d[1], d[2], d[3]);
+#endif
     return PA_OK;
 }
 

@@ -25,13 +25,22 @@ struct Key {
     uint64_t w[NW];
 };
 
-// Hash-table slot: packed key + class id + class size (number of genomes).
+// Hash-table slot: packed key + class id + tile position.  `tpos` is the
+// smallest concatenated-genome window position holding the key (the start of
+// its first occurrence in FASTA order), or NONE when the index has no genome
+// tiling (see the tile arrays in pa_internal.h and the walk in pa_fast.h).
 template <int NW>
 struct Slot {
     uint64_t key[NW];
     uint32_t cls;
-    uint32_t csize;
+    uint32_t tpos;
 };
+
+// Number of genomes of a class: cls < G is a singleton, otherwise the class id
+// is G + the offset of its [size, genomes...] record.
+__device__ __forceinline__ uint32_t class_size_of(uint32_t cls, uint32_t G, const uint32_t *class_genomes) {
+    return cls < G ? 1u : class_genomes[cls - G];
+}
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
     x ^= x >> 33;
@@ -75,6 +84,14 @@ __device__ __forceinline__ uint64_t mask0_of(int k, int nw) {
 __device__ __forceinline__ uint64_t get64(const uint64_t *p, uint32_t o) {
     uint32_t q = o >> 6, r = o & 63;
     uint64_t hi = p[q] << r;
+    return r ? (hi | (p[q + 1] >> (64 - r))) : hi;
+}
+
+// 64 bits at a 64-bit bit offset (packed genomes exceed 2^32 bits).
+__device__ __forceinline__ uint64_t get64_at(const uint64_t *p, uint64_t o) {
+    const uint64_t q = o >> 6;
+    const uint32_t r = (uint32_t)(o & 63);
+    const uint64_t hi = p[q] << r;
     return r ? (hi | (p[q + 1] >> (64 - r))) : hi;
 }
 
@@ -137,7 +154,7 @@ __device__ __forceinline__ uint64_t home_of(const Key<NW> &key, uint64_t h, cons
 // Read-only probe from a home slot (tables are immutable once built).
 template <int NW>
 __device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint64_t cap, const Key<NW> &k,
-                                           uint64_t home, uint64_t &slot, uint32_t &cls, uint32_t &csize) {
+                                           uint64_t home, uint64_t &slot, uint32_t &cls, uint32_t &tpos) {
     uint64_t pos = home;
     for (;;) {
         const Slot<NW> s = t[pos];
@@ -148,7 +165,7 @@ __device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint6
         if (eq) {
             slot = pos;
             cls = s.cls;
-            csize = s.csize;
+            tpos = s.tpos;
             return true;
         }
         pos = (pos + 1 == cap) ? 0 : pos + 1;

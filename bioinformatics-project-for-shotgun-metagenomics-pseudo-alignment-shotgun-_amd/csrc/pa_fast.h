@@ -30,17 +30,18 @@ struct FastCfg {
     static constexpr int E = HS / 64;                  // entries owned per lane
     static constexpr int LCAP = 64 * WPL + 64;         // longest read handled (k <= 63)
     static constexpr int NDW = (LCAP + 8 + 255) / 256; // staged dwords per lane
-    static constexpr int PW = LCAP / 32 + 2;           // packed words
-    static constexpr int BW = LCAP / 64 + 2;           // non-ACGT bitmap words
+    static constexpr int PW = NDW * 8 + 2;             // packed words (32 staged bases each)
+    static constexpr int BW = NDW * 4 + 2;             // non-ACGT bitmap words (64 staged bases each)
+    static constexpr int BMW = 128;                    // distinct-k-mer filter: 4096 bits
 };
 
 template <int WPL>
 struct __align__(16) WaveLds {
     using C = FastCfg<WPL>;
-    uint64_t packed[C::PW];
-    uint64_t poison[C::BW];
-    uint64_t hA_key[C::HS];   // distinct k-mers: table slot; then multi-set masks / p-check genome ids
-    uint32_t stage[C::NDW * 64];
+    uint64_t packed[C::PW];   // the staged bytes 2-bit packed, MSB-first (staged base p at bit 2p)
+    uint64_t diff[C::PW];     // packed XOR the anchor genome stretch (genome walk)
+    uint64_t poison[C::BW];   // LSB-first bitmap of non-ACGT staged bases
+    uint64_t hA_key[C::HS];   // distinct k-mers: key (k <= 31) or table slot; then multi-set masks / p-check genome ids
     uint32_t hA_v[C::HS];     // distinct k-mers: first window; then counts
     uint32_t hA_v2[C::HS];    // first windows
     uint32_t hB_key[C::HS];   // genome set (class id)
@@ -48,6 +49,7 @@ struct __align__(16) WaveLds {
     uint32_t hB_min[C::HS];   // first window of the set
     uint32_t gcnt[64];        // dense path: specific k-mers per genome
     uint32_t gmin[64];        //   and the first window of each
+    uint32_t bm[C::BMW];      // dense path: hash bitmap of the read's k-mers (repeat test)
 };
 
 template <int WPL>
@@ -101,37 +103,24 @@ __device__ __forceinline__ void load_stage(const uint8_t *base, uint64_t o, uint
 struct ReadTotals {      // per-lane window counters + lane-0 read counters of a wave
     uint32_t qf = 0, hr = 0;
     uint32_t unique = 0, amb = 0, unm = 0, drop = 0;
+#ifdef PA_STATS
+    uint32_t d_win = 0, d_probe = 0, d_walk = 0, d_anchor = 0;
+#endif
 };
 
 __device__ __forceinline__ bool bit(uint32_t m, int i) { return (m >> i) & 1u; }
 
 // ---- dense decision (G <= 64): lane g owns genome g ------------------------
-template <int WPL>
-__device__ __forceinline__ void decide_dense(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
-                                             uint32_t qf, uint32_t hr, ReadTotals &tot) {
-    using C = FastCfg<WPL>;
+// L.gcnt / L.gmin hold the specific counts / first windows per genome.  The
+// multi-genome sets of the read (membership mask, distinct k-mers, first window
+// in L.hA_key / hA_v / hA_v2) are only needed for the p-check, so they come from
+// `multi()` on demand (it returns their number).
+template <int WPL, typename MultiFn>
+__device__ __forceinline__ void dense_core(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
+                                           uint32_t qf, uint32_t hr, ReadTotals &tot, bool has_multi,
+                                           MultiFn multi) {
     const int lane = lane_id();
     const uint32_t G = a.G;
-    uint32_t nmulti = 0;
-#pragma unroll
-    for (int e = 0; e < C::E; e++) {
-        const int i = lane + 64 * e;
-        const uint32_t c = L.hB_key[i];
-        const uint32_t is_multi = (c != NONE && c >= G) ? 1u : 0u;
-        if (c < G) {  // NONE >= G
-            L.gcnt[c] = L.hB_cnt[i];
-            L.gmin[c] = L.hB_min[i];
-        }
-        const uint64_t bm = __ballot(is_multi);
-        if (is_multi) {
-            const uint32_t at = nmulti + lanes_below(bm);
-            L.hA_key[at] = a.class_mask[c - G];
-            L.hA_v[at] = L.hB_cnt[i];
-            L.hA_v2[at] = L.hB_min[i];
-        }
-        nmulti += (uint32_t)__popcll(bm);
-    }
-    wave_sync();
     const uint32_t cnt = L.gcnt[lane], smin = L.gmin[lane];
     const uint64_t specb = __ballot(cnt > 0);
     const uint32_t nspec = (uint32_t)__popcll(specb);
@@ -156,7 +145,8 @@ __device__ __forceinline__ void decide_dense(const AlignArgs &a, const WgCounter
         if (lane == 0) tot.amb++;
         return;
     }
-    if (a.prm.p < 0 || nmulti == 0) {
+    const uint32_t nmulti = (a.prm.p < 0 || !has_multi) ? 0u : multi();
+    if (nmulti == 0) {
         if (lane == 0) {
             count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
             tot.unique++;
@@ -189,6 +179,51 @@ __device__ __forceinline__ void decide_dense(const AlignArgs &a, const WgCounter
         count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
         tot.unique++;
     }
+}
+
+// Collect the multi-genome sets grouped in the 32-bit-key hash (hB) into the
+// list dense_core reads; returns their number.
+template <int WPL>
+__device__ __forceinline__ uint32_t dense_multi_list(const AlignArgs &a, WaveLds<WPL> &L) {
+    using C = FastCfg<WPL>;
+    const int lane = lane_id();
+    uint32_t nmulti = 0;
+#pragma unroll
+    for (int e = 0; e < C::E; e++) {
+        const int i = lane + 64 * e;
+        const uint32_t c = L.hB_key[i];
+        const uint32_t is_multi = (c != NONE && c >= a.G) ? 1u : 0u;
+        const uint64_t bm = __ballot(is_multi);
+        if (is_multi) {
+            const uint32_t at = nmulti + lanes_below(bm);
+            L.hA_key[at] = a.class_mask[c - a.G];
+            L.hA_v[at] = L.hB_cnt[i];
+            L.hA_v2[at] = L.hB_min[i];
+        }
+        nmulti += (uint32_t)__popcll(bm);
+    }
+    wave_sync();
+    return nmulti;
+}
+
+// Decision from the genome-set hash hB (every distinct k-mer grouped by set).
+template <int WPL>
+__device__ __forceinline__ void decide_dense(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
+                                             uint32_t qf, uint32_t hr, ReadTotals &tot) {
+    using C = FastCfg<WPL>;
+    const int lane = lane_id();
+#pragma unroll
+    for (int e = 0; e < C::E; e++) {
+        const int i = lane + 64 * e;
+        const uint32_t c = L.hB_key[i];
+        if (c < a.G) {  // NONE >= G
+            L.gcnt[c] = L.hB_cnt[i];
+            L.gmin[c] = L.hB_min[i];
+        }
+    }
+    // hA (distinct k-mer slots) is dead from here on: the multi list may reuse it
+    const uint32_t nmulti = dense_multi_list<WPL>(a, L);
+    dense_core<WPL>(a, wc, L, r, qf, hr, tot, nmulti > 0, [&]() { return nmulti; });
 }
 
 // ---- hash decision (G > 64) --------------------------------------------------
@@ -360,18 +395,90 @@ __device__ __forceinline__ void decide_hash(const AlignArgs &a, const WgCounters
     }
 }
 
-// ---- one read ------------------------------------------------------------------
+// ---- one read --------------------------------------------------------------------
+//
+// Per-lane window state: window j of the lane is read window lane + 64 j; bit j
+// of `pend` / `inc` = unresolved / included.
+template <int NW, int WPL>
+struct Windows {
+    Key<NW> key[WPL];
+    uint64_t slot[NW == 1 ? 1 : WPL];  // table slot = k-mer identity for multi-word keys
+    uint32_t cls[WPL];
+    uint32_t pend, inc, qf, hr;
+};
+
+// ASCII -> 2-bit codes of four bases at once: ((c >> 1) ^ (c >> 2)) & 3 maps
+// A C G T to 0 1 2 3; a byte is a base iff "ACGT"[code] gives it back.
+__device__ __forceinline__ uint32_t swar_codes(uint32_t x) { return ((x >> 1) ^ (x >> 2)) & 0x03030303u; }
+__device__ __forceinline__ uint32_t swar_bad_bytes(uint32_t x, uint32_t codes) {
+    const uint32_t d = x ^ __builtin_amdgcn_perm(0u, 0x54474341u, codes);  // byte lookup in "ACGT"
+    return ((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu | d) & 0x80808080u;           // high bit of every nonzero byte
+}
+// Four codes (byte i = base i) -> one byte, first base in the top bits.
+__device__ __forceinline__ uint32_t swar_pack_byte(uint32_t codes) {
+    return (codes * ((1u << 30) | (1u << 20) | (1u << 10) | 1u)) >> 24;
+}
+
+// Stage, filter and pack one read; window keys, ok bits and filter counts go to
+// `S`.  Staged coordinates: the read's bytes start `shift` bytes into the
+// staging buffer, so read window w is staged (and packed) position w + shift.
+// Returns false if the read has no windows to resolve (dropped by
+// --min-read-quality).
 template <int NW, int WPL, bool DENSE>
-__device__ __forceinline__ void fast_read(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
-                                          WaveQual<WPL> *Q, bool need_q, uint64_t r, uint32_t shift,
-                                          uint32_t len, ReadTotals &tot) {
+__device__ __forceinline__ bool prep_read(const AlignArgs &a, WaveLds<WPL> &L, WaveQual<WPL> *Q, bool need_q,
+                                          uint32_t shift, uint32_t len, const uint32_t (&sd)[FastCfg<WPL>::NDW],
+                                          const uint32_t (&qd)[FastCfg<WPL>::NDW], Windows<NW, WPL> &S,
+                                          ReadTotals &tot) {
     using C = FastCfg<WPL>;
     const int lane = lane_id();
     const int k = a.k;
     const uint32_t flags = a.prm.flags;
-    const uint8_t *sb = (const uint8_t *)L.stage + shift;
     const uint32_t W = (len >= (uint32_t)k) ? len - k + 1 : 0;
-
+    wave_sync();  // the previous read is done with the LDS
+    if (need_q) {
+#pragma unroll
+        for (int j = 0; j < C::NDW; j++) Q->stage[lane + 64 * j] = qd[j];
+    }
+    // per-read LDS state of the dense decision
+    if (DENSE && NW == 1) {
+        L.gcnt[lane] = 0;
+        L.gmin[lane] = NONE;
+        L.bm[lane] = 0;
+        L.bm[lane + 64] = 0;
+    }
+    // ---- 2-bit pack (4 bases per lane and staged dword) + non-ACGT test
+    uint32_t badany = 0;
+    uint8_t *pk8 = (uint8_t *)L.packed;
+#pragma unroll
+    for (int j = 0; j < C::NDW; j++) {
+        const uint32_t x = sd[j];
+        const uint32_t cd = swar_codes(x);
+        const uint32_t p0 = 4u * (lane + 64 * j);  // staged position of the dword's first byte
+        uint32_t bad = swar_bad_bytes(x, cd);
+        // only bytes inside the read count
+        const uint32_t lo = shift > p0 ? shift - p0 : 0u, hi = shift + len > p0 ? shift + len - p0 : 0u;
+        const uint32_t inr = (hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1)) & (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
+        badany |= bad & inr;
+        pk8[(lane + 64 * j) ^ 7] = (uint8_t)swar_pack_byte(cd);
+    }
+    if (lane < 2) L.packed[C::PW - 2 + lane] = 0;
+    const bool any_bad = __ballot(badany != 0) != 0;
+    if (any_bad) {  // rare: reads are ACGT by grammar (src/records.py:262); mark every bad base
+        if (lane < C::BW) L.poison[lane] = 0;
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < C::NDW; j++) {
+            const uint32_t x = sd[j];
+            const uint32_t p0 = 4u * (lane + 64 * j);
+            const uint32_t lo = shift > p0 ? shift - p0 : 0u, hi = shift + len > p0 ? shift + len - p0 : 0u;
+            const uint32_t inr =
+                (hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1)) & (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
+            const uint32_t bad = swar_bad_bytes(x, swar_codes(x)) & inr;
+            const uint32_t nib = ((bad >> 7) & 1u) | ((bad >> 14) & 2u) | ((bad >> 21) & 4u) | ((bad >> 28) & 8u);
+            if (nib) atomicOr((uint32_t *)L.poison + (p0 >> 5), nib << (p0 & 31));
+        }
+    }
+    wave_sync();
     // ---- raw-ASCII quality prefix sums (src/kmer.py:399, 408)
     if (need_q) {  // (not `if (Q)`: a null test of an LDS pointer miscompiles)
         const uint8_t *qb = (const uint8_t *)Q->stage + shift;
@@ -386,23 +493,178 @@ __device__ __forceinline__ void fast_read(const AlignArgs &a, const WgCounters &
         wave_sync();
         if ((flags & F_MRQ) && (int64_t)Q->pref[len] < (int64_t)a.prm.mrq * (int64_t)len) {
             if (lane == 0) tot.drop++;  // dropped, not unmapped (src/kmer.py:587-589)
-            return;
+            return false;
         }
     }
-    // ---- 2-bit pack + non-ACGT bitmap; clear the hashes
-    for (uint32_t c0 = 0; c0 < len; c0 += 64) {
-        const uint32_t i = c0 + lane;
-        const uint32_t code = i < len ? base_code(sb[i]) : 0u;
-        const uint64_t bad = __ballot(code > 3);
-        const uint64_t v = half_or64((uint64_t)(code & 3) << (62 - 2 * (lane & 31)));
-        if ((lane & 31) == 31) L.packed[c0 / 32 + (lane >> 5)] = v;
-        if (lane == 0) L.poison[c0 / 64] = bad;
+    // ---- windows: quality gate, key (src/kmer.py:419-429)
+    const int64_t mkq_k = (int64_t)a.prm.mkq * k;
+    S.pend = S.inc = S.qf = S.hr = 0;
+#pragma unroll
+    for (int j = 0; j < WPL; j++) {
+        const uint32_t w = lane + 64 * j;
+        uint32_t ok = w < W ? 1u : 0u;
+        if (ok && (flags & F_MKQ) && (int64_t)(Q->pref[w + k] - Q->pref[w]) < mkq_k) {
+            S.qf++;
+            ok = 0;
+        }
+        if (ok && any_bad && window_bits(L.poison, w + shift, k) != 0) ok = 0;
+        S.key[j] = extract_key<NW>(L.packed, w + shift, k);
+        S.pend |= ok << j;
     }
-    if (lane < 2) {
-        const uint32_t nc = (len + 63) / 64;
-        L.packed[nc * 2 + lane] = 0;
-        if (lane == 0) L.poison[nc] = 0;
+    return true;
+}
+
+// Resolve the windows of a read (its global-memory phase).
+template <int NW, int WPL>
+__device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L, uint32_t shift,
+                                             Windows<NW, WPL> &S, ReadTotals &tot) {
+    using C = FastCfg<WPL>;
+    const int lane = lane_id();
+    const int k = a.k;
+    const uint32_t flags = a.prm.flags;
+    const Slot<NW> *table = (const Slot<NW> *)a.table;
+    // a window whose k-mer is in the index: --max-genomes gate, else included
+    auto resolve = [&](int j, uint32_t c) {
+        S.cls[j] = c;
+        if ((flags & F_MG) && (int64_t)class_size_of(c, a.G, a.class_genomes) > (int64_t)a.prm.mg)
+            S.hr++;  // highly redundant k-mer (src/kmer.py:425-427)
+        else
+            S.inc |= 1u << j;
+    };
+    // hash-table probes of the windows in m, all of a lane's in flight together;
+    // returns the windows found (first-occurrence positions in tp)
+    auto probe = [&](uint32_t m, uint32_t (&tp)[WPL]) -> uint32_t {
+        uint32_t found = 0;
+#ifdef PA_STATS
+        tot.d_probe += __popc(m);
+#endif
+        uint64_t pos[WPL];
+#pragma unroll
+        for (int j = 0; j < WPL; j++)
+            if (bit(m, j)) pos[j] = home_of<NW>(S.key[j], key_hash(S.key[j]), a.home);
+        while (__ballot(m != 0)) {
+            Slot<NW> s[WPL];
+#pragma unroll
+            for (int j = 0; j < WPL; j++)
+                if (bit(m, j)) s[j] = table[pos[j]];
+#pragma unroll
+            for (int j = 0; j < WPL; j++) {
+                if (!bit(m, j)) continue;
+                if (s[j].key[0] == EMPTY) {
+                    m &= ~(1u << j);
+                    continue;
+                }
+                bool eq = true;
+#pragma unroll
+                for (int t = 0; t < NW; t++) eq &= (s[j].key[t] == S.key[j].w[t]);
+                if (eq) {
+                    m &= ~(1u << j);
+                    found |= 1u << j;
+                    tp[j] = s[j].tpos;
+                    if constexpr (NW > 1) S.slot[j] = pos[j];
+                    resolve(j, s[j].cls);
+                } else {
+                    pos[j] = (pos[j] + 1 == a.cap) ? 0 : pos[j] + 1;
+                }
+            }
+        }
+        return found;
+    };
+    uint32_t tp[WPL];
+    if constexpr (NW == 1) {
+        // ---- genome walk: probe a few seed windows; a found seed places the read
+        // on the concatenated genomes (its key's first occurrence) and every other
+        // window is checked against the genome at the same offset -- the read's
+        // packed bases XOR the genome's (a few words) plus one contiguous tile_cls
+        // load, instead of a random probe per window.  A window counts as resolved
+        // only if its k bases equal the genome's and an indexed window starts
+        // there, so its class is exactly the table's.  Further rounds (if
+        // configured) re-seed among the windows still unresolved.
+        const int sh = 64 - 2 * k;
+#pragma unroll 1
+        for (int round = 0; round < a.walk_rounds; round++) {
+            uint64_t pb[WPL];
+#pragma unroll
+            for (int j = 0; j < WPL; j++) pb[j] = __ballot(bit(S.pend, j));
+            int wf = -1, wl = -1;
+#pragma unroll
+            for (int j = 0; j < WPL; j++)
+                if (pb[j] && wf < 0) wf = 64 * j + __builtin_ctzll(pb[j]);
+#pragma unroll
+            for (int j = WPL - 1; j >= 0; j--)
+                if (pb[j] && wl < 0) wl = 64 * j + 63 - __builtin_clzll(pb[j]);
+            if (wf < 0) break;
+            const int mid = (wf + wl) >> 1;
+            int wm = -1;
+#pragma unroll
+            for (int j = 0; j < WPL; j++) {
+                const int lo = mid - 64 * j;
+                const uint64_t m = lo <= 0 ? pb[j] : (lo >= 64 ? 0ull : (pb[j] & (~0ull << lo)));
+                if (m && wm < 0) wm = 64 * j + __builtin_ctzll(m);
+            }
+            uint32_t seedm = 0;
+#pragma unroll
+            for (int j = 0; j < WPL; j++) {
+                const int w = lane + 64 * j;
+                seedm |= (w == wf || w == wl || w == wm ? 1u : 0u) << j;
+            }
+            const uint32_t found = probe(seedm, tp);
+            S.pend &= ~seedm;
+            if (!__ballot(S.pend != 0)) break;
+            // anchor: a specific seed (its genome is the read's), else any found one
+            int at = -1;
+            uint32_t atp = NONE;
+#pragma unroll
+            for (int pass = 0; pass < 2; pass++)
+#pragma unroll
+                for (int j = 0; j < WPL; j++) {
+                    const bool c = bit(found, j) && tp[j] != NONE && (pass == 1 || S.cls[j] < a.G);
+                    const uint64_t bl = __ballot(c);
+                    if (bl && at < 0) {
+                        const int l = __builtin_ctzll(bl);
+                        at = 64 * j + l;
+                        atp = __builtin_amdgcn_readlane(tp[j], l);
+                    }
+                }
+            const int64_t A = (int64_t)atp - at;    // genome position of read window 0
+            const int64_t g0 = A - (int64_t)shift;  // genome position of staged base 0
+            if (at < 0 || g0 < 0) continue;
+#ifdef PA_STATS
+            if (lane == 0) tot.d_anchor++;
+#endif
+            // diff words: staged packed bases XOR the genome from g0 on (tile_pk is padded)
+            if (lane < C::PW - 1) L.diff[lane] = L.packed[lane] ^ get64_at(a.tile_pk, 2 * (uint64_t)g0 + 64u * lane);
+            uint32_t tc[WPL];
+#pragma unroll
+            for (int j = 0; j < WPL; j++) {
+                tc[j] = NONE;
+                const uint64_t t = (uint64_t)(A + lane + 64 * j);
+                if (bit(S.pend, j) && t < a.tile_n) tc[j] = a.tile_cls[t];
+            }
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < WPL; j++)
+                if (tc[j] != NONE && (get64(L.diff, 2 * (lane + 64 * j + shift)) >> sh) == 0) {
+#ifdef PA_STATS
+                    tot.d_walk++;
+#endif
+                    S.pend &= ~(1u << j);
+                    resolve(j, tc[j]);
+                }
+        }
     }
+    probe(S.pend, tp);  // everything the walk did not resolve
+    S.pend = 0;
+}
+
+// Distinct k-mers, genome sets and the decision: the hash path (any NW, any G).
+template <int NW, int WPL, bool DENSE>
+__device__ __forceinline__ void decide_general(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
+                                               const Windows<NW, WPL> &S, uint64_t r, ReadTotals &tot) {
+    using C = FastCfg<WPL>;
+    const int lane = lane_id();
+    const uint32_t incm = S.inc;
+    // ---- clear the hashes
 #pragma unroll
     for (int e = 0; e < C::E; e++) {
         const int i = lane + 64 * e;
@@ -417,68 +679,18 @@ __device__ __forceinline__ void fast_read(const AlignArgs &a, const WgCounters &
         L.gmin[lane] = NONE;
     }
     wave_sync();
-    // ---- windows: quality gate, key, probe (src/kmer.py:419-429)
-    const Slot<NW> *table = (const Slot<NW> *)a.table;
-    const int64_t mkq_k = (int64_t)a.prm.mkq * k;
-    Key<NW> key[WPL];
-    uint64_t pos[WPL];
-    uint32_t cls[WPL];
-    uint32_t pendm = 0, incm = 0;  // bit j: window lane + 64j still probing / included
-    uint32_t qf = 0, hr = 0;
-#pragma unroll
-    for (int j = 0; j < WPL; j++) {
-        const uint32_t w = lane + 64 * j;
-        uint32_t ok = w < W ? 1u : 0u;
-        if (ok && (flags & F_MKQ) && (int64_t)(Q->pref[w + k] - Q->pref[w]) < mkq_k) {
-            qf++;
-            ok = 0;
-        }
-        if (ok && window_bits(L.poison, w, k) != 0) ok = 0;
-        if (ok) {
-            key[j] = extract_key<NW>(L.packed, w, k);
-            pos[j] = home_of<NW>(key[j], key_hash(key[j]), a.home);
-        }
-        pendm |= ok << j;
-    }
-    while (__ballot(pendm != 0)) {  // all probes of the lane in flight together
-        Slot<NW> s[WPL];
-#pragma unroll
-        for (int j = 0; j < WPL; j++)
-            if (bit(pendm, j)) s[j] = table[pos[j]];
-#pragma unroll
-        for (int j = 0; j < WPL; j++) {
-            if (!bit(pendm, j)) continue;
-            if (s[j].key[0] == EMPTY) {
-                pendm &= ~(1u << j);
-                continue;
-            }
-            bool eq = true;
-#pragma unroll
-            for (int t = 0; t < NW; t++) eq &= (s[j].key[t] == key[j].w[t]);
-            if (eq) {
-                pendm &= ~(1u << j);
-                cls[j] = s[j].cls;
-                if ((flags & F_MG) && (int64_t)s[j].csize > (int64_t)a.prm.mg)
-                    hr++;  // highly redundant k-mer (src/kmer.py:425-427)
-                else
-                    incm |= 1u << j;
-            } else {
-                pos[j] = (pos[j] + 1 == a.cap) ? 0 : pos[j] + 1;
-            }
-        }
-    }
-    if (!__ballot(incm != 0)) {
-        tot.qf += qf;
-        tot.hr += hr;
-        if (lane == 0) tot.unm++;  // no k-mer references -> UNMAPPED (src/kmer.py:516-517)
-        return;
-    }
-    // ---- distinct k-mers: first window per table slot (quirk 3)
+    // ---- distinct k-mers: first window per k-mer (quirk 3); the identity is the
+    // key itself for single-word keys, the table slot otherwise
     uint32_t hp[WPL];
 #pragma unroll
     for (int j = 0; j < WPL; j++)
         if (bit(incm, j)) {
-            hp[j] = lds_insert64(L.hA_key, C::HS, pos[j]);
+            uint64_t id;
+            if constexpr (NW == 1)
+                id = S.key[j].w[0];
+            else
+                id = S.slot[j];
+            hp[j] = lds_insert64(L.hA_key, C::HS, id);
             atomicMin(&L.hA_v[hp[j]], (uint32_t)(lane + 64 * j));
         }
     wave_sync();
@@ -486,15 +698,106 @@ __device__ __forceinline__ void fast_read(const AlignArgs &a, const WgCounters &
 #pragma unroll
     for (int j = 0; j < WPL; j++)
         if (bit(incm, j) && L.hA_v[hp[j]] == (uint32_t)(lane + 64 * j)) {
-            const uint32_t p = lds_insert32(L.hB_key, C::HS, cls[j]);
+            const uint32_t p = lds_insert32(L.hB_key, C::HS, S.cls[j]);
             atomicAdd(&L.hB_cnt[p], 1u);
             atomicMin(&L.hB_min[p], (uint32_t)(lane + 64 * j));
         }
     wave_sync();
+#ifdef PA_STATS
+    if (a.dbg_mode == 4) return;
+#endif
     if (DENSE)
-        decide_dense<WPL>(a, wc, L, r, qf, hr, tot);
+        decide_dense<WPL>(a, wc, L, r, S.qf, S.hr, tot);
     else
-        decide_hash<WPL>(a, wc, L, r, qf, hr, tot);
+        decide_hash<WPL>(a, wc, L, r, S.qf, S.hr, tot);
+}
+
+// Dense decision for single-word keys.  Reads almost never hold a k-mer twice,
+// so a 4096-bit hash bitmap (atomic OR with return) proves the read's included
+// k-mers distinct; then every specific k-mer goes straight to its genome's
+// counter and first window, and the multi-genome sets are grouped only when the
+// p-check needs them.  A possible repeat falls back to the exact hash path.
+template <int WPL>
+__device__ __forceinline__ void decide_dense_fast(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
+                                                  const Windows<1, WPL> &S, uint64_t r, ReadTotals &tot) {
+    using C = FastCfg<WPL>;
+    const int lane = lane_id();
+    const uint32_t incm = S.inc;
+    uint32_t dup = 0;
+#pragma unroll
+    for (int j = 0; j < WPL; j++)
+        if (bit(incm, j)) {
+            const uint32_t h = (uint32_t)((S.key[j].w[0] * 0x9E3779B97F4A7C15ull) >> 52);
+            const uint32_t b = 1u << (h & 31);
+            dup |= atomicOr(&L.bm[h >> 5], b) & b;
+        }
+    if (__ballot(dup != 0)) {
+        decide_general<1, WPL, true>(a, wc, L, S, r, tot);
+        return;
+    }
+    uint32_t multim = 0;
+#pragma unroll
+    for (int j = 0; j < WPL; j++)
+        if (bit(incm, j)) {
+            const uint32_t c = S.cls[j];
+            if (c < a.G) {
+                atomicAdd(&L.gcnt[c], 1u);
+                atomicMin(&L.gmin[c], (uint32_t)(lane + 64 * j));
+            } else {
+                multim |= 1u << j;
+            }
+        }
+    const bool has_multi = __ballot(multim != 0) != 0;
+    wave_sync();
+#ifdef PA_STATS
+    if (a.dbg_mode == 4) return;
+#endif
+    dense_core<WPL>(a, wc, L, r, S.qf, S.hr, tot, has_multi, [&]() -> uint32_t {
+#pragma unroll
+        for (int e = 0; e < C::E; e++) {
+            const int i = lane + 64 * e;
+            L.hB_key[i] = NONE;
+            L.hB_cnt[i] = 0;
+            L.hB_min[i] = NONE;
+        }
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < WPL; j++)
+            if (bit(multim, j)) {
+                const uint32_t p = lds_insert32(L.hB_key, C::HS, S.cls[j]);
+                atomicAdd(&L.hB_cnt[p], 1u);
+                atomicMin(&L.hB_min[p], (uint32_t)(lane + 64 * j));
+            }
+        wave_sync();
+        return dense_multi_list<WPL>(a, L);
+    });
+}
+
+template <int NW, int WPL, bool DENSE>
+__device__ __forceinline__ void fast_read(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
+                                          WaveQual<WPL> *Q, bool need_q, uint64_t r, uint32_t shift, uint32_t len,
+                                          const uint32_t (&sd)[FastCfg<WPL>::NDW],
+                                          const uint32_t (&qd)[FastCfg<WPL>::NDW], ReadTotals &tot) {
+    Windows<NW, WPL> S;
+    if (!prep_read<NW, WPL, DENSE>(a, L, Q, need_q, shift, len, sd, qd, S, tot)) return;
+#ifdef PA_STATS
+    tot.d_win += __popc(S.pend);
+    if (a.dbg_mode == 2) return;
+#endif
+    resolve_read<NW, WPL>(a, L, shift, S, tot);
+#ifdef PA_STATS
+    if (a.dbg_mode == 3) return;
+#endif
+    if (!__ballot(S.inc != 0)) {
+        tot.qf += S.qf;
+        tot.hr += S.hr;
+        if (lane_id() == 0) tot.unm++;  // no k-mer references -> UNMAPPED (src/kmer.py:516-517)
+        return;
+    }
+    if constexpr (DENSE && NW == 1)
+        decide_dense_fast<WPL>(a, wc, L, S, r, tot);
+    else
+        decide_general<NW, WPL, DENSE>(a, wc, L, S, r, tot);
 }
 
 template <int NW, int WPL, bool DENSE>
@@ -522,7 +825,8 @@ __global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
     }
     __syncthreads();
 
-    // contiguous chunk of reads for this wave
+    // contiguous chunk of reads for this wave; the bytes of read r+1 are loaded
+    // while read r is classified (and the offset of read r+2)
     const uint64_t nw = (uint64_t)gridDim.x * kWaves, gw = (uint64_t)blockIdx.x * kWaves + wid;
     const uint64_t rb = a.n * gw / nw, re = a.n * (gw + 1) / nw;
     ReadTotals tot;
@@ -541,16 +845,9 @@ __global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
             const uint32_t len = (uint32_t)(o_nxt - o_cur);
             const uint32_t W = (len >= (uint32_t)a.k) ? len - a.k + 1 : 0;
             if (W > 64u * WPL || len > (uint32_t)(C::LCAP - 8)) {
-                if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;
+                if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;  // the exact kernel takes it
             } else {
-                wave_sync();
-#pragma unroll
-                for (int j = 0; j < C::NDW; j++) {
-                    L.stage[lane + 64 * j] = sd[j];
-                    if (need_q) Q->stage[lane + 64 * j] = qd[j];
-                }
-                wave_sync();
-                fast_read<NW, WPL, DENSE>(a, wc, L, Q, need_q, r, (uint32_t)(o_cur & 3), len, tot);
+                fast_read<NW, WPL, DENSE>(a, wc, L, Q, need_q, r, (uint32_t)(o_cur & 3), len, sd, qd, tot);
             }
             o_cur = o_nxt;
             o_nxt = o_nn;
@@ -564,6 +861,18 @@ __global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
     // ---- flush
     const uint32_t qf_w = wave_sum(tot.qf), hr_w = wave_sum(tot.hr);
     const bool has_mkq = a.prm.flags & F_MKQ, has_mg = a.prm.flags & F_MG;
+#ifdef PA_STATS
+    {
+        const uint32_t s0 = wave_sum(tot.d_win), s1 = wave_sum(tot.d_probe), s2 = wave_sum(tot.d_walk),
+                       s3 = wave_sum(tot.d_anchor);
+        if (lane == 0) {
+            atomicAdd(&a.dbg[0], (unsigned long long)s0);
+            atomicAdd(&a.dbg[1], (unsigned long long)s1);
+            atomicAdd(&a.dbg[2], (unsigned long long)s2);
+            atomicAdd(&a.dbg[3], (unsigned long long)s3);
+        }
+    }
+#endif
     if (lane == 0) {
         if (tot.unique) atomicAdd(&a.stats[0], (unsigned long long)tot.unique);
         if (tot.amb) atomicAdd(&a.stats[1], (unsigned long long)tot.amb);

@@ -3,15 +3,22 @@
 //
 // Index layout in HBM
 //   table          open addressing, linear probing, `cap` slots of
-//                  {uint64 key[NW]; uint32 cls; uint32 csize} (16 B for k <= 31),
+//                  {uint64 key[NW]; uint32 cls; uint32 tpos} (16 B for k <= 31),
 //                  load factor <= 0.5 (cap = 2 x genome windows).
 //   classes        the genome SET of a k-mer (the keys of kmers[kmer] in the
 //                  reference) is a "class": cls < G means the singleton {cls};
 //                  cls >= G is a deduplicated multi-genome set stored as the
 //                  record class_genomes[cls - G] = [size, ascending genomes...]
-//                  (one contiguous read in the align kernels).  csize caches
-//                  the set size in the slot so --max-genomes and the
-//                  specific/unspecific test need no second memory access.
+//                  (one contiguous read in the align kernels; the size serves
+//                  --max-genomes).
+//   tiling         (k <= 31, < 2^32 bases) the genomes concatenated in FASTA
+//                  order as a 2-bit string `tile_pk` plus `tile_cls[t]` = class
+//                  of the k-mer starting at concatenated position t (NONE if no
+//                  indexed window starts there: N bases, genome ends).  A slot's
+//                  tpos is the first position of its key.  A read that matches
+//                  a genome stretch is then resolved by ONE table probe plus a
+//                  contiguous read of tile_cls / tile_pk (pa_fast.h), each
+//                  window still verified base for base against the genome.
 //
 // Build pipeline (all stream-ordered, one host sync at the end)
 //   1. ASCII -> 2-bit codes (4 = anything else, e.g. 'N').
@@ -25,6 +32,7 @@
 //      each list against its class representative element by element (a hash
 //      collision is reported as PA_EINTERNAL, never merged silently), assign
 //      class ids and copy representative lists into class_genomes.
+//   6. tiling: pack the genomes, then per genome look up every window's class.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -119,7 +127,8 @@ __device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, ui
 template <int NW>
 __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
                                uint64_t mask0, uint32_t g, Slot<NW> *table, HomeCfg hc, uint32_t *deg,
-                               uint32_t *last_g, uint32_t *first_g, unsigned long long *n_kmers, uint32_t *err) {
+                               uint32_t *last_g, uint32_t *first_g, unsigned long long *n_kmers, uint32_t *err,
+                               int tile) {
     const uint64_t cap = hc.cap;
     uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
     if (w0 >= nwin) return;
@@ -141,6 +150,10 @@ __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstar
         if (run < k) continue;  // window contains a non-ACGT base (src/kmer.py:145)
         uint64_t slot = table_insert<NW>(table, cap, key, home_of(key, key_hash(key), hc), n_kmers, err);
         if (slot == ~0ull) return;
+        if (tile) {  // first occurrence; a stale plain load can only be larger
+            const uint32_t t = (uint32_t)(gstart + w);
+            if (table[slot].tpos > t) atomicMin(&table[slot].tpos, t);
+        }
         uint32_t old = atomicMax(&last_g[slot], g + 1);
         if (old < g + 1) {
             uint32_t d = atomicAdd(&deg[slot], 1u);
@@ -162,7 +175,6 @@ __global__ void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg,
             d = deg[s];
             if (d == 1) {
                 table[s].cls = aux[s];
-                table[s].csize = 1;
                 d = 0;
             }
         }
@@ -176,7 +188,6 @@ __global__ void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg,
         if (d >= 2) {
             off[s] = wbase + incl - d;
             aux[s] = 0;
-            table[s].csize = d;
         }
     }
 }
@@ -206,8 +217,8 @@ __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart,
         key_push(key, c & 3, mask0);
         if (run < k) continue;
         uint64_t slot;
-        uint32_t cls, csize;
-        if (!table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, csize)) continue;
+        uint32_t cls, tpos;
+        if (!table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) continue;
         if (deg[slot] < 2) continue;
         uint32_t old = atomicMax(&last_g[slot], g + 1);
         if (old < g + 1) {
@@ -314,7 +325,7 @@ __global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint32_t *de
 
 template <int NW>
 __global__ void k_lookup(const Slot<NW> *table, HomeCfg hc, const uint8_t *kmers, uint64_t n, int k, uint64_t mask0,
-                         int64_t *cls_out, uint32_t *size_out) {
+                         uint32_t G, const uint32_t *class_genomes, int64_t *cls_out, uint32_t *size_out) {
     const uint64_t cap = hc.cap;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -329,13 +340,69 @@ __global__ void k_lookup(const Slot<NW> *table, HomeCfg hc, const uint8_t *kmers
         key_push(key, c & 3, mask0);
     }
     uint64_t slot;
-    uint32_t cls = 0, csize = 0;
-    if (ok && table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, csize)) {
+    uint32_t cls = 0, tpos = 0;
+    if (ok && table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) {
         cls_out[i] = cls;
-        size_out[i] = csize;
+        size_out[i] = class_size_of(cls, G, class_genomes);
     } else {
         cls_out[i] = -1;
         size_out[i] = 0;
+    }
+}
+
+// ---- genome tiling ------------------------------------------------------------
+
+// 32 bases per word, first base in the top bits (the read packing of pa_fast.h);
+// non-ACGT codes pack as 0 -- tile_cls marks every window that holds one.
+__global__ void k_tile_pack(const uint8_t *__restrict__ codes, uint64_t n, uint64_t *__restrict__ pk,
+                            uint64_t nwords) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; i < nwords; i += stride) {
+        uint64_t v = 0;
+        const uint64_t b = i * 32;
+        if (b + 32 <= n) {
+            const uint4 *q = (const uint4 *)(codes + b);  // codes are 16-B aligned (hipMalloc), b % 32 == 0
+            const uint4 x = q[0], y = q[1];
+            const uint32_t wds[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (int d = 0; d < 8; d++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) v = (v << 2) | ((wds[d] >> (8 * j)) & 3u);
+        } else {
+            for (int j = 0; j < 32; j++) v = (v << 2) | (b + j < n ? (uint64_t)(codes[b + j] & 3u) : 0ull);
+        }
+        pk[i] = v;
+    }
+}
+
+// Class of the k-mer starting at every window of one genome (tile_cls is
+// pre-filled with NONE, which stays at windows with non-ACGT bases).
+template <int NW>
+__global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k, uint64_t mask0,
+                           const Slot<NW> *table, HomeCfg hc, uint32_t *tile_cls) {
+    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+    if (w0 >= nwin) return;
+    uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
+    const uint8_t *s = codes + gstart + w0;
+    Key<NW> key;
+#pragma unroll
+    for (int j = 0; j < NW; j++) key.w[j] = 0;
+    int run = 0;
+    for (int i = 0; i < k - 1; i++) {
+        uint32_t c = s[i];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+    }
+    for (uint64_t w = w0; w < w1; w++) {
+        uint32_t c = s[w - w0 + k - 1];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+        if (run < k) continue;
+        uint64_t slot;
+        uint32_t cls, tpos;
+        if (table_find<NW>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos))
+            tile_cls[gstart + w] = cls;
     }
 }
 
@@ -491,7 +558,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         uint64_t nwin = len - k + 1;
         hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
                            idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, deg, last_g, aux, cnt + 0,
-                           err);
+                           err, idx->tile_n > 0 ? 1 : 0);
     }
     B_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_build_prep<NW>, dim3(grid_for(cap, kBlock) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0,
@@ -570,6 +637,24 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         idx->class_entries = entries;
         idx->device_bytes += n_multi * 12 + std::max<uint64_t>(entries, 1) * 4;
     }
+    if (idx->tile_n > 0) {  // step 6: genome tiling
+        const uint64_t n = idx->tile_n, nwords = n / 32 + 32;  // padded: the walk reads up to 18 words past a position
+        B_HIP(hipMalloc(&idx->tile_cls, n * 4));
+        B_HIP(hipMalloc(&idx->tile_pk, nwords * 8));
+        B_HIP(hipMemsetAsync(idx->tile_cls, 0xFF, n * 4, st));
+        hipLaunchKernelGGL(k_tile_pack, dim3(grid_for(nwords) > 65536 ? 65536 : grid_for(nwords)), dim3(kBlock), 0, st,
+                           idx->codes, n, idx->tile_pk, nwords);
+        for (uint32_t g = 0; g < G; g++) {
+            uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
+            if ((uint64_t)k > len) continue;
+            uint64_t nwin = len - k + 1;
+            hipLaunchKernelGGL(k_tile_cls<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
+                               idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls);
+        }
+        B_HIP(hipGetLastError());
+        B_HIP(hipStreamSynchronize(st));
+        idx->device_bytes += n * 4 + nwords * 8;
+    }
 #undef B_HIP
     cleanup();
     return rc;
@@ -581,7 +666,7 @@ pa_status lookup_nw(const pa_index *idx, const uint8_t *d_kmers, uint64_t n, int
     const int k = (int)idx->k;
     const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
     hipLaunchKernelGGL(k_lookup<NW>, dim3(grid_for(n)), dim3(kBlock), 0, st, (const Slot<NW> *)idx->table, idx->home,
-                       d_kmers, n, k, mask0, d_cls, d_size);
+                       d_kmers, n, k, mask0, idx->n_genomes, idx->class_genomes, d_cls, d_size);
     PA_HIP(hipGetLastError());
     return PA_OK;
 }
@@ -608,6 +693,10 @@ void index_release(pa_index *idx) {
     hipFree(idx->class_mask);
     hipFree(idx->codes);
     hipFree(idx->goff);
+    hipFree(idx->tile_cls);
+    hipFree(idx->tile_pk);
+    idx->tile_cls = nullptr;
+    idx->tile_pk = nullptr;
     hipFree(idx->ws.ptr);
     hipFree(idx->queue);
     hipFree(idx->counters);
@@ -647,7 +736,14 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         }
         if (m == 0) R = 1;
     }
-    uint64_t cap = std::max<uint64_t>(64, 2 * windows + 64);
+    // genome tiling for single-word keys while positions fit 32 bits (tpos);
+    // PA_NO_TILE=1 turns it off (A/B measurements)
+    const char *no_tile = std::getenv("PA_NO_TILE");
+    idx->tile_n = (idx->nw == 1 && k > 0 && total > 0 && total < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
+                      ? total : 0;
+    uint64_t cap_mult = 2;
+    if (const char *e = std::getenv("PA_CAP_MULT")) cap_mult = std::max(2, std::atoi(e));
+    uint64_t cap = std::max<uint64_t>(64, cap_mult * windows + 64);
     if (m > 0) cap = (cap + R - 1) / R * R;
     idx->cap = cap;
     idx->home = pad::HomeCfg{cap, m > 0 ? cap / R : 0, R, (int)std::max<int64_t>(k, 0), m};

@@ -34,7 +34,7 @@ void set_error(const std::string &msg);
 // Number of 64-bit words of a packed k-mer key: 2k bits, top word < 64 bits
 // so that an all-ones top word can never be a key (empty-slot sentinel).
 inline int key_words(int64_t k) { return (int)(k / 32) + 1; }
-// Bytes per hash-table slot: key words + {uint32 class, uint32 class size}.
+// Bytes per hash-table slot: key words + {uint32 class, uint32 tile position}.
 inline int slot_bytes(int nw) { return 8 * nw + 8; }
 // Read buffers are over-allocated so a wave may fetch a whole staging window
 // (up to 512 B) past any read start without a bounds check.
@@ -59,7 +59,7 @@ struct pa_index {
     int64_t k = 0;
     int nw = 1;
     uint32_t n_genomes = 0;
-    // open-addressing table: slots of {uint64 key[nw]; uint32 cls; uint32 csize}
+    // open-addressing table: slots of {uint64 key[nw]; uint32 cls; uint32 tpos}
     void *table = nullptr;
     uint64_t cap = 0;
     pad::HomeCfg home{};               // home-slot function (minimizer regions for k <= 31)
@@ -76,6 +76,12 @@ struct pa_index {
     uint64_t *goff = nullptr;          // device [n_genomes+1]
     std::vector<uint64_t> h_goff;
     uint64_t total_windows = 0;
+    // genome tiling (single-word keys, < 2^32 genome bases): the genomes as one
+    // concatenated 2-bit string plus the class of the k-mer starting at every
+    // position (NONE where no indexed window starts); slots point into it (tpos)
+    uint64_t tile_n = 0;               // concatenated bases (0: no tiling)
+    uint32_t *tile_cls = nullptr;      // [tile_n]
+    uint64_t *tile_pk = nullptr;       // [tile_n / 32 + 32] MSB-first 2-bit words (padded)
     uint64_t device_bytes = 0;
     // align scratch
     pa::Workspace ws;
