@@ -100,9 +100,11 @@ __device__ __forceinline__ void load_stage(const uint8_t *base, uint64_t o, uint
     for (int j = 0; j < FastCfg<WPL>::NDW; j++) d[j] = p[lane_id() + 64 * j];
 }
 
-struct ReadTotals {      // per-lane window counters + lane-0 read counters of a wave
+enum : int { OUT_UNIQUE = 0, OUT_AMB = 1, OUT_DEFER = 2, OUT_UNMAPPED = 3, OUT_DROP = 4 };
+
+struct ReadTotals {      // per-lane window counters + read counters (the same in every lane) of a wave
     uint32_t qf = 0, hr = 0;
-    uint32_t unique = 0, amb = 0, unm = 0, drop = 0;
+    uint32_t unique = 0, mapped = 0, unm = 0, drop = 0;
 #ifdef PA_STATS
     uint32_t d_win = 0, d_probe = 0, d_walk = 0, d_anchor = 0;
 #endif
@@ -116,21 +118,15 @@ __device__ __forceinline__ bool bit(uint32_t m, int i) { return (m >> i) & 1u; }
 // in L.hA_key / hA_v / hA_v2) are only needed for the p-check, so they come from
 // `multi()` on demand (it returns their number).
 template <int WPL, typename MultiFn>
-__device__ __forceinline__ void dense_core(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
-                                           uint32_t qf, uint32_t hr, ReadTotals &tot, bool has_multi,
-                                           MultiFn multi) {
+__device__ __forceinline__ int dense_core(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
+                                          bool has_multi, MultiFn multi) {
     const int lane = lane_id();
     const uint32_t G = a.G;
     const uint32_t cnt = L.gcnt[lane], smin = L.gmin[lane];
     const uint64_t specb = __ballot(cnt > 0);
     const uint32_t nspec = (uint32_t)__popcll(specb);
     const uint64_t read_idx = a.base + r;
-    tot.qf += qf;
-    tot.hr += hr;
-    if (nspec == 0) {
-        if (lane == 0) tot.amb++;  // AMBIGUOUS with an empty genome list
-        return;
-    }
+    if (nspec == 0) return OUT_AMB;  // AMBIGUOUS with an empty genome list
     // top = most specific k-mers, ties to the first inserted (smallest first window)
     const uint64_t key = cnt > 0 ? (((uint64_t)cnt << 32) | (NONE - smin)) : 0;
     const uint64_t top = wave_max64(key);
@@ -142,16 +138,12 @@ __device__ __forceinline__ void dense_core(const AlignArgs &a, const WgCounters 
         uint32_t rank = 0;
         for (uint64_t m = specb; m; m &= m - 1) rank += __builtin_amdgcn_readlane(smin, __builtin_ctzll(m)) < smin;
         if (cnt > 0) count_genome(a, wc, lane, false, 1, first_key(read_idx, rank));
-        if (lane == 0) tot.amb++;
-        return;
+        return OUT_AMB;
     }
     const uint32_t nmulti = (a.prm.p < 0 || !has_multi) ? 0u : multi();
     if (nmulti == 0) {
-        if (lane == 0) {
-            count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
-            tot.unique++;
-        }
-        return;
+        if (lane == 0) count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
+        return OUT_UNIQUE;
     }
     // p-validation: totals over specific + unspecific k-mers (src/kmer.py:464-480)
     uint32_t t = cnt, tmin = cnt > 0 ? smin : NONE;
@@ -174,11 +166,10 @@ __device__ __forceinline__ void dense_core(const AlignArgs &a, const WgCounters 
             rank += ((((uint64_t)__builtin_amdgcn_readlane(tmin, s)) << 32) | (uint32_t)s) < me;
         }
         if (q) count_genome(a, wc, lane, false, lane == gstar ? 2 : 1, first_key(read_idx, lane == gstar ? 0 : rank));
-        if (lane == 0) tot.amb++;
-    } else if (lane == 0) {
-        count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
-        tot.unique++;
+        return OUT_AMB;
     }
+    if (lane == 0) count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
+    return OUT_UNIQUE;
 }
 
 // Collect the multi-genome sets grouped in the 32-bit-key hash (hB) into the
@@ -208,8 +199,7 @@ __device__ __forceinline__ uint32_t dense_multi_list(const AlignArgs &a, WaveLds
 
 // Decision from the genome-set hash hB (every distinct k-mer grouped by set).
 template <int WPL>
-__device__ __forceinline__ void decide_dense(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
-                                             uint32_t qf, uint32_t hr, ReadTotals &tot) {
+__device__ __forceinline__ int decide_dense(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r) {
     using C = FastCfg<WPL>;
     const int lane = lane_id();
 #pragma unroll
@@ -223,13 +213,12 @@ __device__ __forceinline__ void decide_dense(const AlignArgs &a, const WgCounter
     }
     // hA (distinct k-mer slots) is dead from here on: the multi list may reuse it
     const uint32_t nmulti = dense_multi_list<WPL>(a, L);
-    dense_core<WPL>(a, wc, L, r, qf, hr, tot, nmulti > 0, [&]() { return nmulti; });
+    return dense_core<WPL>(a, wc, L, r, nmulti > 0, [&]() { return nmulti; });
 }
 
 // ---- hash decision (G > 64) --------------------------------------------------
 template <int WPL>
-__device__ __forceinline__ void decide_hash(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
-                                            uint32_t qf, uint32_t hr, ReadTotals &tot) {
+__device__ __forceinline__ int decide_hash(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r) {
     using C = FastCfg<WPL>;
     const int lane = lane_id();
     const uint32_t G = a.G;
@@ -251,12 +240,7 @@ __device__ __forceinline__ void decide_hash(const AlignArgs &a, const WgCounters
         }
     }
     const uint64_t read_idx = a.base + r;
-    tot.qf += qf;  // committed from here on unless the read is deferred below
-    tot.hr += hr;
-    if (nspec == 0) {
-        if (lane == 0) tot.amb++;
-        return;
-    }
+    if (nspec == 0) return OUT_AMB;
     const uint64_t top = wave_max64(top_l);
     const uint32_t gstar = (uint32_t)top, topcnt = (uint32_t)(top >> 48);
     uint32_t sec_l = 0;
@@ -283,15 +267,11 @@ __device__ __forceinline__ void decide_hash(const AlignArgs &a, const WgCounters
 #pragma unroll
         for (int e = 0; e < C::E; e++)
             if (bit(specm, e)) count_genome(a, wc, L.hB_key[lane + 64 * e], false, 1, first_key(read_idx, rank[e]));
-        if (lane == 0) tot.amb++;
-        return;
+        return OUT_AMB;
     }
     if (a.prm.p < 0 || nmulti == 0) {
-        if (lane == 0) {
-            count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
-            tot.unique++;
-        }
-        return;
+        if (lane == 0) count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
+        return OUT_UNIQUE;
     }
     // p-validation over an LDS genome hash
     wave_sync();
@@ -345,10 +325,8 @@ __device__ __forceinline__ void decide_hash(const AlignArgs &a, const WgCounters
     for (int e = 0; e < C::E; e++) claimed += (uint32_t)__popcll(__ballot(L.hA_key[lane + 64 * e] != EMPTY));
     if (__ballot(ovf) || claimed > limit) {
         // the read's genome union does not fit the wave's LDS: the exact kernel takes it
-        tot.qf -= qf;
-        tot.hr -= hr;
         if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;
-        return;
+        return OUT_DEFER;
     }
     uint32_t ts_l = 0, mx_l = 0;
 #pragma unroll
@@ -388,11 +366,10 @@ __device__ __forceinline__ void decide_hash(const AlignArgs &a, const WgCounters
             else
                 count_genome(a, wc, g, false, 1, first_key(read_idx, rank[e]));
         }
-        if (lane == 0) tot.amb++;
-    } else if (lane == 0) {
-        count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
-        tot.unique++;
+        return OUT_AMB;
     }
+    if (lane == 0) count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
+    return OUT_UNIQUE;
 }
 
 // ---- one read --------------------------------------------------------------------
@@ -492,8 +469,7 @@ __device__ __forceinline__ bool prep_read(const AlignArgs &a, WaveLds<WPL> &L, W
         if (lane == 0) Q->pref[0] = 0;
         wave_sync();
         if ((flags & F_MRQ) && (int64_t)Q->pref[len] < (int64_t)a.prm.mrq * (int64_t)len) {
-            if (lane == 0) tot.drop++;  // dropped, not unmapped (src/kmer.py:587-589)
-            return false;
+            return false;  // dropped, not unmapped (src/kmer.py:587-589)
         }
     }
     // ---- windows: quality gate, key (src/kmer.py:419-429)
@@ -572,14 +548,38 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
     };
     uint32_t tp[WPL];
     if constexpr (NW == 1) {
-        // ---- genome walk: probe a few seed windows; a found seed places the read
-        // on the concatenated genomes (its key's first occurrence) and every other
-        // window is checked against the genome at the same offset -- the read's
-        // packed bases XOR the genome's (a few words) plus one contiguous tile_cls
-        // load, instead of a random probe per window.  A window counts as resolved
-        // only if its k bases equal the genome's and an indexed window starts
-        // there, so its class is exactly the table's.  Further rounds (if
-        // configured) re-seed among the windows still unresolved.
+        // One lane per probe: keys are re-extracted from the packed read in LDS,
+        // so the probing lanes need not own the windows they probe.
+        auto probe_one = [&](bool act, uint32_t w, uint32_t &cls, uint32_t &tpos) -> bool {
+            Key<1> key = extract_key<1>(L.packed, w + shift, k);
+            uint64_t pos = act ? home_of<1>(key, key_hash(key), a.home) : 0;
+            bool found = false;
+            while (__ballot(act)) {
+                if (act) {
+                    const Slot<1> s = table[pos];
+                    if (s.key[0] == EMPTY) {
+                        act = false;
+                    } else if (s.key[0] == key.w[0]) {
+                        act = false;
+                        found = true;
+                        cls = s.cls;
+                        tpos = s.tpos;
+                    } else {
+                        pos = (pos + 1 == a.cap) ? 0 : pos + 1;
+                    }
+                }
+            }
+            return found;
+        };
+        // ---- genome walk: probe three seed windows (first, middle, last pending);
+        // a found seed places the read on the concatenated genomes (its key's
+        // first occurrence) and every pending window is checked against the
+        // genome at the same offset -- the read's packed bases XOR the genome's
+        // (a few words) plus one contiguous tile_cls load, instead of a random
+        // probe per window.  A window counts as resolved only if its k bases equal
+        // the genome's and an indexed window starts there, so its class is
+        // exactly the table's.  Seeds stay pending: the walk (or the final
+        // probes) resolves them like any other window.
         const int sh = 64 - 2 * k;
 #pragma unroll 1
         for (int round = 0; round < a.walk_rounds; round++) {
@@ -595,40 +595,26 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
                 if (pb[j] && wl < 0) wl = 64 * j + 63 - __builtin_clzll(pb[j]);
             if (wf < 0) break;
             const int mid = (wf + wl) >> 1;
-            int wm = -1;
+            int wm = wl;
 #pragma unroll
-            for (int j = 0; j < WPL; j++) {
+            for (int j = WPL - 1; j >= 0; j--) {
                 const int lo = mid - 64 * j;
                 const uint64_t m = lo <= 0 ? pb[j] : (lo >= 64 ? 0ull : (pb[j] & (~0ull << lo)));
-                if (m && wm < 0) wm = 64 * j + __builtin_ctzll(m);
+                if (m) wm = 64 * j + __builtin_ctzll(m);
             }
-            uint32_t seedm = 0;
-#pragma unroll
-            for (int j = 0; j < WPL; j++) {
-                const int w = lane + 64 * j;
-                seedm |= (w == wf || w == wl || w == wm ? 1u : 0u) << j;
-            }
-            const uint32_t found = probe(seedm, tp);
-            S.pend &= ~seedm;
-            if (!__ballot(S.pend != 0)) break;
+            const uint32_t sw = lane == 0 ? (uint32_t)wf : lane == 1 ? (uint32_t)wm : (uint32_t)wl;
+            uint32_t scls = NONE, stp = NONE;
+#ifdef PA_STATS
+            tot.d_probe += lane < 3 ? 1u : 0u;
+#endif
+            const bool sf = probe_one(lane < 3, sw, scls, stp) && stp != NONE;
             // anchor: a specific seed (its genome is the read's), else any found one
-            int at = -1;
-            uint32_t atp = NONE;
-#pragma unroll
-            for (int pass = 0; pass < 2; pass++)
-#pragma unroll
-                for (int j = 0; j < WPL; j++) {
-                    const bool c = bit(found, j) && tp[j] != NONE && (pass == 1 || S.cls[j] < a.G);
-                    const uint64_t bl = __ballot(c);
-                    if (bl && at < 0) {
-                        const int l = __builtin_ctzll(bl);
-                        at = 64 * j + l;
-                        atp = __builtin_amdgcn_readlane(tp[j], l);
-                    }
-                }
-            const int64_t A = (int64_t)atp - at;    // genome position of read window 0
+            const uint64_t b1 = __ballot(sf && scls < a.G), b2 = __ballot(sf);
+            if (!b2) continue;
+            const int l = (int)__builtin_ctzll(b1 ? b1 : b2);
+            const int64_t A = (int64_t)__builtin_amdgcn_readlane(stp, l) - (int64_t)__builtin_amdgcn_readlane(sw, l);
             const int64_t g0 = A - (int64_t)shift;  // genome position of staged base 0
-            if (at < 0 || g0 < 0) continue;
+            if (g0 < 0) continue;
 #ifdef PA_STATS
             if (lane == 0) tot.d_anchor++;
 #endif
@@ -652,15 +638,45 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
                     resolve(j, tc[j]);
                 }
         }
+        // ---- remaining windows: compact them onto the lanes, one probe per lane
+        uint32_t *list = L.hA_v, *res = L.hA_v2;  // free until the decision
+        uint32_t npend = 0;
+#pragma unroll
+        for (int j = 0; j < WPL; j++) {
+            const uint64_t b = __ballot(bit(S.pend, j));
+            if (bit(S.pend, j)) list[npend + lanes_below(b)] = lane + 64 * j;
+            npend += (uint32_t)__popcll(b);
+        }
+        if (npend == 0) return;
+        wave_sync();
+#ifdef PA_STATS
+        tot.d_probe += lane < (int)npend ? 1u : 0u;
+#endif
+        for (uint32_t base = 0; base < npend; base += 64) {
+            const bool act = base + lane < npend;
+            const uint32_t w = act ? list[base + lane] : 0u;
+            uint32_t c = NONE, t = NONE;
+            probe_one(act, w, c, t);  // not found: c stays NONE (never a class id)
+            if (act) res[w] = c;
+        }
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < WPL; j++)
+            if (bit(S.pend, j)) {
+                const uint32_t c = res[lane + 64 * j];
+                if (c != NONE) resolve(j, c);
+            }
+        S.pend = 0;
+        return;
     }
-    probe(S.pend, tp);  // everything the walk did not resolve
+    probe(S.pend, tp);  // multi-word keys: every window probes
     S.pend = 0;
 }
 
 // Distinct k-mers, genome sets and the decision: the hash path (any NW, any G).
 template <int NW, int WPL, bool DENSE>
-__device__ __forceinline__ void decide_general(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
-                                               const Windows<NW, WPL> &S, uint64_t r, ReadTotals &tot) {
+__device__ __forceinline__ int decide_general(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
+                                              const Windows<NW, WPL> &S, uint64_t r) {
     using C = FastCfg<WPL>;
     const int lane = lane_id();
     const uint32_t incm = S.inc;
@@ -703,13 +719,10 @@ __device__ __forceinline__ void decide_general(const AlignArgs &a, const WgCount
             atomicMin(&L.hB_min[p], (uint32_t)(lane + 64 * j));
         }
     wave_sync();
-#ifdef PA_STATS
-    if (a.dbg_mode == 4) return;
-#endif
     if (DENSE)
-        decide_dense<WPL>(a, wc, L, r, S.qf, S.hr, tot);
+        return decide_dense<WPL>(a, wc, L, r);
     else
-        decide_hash<WPL>(a, wc, L, r, S.qf, S.hr, tot);
+        return decide_hash<WPL>(a, wc, L, r);
 }
 
 // Dense decision for single-word keys.  Reads almost never hold a k-mer twice,
@@ -718,8 +731,8 @@ __device__ __forceinline__ void decide_general(const AlignArgs &a, const WgCount
 // counter and first window, and the multi-genome sets are grouped only when the
 // p-check needs them.  A possible repeat falls back to the exact hash path.
 template <int WPL>
-__device__ __forceinline__ void decide_dense_fast(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
-                                                  const Windows<1, WPL> &S, uint64_t r, ReadTotals &tot) {
+__device__ __forceinline__ int decide_dense_fast(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
+                                                 const Windows<1, WPL> &S, uint64_t r) {
     using C = FastCfg<WPL>;
     const int lane = lane_id();
     const uint32_t incm = S.inc;
@@ -731,10 +744,7 @@ __device__ __forceinline__ void decide_dense_fast(const AlignArgs &a, const WgCo
             const uint32_t b = 1u << (h & 31);
             dup |= atomicOr(&L.bm[h >> 5], b) & b;
         }
-    if (__ballot(dup != 0)) {
-        decide_general<1, WPL, true>(a, wc, L, S, r, tot);
-        return;
-    }
+    if (__ballot(dup != 0)) return decide_general<1, WPL, true>(a, wc, L, S, r);
     uint32_t multim = 0;
 #pragma unroll
     for (int j = 0; j < WPL; j++)
@@ -749,10 +759,7 @@ __device__ __forceinline__ void decide_dense_fast(const AlignArgs &a, const WgCo
         }
     const bool has_multi = __ballot(multim != 0) != 0;
     wave_sync();
-#ifdef PA_STATS
-    if (a.dbg_mode == 4) return;
-#endif
-    dense_core<WPL>(a, wc, L, r, S.qf, S.hr, tot, has_multi, [&]() -> uint32_t {
+    return dense_core<WPL>(a, wc, L, r, has_multi, [&]() -> uint32_t {
 #pragma unroll
         for (int e = 0; e < C::E; e++) {
             const int i = lane + 64 * e;
@@ -774,30 +781,45 @@ __device__ __forceinline__ void decide_dense_fast(const AlignArgs &a, const WgCo
 }
 
 template <int NW, int WPL, bool DENSE>
+__device__ __forceinline__ int classify_read(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
+                                             WaveQual<WPL> *Q, bool need_q, uint64_t r, uint32_t shift, uint32_t len,
+                                             const uint32_t (&sd)[FastCfg<WPL>::NDW],
+                                             const uint32_t (&qd)[FastCfg<WPL>::NDW], Windows<NW, WPL> &S,
+                                             ReadTotals &tot) {
+    if (!prep_read<NW, WPL, DENSE>(a, L, Q, need_q, shift, len, sd, qd, S, tot)) return OUT_DROP;
+#ifdef PA_STATS
+    tot.d_win += __popc(S.pend);
+    if (a.dbg_mode == 2) return OUT_UNMAPPED;
+#endif
+    resolve_read<NW, WPL>(a, L, shift, S, tot);
+#ifdef PA_STATS
+    if (a.dbg_mode == 3) return OUT_UNMAPPED;
+#endif
+    if (!__ballot(S.inc != 0)) return OUT_UNMAPPED;  // no k-mer references (src/kmer.py:516-517)
+    if constexpr (DENSE && NW == 1)
+        return decide_dense_fast<WPL>(a, wc, L, S, r);
+    else
+        return decide_general<NW, WPL, DENSE>(a, wc, L, S, r);
+}
+
+// One read; the read counters are updated in one place from the outcome (LLVM
+// merges per-branch increments of different fields into an indexed store,
+// which moves the counters to scratch memory).
+template <int NW, int WPL, bool DENSE>
 __device__ __forceinline__ void fast_read(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
                                           WaveQual<WPL> *Q, bool need_q, uint64_t r, uint32_t shift, uint32_t len,
                                           const uint32_t (&sd)[FastCfg<WPL>::NDW],
                                           const uint32_t (&qd)[FastCfg<WPL>::NDW], ReadTotals &tot) {
     Windows<NW, WPL> S;
-    if (!prep_read<NW, WPL, DENSE>(a, L, Q, need_q, shift, len, sd, qd, S, tot)) return;
-#ifdef PA_STATS
-    tot.d_win += __popc(S.pend);
-    if (a.dbg_mode == 2) return;
-#endif
-    resolve_read<NW, WPL>(a, L, shift, S, tot);
-#ifdef PA_STATS
-    if (a.dbg_mode == 3) return;
-#endif
-    if (!__ballot(S.inc != 0)) {
-        tot.qf += S.qf;
-        tot.hr += S.hr;
-        if (lane_id() == 0) tot.unm++;  // no k-mer references -> UNMAPPED (src/kmer.py:516-517)
-        return;
-    }
-    if constexpr (DENSE && NW == 1)
-        decide_dense_fast<WPL>(a, wc, L, S, r, tot);
-    else
-        decide_general<NW, WPL, DENSE>(a, wc, L, S, r, tot);
+    const int out = classify_read<NW, WPL, DENSE>(a, wc, L, Q, need_q, r, shift, len, sd, qd, S, tot);
+    // a dropped read has no window counts; a deferred one is counted by the exact kernel
+    const bool counted = out != OUT_DROP && out != OUT_DEFER;
+    tot.qf += counted ? S.qf : 0u;
+    tot.hr += counted ? S.hr : 0u;
+    tot.unique += out == OUT_UNIQUE ? 1u : 0u;
+    tot.mapped += (out == OUT_UNIQUE || out == OUT_AMB) ? 1u : 0u;
+    tot.unm += out == OUT_UNMAPPED ? 1u : 0u;
+    tot.drop += out == OUT_DROP ? 1u : 0u;
 }
 
 template <int NW, int WPL, bool DENSE>
@@ -875,7 +897,7 @@ __global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
 #endif
     if (lane == 0) {
         if (tot.unique) atomicAdd(&a.stats[0], (unsigned long long)tot.unique);
-        if (tot.amb) atomicAdd(&a.stats[1], (unsigned long long)tot.amb);
+        if (tot.mapped > tot.unique) atomicAdd(&a.stats[1], (unsigned long long)(tot.mapped - tot.unique));
         if (tot.unm) atomicAdd(&a.stats[2], (unsigned long long)tot.unm);
         if (tot.drop) atomicAdd(&a.stats[3], (unsigned long long)tot.drop);
         if (qf_w && has_mkq) atomicAdd(&a.stats[4], (unsigned long long)qf_w);
