@@ -42,10 +42,14 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, stats: bool = False) -> str:
-    build_dir = BUILD + ("_stats" if stats else "")
-    lib = os.path.join(HERE, "libpa_stats.so") if stats else LIB
-    flags = FLAGS + (["-DPA_STATS"] if stats else [])
+def build(force: bool = False, verbose: bool = False, stats: bool = False, variant: str = "",
+          defines=()) -> str:
+    """Build libpa.so; `stats` or a named `variant` (with extra -D defines) go to
+    their own build directory and libpa_<name>.so (experiments, PA_LIBRARY)."""
+    name = "stats" if stats else variant
+    build_dir = BUILD + (f"_{name}" if name else "")
+    lib = os.path.join(HERE, f"libpa_{name}.so") if name else LIB
+    flags = FLAGS + (["-DPA_STATS"] if stats else []) + [f"-D{d}" for d in defines]
     os.makedirs(build_dir, exist_ok=True)
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "pa.h")]
@@ -78,4 +82,7 @@ def build(force: bool = False, verbose: bool = False, stats: bool = False) -> st
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, stats="--stats" in sys.argv))
+    var = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--variant=")]
+    defs = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--define=")]
+    print(build(force="--force" in sys.argv, verbose=True, stats="--stats" in sys.argv,
+                variant=var[0] if var else "", defines=defs))

@@ -64,6 +64,7 @@ struct AlignArgs {
     const uint32_t *tile_cls;       // genome tiling (pa_index.hip); tile_n == 0: none
     const uint64_t *tile_pk;
     uint64_t tile_n;
+    const uint64_t *goff;           // genome start positions [G + 1] (concatenated coordinates)
     int walk_rounds;
     int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
     const uint8_t *seq;
@@ -507,6 +508,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.class_mask = idx->class_mask;
     a.tile_cls = idx->tile_cls;
     a.tile_pk = idx->tile_pk;
+    a.goff = idx->goff;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
     if (const char *e = std::getenv("PA_WALK_ROUNDS")) a.walk_rounds = std::atoi(e);

@@ -24,15 +24,17 @@
 //   hash (G > 64): per-read LDS genome hash; reads whose genome union overflows
 //     it are deferred to k_align_exact.
 
+#ifndef PA_HS_PER_WPL
+#define PA_HS_PER_WPL 128
+#endif
 template <int WPL>
 struct FastCfg {
-    static constexpr int HS = 128 * WPL;               // hash entries per wave (>= 2 x windows)
+    static constexpr int HS = PA_HS_PER_WPL * WPL;     // hash entries per wave (>= windows)
     static constexpr int E = HS / 64;                  // entries owned per lane
     static constexpr int LCAP = 64 * WPL + 64;         // longest read handled (k <= 63)
     static constexpr int NDW = (LCAP + 8 + 255) / 256; // staged dwords per lane
     static constexpr int PW = NDW * 8 + 2;             // packed words (32 staged bases each)
     static constexpr int BW = NDW * 4 + 2;             // non-ACGT bitmap words (64 staged bases each)
-    static constexpr int BMW = 128;                    // distinct-k-mer filter: 4096 bits
 };
 
 template <int WPL>
@@ -49,7 +51,6 @@ struct __align__(16) WaveLds {
     uint32_t hB_min[C::HS];   // first window of the set
     uint32_t gcnt[64];        // dense path: specific k-mers per genome
     uint32_t gmin[64];        //   and the first window of each
-    uint32_t bm[C::BMW];      // dense path: hash bitmap of the read's k-mers (repeat test)
 };
 
 template <int WPL>
@@ -116,10 +117,11 @@ __device__ __forceinline__ bool bit(uint32_t m, int i) { return (m >> i) & 1u; }
 // L.gcnt / L.gmin hold the specific counts / first windows per genome.  The
 // multi-genome sets of the read (membership mask, distinct k-mers, first window
 // in L.hA_key / hA_v / hA_v2) are only needed for the p-check, so they come from
-// `multi()` on demand (it returns their number).
-template <int WPL, typename MultiFn>
+// `multi()` on demand (it returns their number); `settled(gstar)` may first
+// prove that no genome can exceed G*'s total by more than p.
+template <int WPL, typename SettledFn, typename MultiFn>
 __device__ __forceinline__ int dense_core(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L, uint64_t r,
-                                          bool has_multi, MultiFn multi) {
+                                          bool has_multi, SettledFn settled, MultiFn multi) {
     const int lane = lane_id();
     const uint32_t G = a.G;
     const uint32_t cnt = L.gcnt[lane], smin = L.gmin[lane];
@@ -140,7 +142,7 @@ __device__ __forceinline__ int dense_core(const AlignArgs &a, const WgCounters &
         if (cnt > 0) count_genome(a, wc, lane, false, 1, first_key(read_idx, rank));
         return OUT_AMB;
     }
-    const uint32_t nmulti = (a.prm.p < 0 || !has_multi) ? 0u : multi();
+    const uint32_t nmulti = (a.prm.p < 0 || !has_multi || settled(gstar)) ? 0u : multi();
     if (nmulti == 0) {
         if (lane == 0) count_genome(a, wc, gstar, true, 1, first_key(read_idx, 0));
         return OUT_UNIQUE;
@@ -213,7 +215,7 @@ __device__ __forceinline__ int decide_dense(const AlignArgs &a, const WgCounters
     }
     // hA (distinct k-mer slots) is dead from here on: the multi list may reuse it
     const uint32_t nmulti = dense_multi_list<WPL>(a, L);
-    return dense_core<WPL>(a, wc, L, r, nmulti > 0, [&]() { return nmulti; });
+    return dense_core<WPL>(a, wc, L, r, nmulti > 0, [](int) { return false; }, [&]() { return nmulti; });
 }
 
 // ---- hash decision (G > 64) --------------------------------------------------
@@ -382,6 +384,8 @@ struct Windows {
     uint64_t slot[NW == 1 ? 1 : WPL];  // table slot = k-mer identity for multi-word keys
     uint32_t cls[WPL];
     uint32_t pend, inc, qf, hr;
+    uint32_t walk;  // windows resolved by the genome walk
+    uint32_t ga;    // genome of the walk's anchor when its seed was specific, else NONE
 };
 
 // ASCII -> 2-bit codes of four bases at once: ((c >> 1) ^ (c >> 2)) & 3 maps
@@ -420,8 +424,8 @@ __device__ __forceinline__ bool prep_read(const AlignArgs &a, WaveLds<WPL> &L, W
     if (DENSE && NW == 1) {
         L.gcnt[lane] = 0;
         L.gmin[lane] = NONE;
-        L.bm[lane] = 0;
-        L.bm[lane + 64] = 0;
+#pragma unroll
+        for (int e = 0; e < C::E; e++) L.hA_key[C::E * lane + e] = EMPTY;  // contiguous: wide stores
     }
     // ---- 2-bit pack (4 bases per lane and staged dword) + non-ACGT test
     uint32_t badany = 0;
@@ -474,7 +478,8 @@ __device__ __forceinline__ bool prep_read(const AlignArgs &a, WaveLds<WPL> &L, W
     }
     // ---- windows: quality gate, key (src/kmer.py:419-429)
     const int64_t mkq_k = (int64_t)a.prm.mkq * k;
-    S.pend = S.inc = S.qf = S.hr = 0;
+    S.pend = S.inc = S.qf = S.hr = S.walk = 0;
+    S.ga = NONE;
 #pragma unroll
     for (int j = 0; j < WPL; j++) {
         const uint32_t w = lane + 64 * j;
@@ -612,9 +617,18 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
             const uint64_t b1 = __ballot(sf && scls < a.G), b2 = __ballot(sf);
             if (!b2) continue;
             const int l = (int)__builtin_ctzll(b1 ? b1 : b2);
+            const uint32_t ga = b1 ? __builtin_amdgcn_readlane(scls, l) : NONE;
             const int64_t A = (int64_t)__builtin_amdgcn_readlane(stp, l) - (int64_t)__builtin_amdgcn_readlane(sw, l);
             const int64_t g0 = A - (int64_t)shift;  // genome position of staged base 0
             if (g0 < 0) continue;
+            // walk bits (and the anchor genome) only in round 0 and only inside the
+            // anchor genome's own range: a read may match across a genome boundary
+            uint64_t gs = 0, ge = 0;
+            if (round == 0 && ga != NONE) {
+                S.ga = ga;
+                gs = a.goff[ga];
+                ge = a.goff[ga + 1];
+            }
 #ifdef PA_STATS
             if (lane == 0) tot.d_anchor++;
 #endif
@@ -635,6 +649,8 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
                     tot.d_walk++;
 #endif
                     S.pend &= ~(1u << j);
+                    const uint64_t t = (uint64_t)(A + lane + 64 * j);
+                    if (t >= gs && t < ge) S.walk |= 1u << j;
                     resolve(j, tc[j]);
                 }
         }
@@ -725,33 +741,35 @@ __device__ __forceinline__ int decide_general(const AlignArgs &a, const WgCounte
         return decide_hash<WPL>(a, wc, L, r);
 }
 
-// Dense decision for single-word keys.  Reads almost never hold a k-mer twice,
-// so a 4096-bit hash bitmap (atomic OR with return) proves the read's included
-// k-mers distinct; then every specific k-mer goes straight to its genome's
-// counter and first window, and the multi-genome sets are grouped only when the
-// p-check needs them.  A possible repeat falls back to the exact hash path.
+// Dense decision for single-word keys.  Distinct k-mers (quirk 3) by one LDS
+// hash insert per window: the window whose insert lands counts its k-mer once,
+// every window of a k-mer still takes part in the first-window minimum (all of
+// them share its genome set, so the minimum over all windows is the minimum
+// over the k-mer's first windows).  Specific k-mers go straight to their
+// genome's counter and first window; the multi-genome sets are grouped only
+// when the p-check needs them.
 template <int WPL>
 __device__ __forceinline__ int decide_dense_fast(const AlignArgs &a, const WgCounters &wc, WaveLds<WPL> &L,
                                                  const Windows<1, WPL> &S, uint64_t r) {
     using C = FastCfg<WPL>;
     const int lane = lane_id();
     const uint32_t incm = S.inc;
-    uint32_t dup = 0;
+    uint32_t firstm = 0, multim = 0;
 #pragma unroll
     for (int j = 0; j < WPL; j++)
         if (bit(incm, j)) {
-            const uint32_t h = (uint32_t)((S.key[j].w[0] * 0x9E3779B97F4A7C15ull) >> 52);
-            const uint32_t b = 1u << (h & 31);
-            dup |= atomicOr(&L.bm[h >> 5], b) & b;
-        }
-    if (__ballot(dup != 0)) return decide_general<1, WPL, true>(a, wc, L, S, r);
-    uint32_t multim = 0;
-#pragma unroll
-    for (int j = 0; j < WPL; j++)
-        if (bit(incm, j)) {
+            const uint64_t key = S.key[j].w[0];
+            uint32_t p = lds_hash_slot(key, C::HS - 1);
+            for (;;) {
+                const uint64_t old = atomicCAS((unsigned long long *)&L.hA_key[p], (unsigned long long)EMPTY,
+                                               (unsigned long long)key);
+                if (old == EMPTY) firstm |= 1u << j;
+                if (old == EMPTY || old == key) break;
+                p = (p + 1) & (C::HS - 1);
+            }
             const uint32_t c = S.cls[j];
             if (c < a.G) {
-                atomicAdd(&L.gcnt[c], 1u);
+                if (bit(firstm, j)) atomicAdd(&L.gcnt[c], 1u);
                 atomicMin(&L.gmin[c], (uint32_t)(lane + 64 * j));
             } else {
                 multim |= 1u << j;
@@ -759,7 +777,31 @@ __device__ __forceinline__ int decide_dense_fast(const AlignArgs &a, const WgCou
         }
     const bool has_multi = __ballot(multim != 0) != 0;
     wave_sync();
-    return dense_core<WPL>(a, wc, L, r, has_multi, [&]() -> uint32_t {
+#ifdef PA_STATS
+    if (a.dbg_mode == 4) return OUT_AMB;
+#endif
+    // p-check bound: total[g] - total[G*] <= #distinct k-mers whose set lacks G*;
+    // if that is <= p no demotion is possible (src/kmer.py:469-480).  Windows the
+    // genome walk resolved lie in the anchor genome, so when that is G* they
+    // contain it without a look at their set.
+    auto settled = [&](int gstar) -> bool {
+        uint32_t lack = 0;
+#pragma unroll
+        for (int j = 0; j < WPL; j++)
+            if (bit(firstm, j)) {
+                const uint32_t c = S.cls[j];
+                bool has;
+                if (c < a.G)
+                    has = c == (uint32_t)gstar;
+                else if (bit(S.walk, j) && S.ga == (uint32_t)gstar)
+                    has = true;
+                else
+                    has = (a.class_mask[c - a.G] >> gstar) & 1;
+                lack += has ? 0u : 1u;
+            }
+        return (int64_t)wave_sum(lack) <= (int64_t)a.prm.p;
+    };
+    return dense_core<WPL>(a, wc, L, r, has_multi, settled, [&]() -> uint32_t {
 #pragma unroll
         for (int e = 0; e < C::E; e++) {
             const int i = lane + 64 * e;
@@ -772,7 +814,7 @@ __device__ __forceinline__ int decide_dense_fast(const AlignArgs &a, const WgCou
         for (int j = 0; j < WPL; j++)
             if (bit(multim, j)) {
                 const uint32_t p = lds_insert32(L.hB_key, C::HS, S.cls[j]);
-                atomicAdd(&L.hB_cnt[p], 1u);
+                if (bit(firstm, j)) atomicAdd(&L.hB_cnt[p], 1u);
                 atomicMin(&L.hB_min[p], (uint32_t)(lane + 64 * j));
             }
         wave_sync();

@@ -326,3 +326,70 @@ def test_edge_cases():
     N.align(index, N.Reads.upload(seq, qual, off), N.Params.make(), 0, res)
     o = oix.align(seq.tobytes(), qual.tobytes(), off, detail=False)
     assert res.fetch()[0].tolist() == o.stats.tolist()
+
+
+def _walk_adversarial_case(seed, n_genomes, k):
+    """Genomes and reads aimed at the genome walk of the fast kernel: tandem
+    repeats (a k-mer several times in one read), reads across the junction of
+    two consecutive genomes (a walk could run on into the next genome), reads
+    at the very start of the first genome, copies of one genome stretch in
+    several genomes, and N runs next to repeats."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    gens = []
+    shared = acgt[rng.integers(0, 4, 400)]
+    for g in range(n_genomes):
+        parts = [acgt[rng.integers(0, 4, int(rng.integers(300, 900)))]]
+        unit = acgt[rng.integers(0, 4, int(rng.integers(1, 9)))]
+        parts.append(np.tile(unit, 200 // len(unit) + 1)[:int(rng.integers(40, 200))])  # tandem repeat
+        parts.append(acgt[rng.integers(0, 4, 300)])
+        if g % 3 == 0:
+            parts.append(shared)  # one stretch in several genomes
+        parts.append(np.full(int(rng.integers(1, 4)), ord("N"), dtype=np.uint8))
+        parts.append(np.tile(unit, 20)[:60])
+        parts.append(acgt[rng.integers(0, 4, int(rng.integers(200, 500)))])
+        gens.append(np.concatenate(parts))
+    reads = []
+    cat = np.concatenate(gens)
+    starts = np.cumsum([0] + [len(g) for g in gens])
+    for i in range(3000):
+        kind = i % 4
+        L = int(rng.integers(k, 150)) if i % 5 else int(rng.integers(1, k + 3))
+        if kind == 0:  # across the junction of genomes g and g+1
+            g = int(rng.integers(0, n_genomes - 1))
+            st = int(starts[g + 1]) - int(rng.integers(1, L + 1))
+        elif kind == 1:  # the first bases of the first genome
+            st = int(rng.integers(0, 4))
+        else:
+            st = int(rng.integers(0, len(cat) - L))
+        r = cat[st:st + L].copy()
+        bad = r == ord("N")
+        r[bad] = acgt[rng.integers(0, 4, int(bad.sum()))]
+        err = rng.random(L) < 0.01
+        r[err] = acgt[rng.integers(0, 4, int(err.sum()))]
+        reads.append(r)
+    off = np.zeros(len(reads) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r) for r in reads])
+    s = np.concatenate(reads)
+    q = np.clip(rng.normal(60, 8, len(s)).round(), 35, 74).astype(np.uint8)
+    return gens, s, q, off
+
+
+@pytest.mark.parametrize("n_genomes,k", [(6, 31), (12, 21), (90, 25), (5, 13)])
+def test_walk_adversarial_vs_oracle(n_genomes, k):
+    gens, s, q, off = _walk_adversarial_case(1000 + n_genomes + k, n_genomes, k)
+    index = N.Index(gens, k)
+    oix = O.OracleIndex(gens, k)
+    assert index.n_kmers == oix.n_kmers
+    reads = N.Reads.upload(s, q, off)
+    for ps in (dict(), dict(m=0, p=0), dict(p=3), dict(p=-1), dict(mg=2), dict(mrq=58, mkq=60)):
+        full = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+        result = N.Result(index)
+        N.align(index, reads, N.Params.make(full["m"], full["p"], full["mrq"], full["mkq"], full["mg"]), 777, result)
+        stats, uq, am, fk = result.fetch()
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"], mkq=full["mkq"],
+                      mg=full["mg"], read_base=777, detail=False)
+        assert stats.tolist() == o.stats.tolist(), ps
+        assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
+        ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+        assert fk.tolist() == ofk.tolist(), ps
