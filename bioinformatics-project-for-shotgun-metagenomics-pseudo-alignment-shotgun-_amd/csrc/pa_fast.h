@@ -555,23 +555,35 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
     if constexpr (NW == 1) {
         // One lane per probe: keys are re-extracted from the packed read in LDS,
         // so the probing lanes need not own the windows they probe.
+        // Linear probing a 64-B line (4 slots) per step: cap is a multiple of 4
+        // and the table 64-B aligned, so the slots from pos to the line's end
+        // come in one memory request, and most searches -- hits and misses --
+        // end in their first line.
         auto probe_one = [&](bool act, uint32_t w, uint32_t &cls, uint32_t &tpos) -> bool {
-            Key<1> key = extract_key<1>(L.packed, w + shift, k);
+            const Key<1> key = extract_key<1>(L.packed, w + shift, k);
             uint64_t pos = act ? home_of<1>(key, key_hash(key), a.home) : 0;
             bool found = false;
             while (__ballot(act)) {
                 if (act) {
-                    const Slot<1> s = table[pos];
-                    if (s.key[0] == EMPTY) {
-                        act = false;
-                    } else if (s.key[0] == key.w[0]) {
-                        act = false;
-                        found = true;
-                        cls = s.cls;
-                        tpos = s.tpos;
-                    } else {
-                        pos = (pos + 1 == a.cap) ? 0 : pos + 1;
+                    const uint64_t base = pos & ~3ull;
+                    Slot<1> s[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) s[i] = table[base + i];
+                    bool done = false;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        if (done || base + i < pos) continue;
+                        if (s[i].key[0] == EMPTY) {
+                            done = true;
+                        } else if (s[i].key[0] == key.w[0]) {
+                            done = true;
+                            found = true;
+                            cls = s[i].cls;
+                            tpos = s[i].tpos;
+                        }
                     }
+                    act = !done;
+                    pos = (base + 4 == a.cap) ? 0 : base + 4;
                 }
             }
             return found;

@@ -744,7 +744,8 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     uint64_t cap_mult = 2;
     if (const char *e = std::getenv("PA_CAP_MULT")) cap_mult = std::max(2, std::atoi(e));
     uint64_t cap = std::max<uint64_t>(64, cap_mult * windows + 64);
-    if (m > 0) cap = (cap + R - 1) / R * R;
+    const uint64_t align = std::max<uint64_t>(4, R);  // whole 64-B lines (the fast kernel probes a line per step)
+    cap = (cap + align - 1) / align * align;
     idx->cap = cap;
     idx->home = pad::HomeCfg{cap, m > 0 ? cap / R : 0, R, (int)std::max<int64_t>(k, 0), m};
     const int sb = slot_bytes(idx->nw);
