@@ -66,6 +66,7 @@ struct AlignArgs {
     uint64_t tile_n;
     const uint64_t *goff;           // genome start positions [G + 1] (concatenated coordinates)
     int walk_rounds;
+    uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
     int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
     const uint8_t *seq;
     const uint8_t *qual;
@@ -78,11 +79,18 @@ struct AlignArgs {
     unsigned long long *uniq;    // [G]
     unsigned long long *amb;     // [G]
     unsigned long long *first;   // [G]
-    // deferral
+    // deferral to the exact kernel
     uint32_t *queue;
     unsigned long long *qcount;
     unsigned long long *deferred_total;
-    unsigned long long *dbg;  // PA_STATS builds: [0] windows [1] probed [2] walk-resolved [3] anchors
+    // lane kernel: reads it leaves to the wave kernel
+    uint32_t *queue_hard;
+    unsigned long long *queue_hard_count;
+    // wave kernel input: a list of read indices (null: reads 0 .. n-1)
+    const uint32_t *rlist;
+    const unsigned long long *rlist_count;
+    unsigned long long *dbg;  // PA_STATS builds: [0] windows [1] probed [2] walk-resolved [3] anchors (wave
+                              // kernel), [4..11] lane kernel: reads left to the wave kernel, by reason
 };
 
 __device__ __forceinline__ uint64_t first_key(uint64_t read, uint32_t rank) { return (read << 20) | rank; }
@@ -110,6 +118,7 @@ __device__ __forceinline__ void count_genome(const AlignArgs &a, const WgCounter
 }
 
 #include "pa_fast.h"
+#include "pa_lane.h"
 
 
 // ---------------------------------------------------------------------------
@@ -469,6 +478,22 @@ pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
     return PA_OK;
 }
 
+pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
+    const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
+    const size_t shm = a.G <= kLdsGenomeCap ? (size_t)a.G * 12 : 0;
+    auto kern = need_q ? k_align_lane<true> : k_align_lane<false>;
+    int per_cu = 0, dev = 0, cus = 256;
+    PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, shm));
+    PA_HIP(hipGetDevice(&dev));
+    PA_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const uint64_t want = (a.n + kBlock - 1) / kBlock;
+    const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)cus;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), shm, st, a);
+    PA_HIP(hipGetLastError());
+    return PA_OK;
+}
+
 template <int NW>
 pa_status launch_fast_wpl(const AlignArgs &a, int wpl, hipStream_t st) {
     size_t shm = fast_lds_bytes(a.G, wpl, (a.prm.flags & (F_MRQ | F_MKQ)) != 0);
@@ -511,6 +536,8 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.goff = idx->goff;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
+    a.lane_maxpend = 64;
+    if (const char *e = std::getenv("PA_LANE_MAXPEND")) a.lane_maxpend = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("PA_WALK_ROUNDS")) a.walk_rounds = std::atoi(e);
     if (const char *e = std::getenv("PA_DBG_MODE")) a.dbg_mode = std::atoi(e);
     a.seq = r->seq;
@@ -576,9 +603,11 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     if (r->n == 0) return PA_OK;
     if (idx->queue_cap < r->n) {
         hipFree(idx->queue);
-        idx->queue = nullptr;
+        hipFree(idx->queue_hard);
+        idx->queue = idx->queue_hard = nullptr;
         idx->queue_cap = 0;
         PA_HIP(hipMalloc(&idx->queue, r->n * 4));
+        PA_HIP(hipMalloc(&idx->queue_hard, r->n * 4));
         idx->queue_cap = r->n;
     }
     AlignArgs a = make_args(idx, r, p, base);
@@ -593,7 +622,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     a.dbg = (unsigned long long *)idx->counters + 4;
     PA_HIP(hipMemsetAsync(idx->counters, 0, 8, st));
 #ifdef PA_STATS
-    PA_HIP(hipMemsetAsync(a.dbg, 0, 32, st));
+    PA_HIP(hipMemsetAsync(a.dbg, 0, 104, st));
 #endif
     ExactArgs x{};
     unsigned egrid = 0;
@@ -601,21 +630,33 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     x.a = a;
     x.detail = 0;
     const bool fast_ok = idx->k > 0 && idx->nw <= 2 && idx->n_kmers > 0;
+    // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
+    const char *no_lane = std::getenv("PA_NO_LANE");
+    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && !(no_lane && no_lane[0] == '1');
     if (fast_ok) {
         const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
         const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4
+        hipEvent_t e0 = nullptr, e1 = nullptr;
         if (idx->profile) {
-            hipEvent_t e0, e1;
             PA_HIP(hipEventCreate(&e0));
             PA_HIP(hipEventCreate(&e1));
             PA_HIP(hipEventRecord(e0, st));
-            idx->ev_start.push_back(e0);
-            PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
-            PA_HIP(hipEventRecord(e1, st));
-            idx->ev_stop.push_back(e1);
-        } else {
-            PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
         }
+        if (lane_ok) {
+            a.queue_hard = idx->queue_hard;
+            a.queue_hard_count = (unsigned long long *)idx->counters + 3;
+            PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));
+            PA_TRY(launch_lane(a, st));
+            a.rlist = idx->queue_hard;
+            a.rlist_count = a.queue_hard_count;
+        }
+        PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
+        if (idx->profile) {
+            PA_HIP(hipEventRecord(e1, st));
+            idx->ev_start.push_back(e0);
+            idx->ev_stop.push_back(e1);
+        }
+        x.a = a;
         x.use_queue = 1;
     } else {
         x.use_queue = 0;
@@ -623,11 +664,13 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     launch_exact_nw(idx->nw, x, egrid, st);
     PA_HIP(hipGetLastError());
 #ifdef PA_STATS
-    unsigned long long d[4];
-    PA_HIP(hipMemcpyAsync(d, a.dbg, 32, hipMemcpyDeviceToHost, st));
+    unsigned long long d[17];
+    PA_HIP(hipMemcpyAsync(d, idx->counters, 136, hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
-    fprintf(stderr, "[pa_stats] reads %llu windows %llu probed %llu walk %llu anchors %llu\n",
-            (unsigned long long)r->n, d[0], d[1], d[2], d[3]);
+    fprintf(stderr, "[pa_stats] reads %llu lane-hard %llu exact %llu | wave kernel: windows %llu probed %llu walk %llu anchors %llu\n",
+            (unsigned long long)r->n, d[3], d[0], d[4], d[5], d[6], d[7]);
+    fprintf(stderr, "[pa_stats] lane hard reasons: long %llu mkq %llu bad %llu no-anchor %llu range %llu mismatches %llu rep %llu found %llu pending %llu\n",
+            d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], d[16]);
 #endif
     return PA_OK;
 }

@@ -651,7 +651,10 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
             for (int j = 0; j < WPL; j++) {
                 tc[j] = NONE;
                 const uint64_t t = (uint64_t)(A + lane + 64 * j);
-                if (bit(S.pend, j) && t < a.tile_n) tc[j] = a.tile_cls[t];
+                if (bit(S.pend, j) && t < a.tile_n) {
+                    const uint32_t v = a.tile_cls[t];
+                    tc[j] = v == NONE ? NONE : (v & ~PA_TILE_REP);
+                }
             }
             wave_sync();
 #pragma unroll
@@ -876,8 +879,11 @@ __device__ __forceinline__ void fast_read(const AlignArgs &a, const WgCounters &
     tot.drop += out == OUT_DROP ? 1u : 0u;
 }
 
+#ifndef PA_FAST_MIN_WAVES
+#define PA_FAST_MIN_WAVES 1
+#endif
 template <int NW, int WPL, bool DENSE>
-__global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
+__global__ __launch_bounds__(kBlock, PA_FAST_MIN_WAVES) void k_align_fast(AlignArgs a) {
     using C = FastCfg<WPL>;
     extern __shared__ __align__(16) unsigned char smem[];
     const int lane = lane_id();
@@ -901,32 +907,38 @@ __global__ __launch_bounds__(kBlock) void k_align_fast(AlignArgs a) {
     }
     __syncthreads();
 
-    // contiguous chunk of reads for this wave; the bytes of read r+1 are loaded
-    // while read r is classified (and the offset of read r+2)
+    // contiguous chunk of reads (or of the read list) for this wave; the bytes of
+    // the next read are loaded while the current one is classified
+    const uint64_t nq = a.rlist ? (uint64_t)*a.rlist_count : a.n;
     const uint64_t nw = (uint64_t)gridDim.x * kWaves, gw = (uint64_t)blockIdx.x * kWaves + wid;
-    const uint64_t rb = a.n * gw / nw, re = a.n * (gw + 1) / nw;
+    const uint64_t qb = nq * gw / nw, qe = nq * (gw + 1) / nw;
     ReadTotals tot;
-    if (rb < re) {
-        uint64_t o_cur = a.off[rb], o_nxt = a.off[rb + 1];
+    if (qb < qe) {
+        uint64_t r = a.rlist ? a.rlist[qb] : qb;
+        uint64_t o_cur = a.off[r], o_end = a.off[r + 1];
         uint32_t sd[C::NDW], qd[C::NDW];
         load_stage<WPL>(a.seq, o_cur, sd);
         if (need_q) load_stage<WPL>(a.qual, o_cur, qd);
-        for (uint64_t r = rb; r < re; r++) {
-            const uint64_t o_nn = (r + 2 <= a.n) ? a.off[r + 2] : o_nxt;
+        for (uint64_t q = qb; q < qe; q++) {
+            uint64_t r_n = 0, o_n = 0, e_n = 0;
             uint32_t sn[C::NDW], qn[C::NDW];
-            if (r + 1 < re) {  // prefetch the next read while this one is classified
-                load_stage<WPL>(a.seq, o_nxt, sn);
-                if (need_q) load_stage<WPL>(a.qual, o_nxt, qn);
+            if (q + 1 < qe) {  // prefetch the next read while this one is classified
+                r_n = a.rlist ? a.rlist[q + 1] : q + 1;
+                o_n = a.off[r_n];
+                e_n = a.off[r_n + 1];
+                load_stage<WPL>(a.seq, o_n, sn);
+                if (need_q) load_stage<WPL>(a.qual, o_n, qn);
             }
-            const uint32_t len = (uint32_t)(o_nxt - o_cur);
+            const uint32_t len = (uint32_t)(o_end - o_cur);
             const uint32_t W = (len >= (uint32_t)a.k) ? len - a.k + 1 : 0;
             if (W > 64u * WPL || len > (uint32_t)(C::LCAP - 8)) {
                 if (lane == 0) a.queue[atomicAdd(a.qcount, 1ull)] = (uint32_t)r;  // the exact kernel takes it
             } else {
                 fast_read<NW, WPL, DENSE>(a, wc, L, Q, need_q, r, (uint32_t)(o_cur & 3), len, sd, qd, tot);
             }
-            o_cur = o_nxt;
-            o_nxt = o_nn;
+            r = r_n;
+            o_cur = o_n;
+            o_end = e_n;
 #pragma unroll
             for (int j = 0; j < C::NDW; j++) {
                 sd[j] = sn[j];

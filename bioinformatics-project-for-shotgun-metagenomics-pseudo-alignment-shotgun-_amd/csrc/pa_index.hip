@@ -406,6 +406,37 @@ __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, u
     }
 }
 
+// Local-repeat flags: bit 31 (PA_TILE_REP) of tile_cls[t] marks an indexed
+// window whose k-mer starts again at an indexed window within the next
+// kTileRepDist positions.  A read walked along the genomes then holds a k-mer
+// twice only if one of its walked windows carries the flag (its windows are
+// < kTileRepDist apart), which the lane kernel (pa_lane.h) tests instead of
+// deduplicating.  One block per 256 positions, keys staged in LDS.
+constexpr int kTileRepDist = 127;
+__global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ pk, uint32_t *tile_cls, uint64_t n,
+                                                  int k) {
+    __shared__ uint64_t keys[256 + kTileRepDist];
+    __shared__ uint32_t valid[256 + kTileRepDist];
+    const int sh = 64 - 2 * k;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256; b < n; b += (uint64_t)gridDim.x * 256) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 256 + kTileRepDist; i += 256) {
+            const uint64_t t = b + i;
+            const bool ok = t < n && tile_cls[t] != NONE;
+            valid[i] = ok;
+            keys[i] = ok ? (get64_at(pk, 2 * t) >> sh) : 0;
+        }
+        __syncthreads();
+        const uint64_t t = b + threadIdx.x;
+        if (t < n && valid[threadIdx.x]) {
+            const uint64_t me = keys[threadIdx.x];
+            bool rep = false;
+            for (int d = 1; d <= kTileRepDist; d++) rep |= valid[threadIdx.x + d] && keys[threadIdx.x + d] == me;
+            if (rep) tile_cls[t] |= PA_TILE_REP;
+        }
+    }
+}
+
 // ---- EXTSIM statistics ------------------------------------------------------
 
 template <int NW>
@@ -637,6 +668,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         idx->class_entries = entries;
         idx->device_bytes += n_multi * 12 + std::max<uint64_t>(entries, 1) * 4;
     }
+    if (idx->tile_n > 0 && (uint64_t)G + idx->class_entries >= PA_TILE_REP) idx->tile_n = 0;  // ids need bit 31
     if (idx->tile_n > 0) {  // step 6: genome tiling
         const uint64_t n = idx->tile_n, nwords = n / 32 + 32;  // padded: the walk reads up to 18 words past a position
         B_HIP(hipMalloc(&idx->tile_cls, n * 4));
@@ -651,6 +683,9 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_tile_cls<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
                                idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls);
         }
+        if (k <= 31)
+            hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
+                               st, idx->tile_pk, idx->tile_cls, n, k);
         B_HIP(hipGetLastError());
         B_HIP(hipStreamSynchronize(st));
         idx->device_bytes += n * 4 + nwords * 8;
@@ -699,6 +734,7 @@ void index_release(pa_index *idx) {
     idx->tile_pk = nullptr;
     hipFree(idx->ws.ptr);
     hipFree(idx->queue);
+    hipFree(idx->queue_hard);
     hipFree(idx->counters);
     for (auto e : idx->ev_start) hipEventDestroy(e);
     for (auto e : idx->ev_stop) hipEventDestroy(e);
@@ -753,8 +789,8 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
     PA_HIP(hipMalloc(&idx->codes, std::max<uint64_t>(total, 1)));
     PA_HIP(hipMalloc(&idx->goff, (n + 1) * 8));
-    PA_HIP(hipMalloc(&idx->counters, 8 * 8));
-    PA_HIP(hipMemsetAsync(idx->counters, 0, 8 * 8, st));
+    PA_HIP(hipMalloc(&idx->counters, 24 * 8));
+    PA_HIP(hipMemsetAsync(idx->counters, 0, 24 * 8, st));
     PA_HIP(hipMemcpyAsync(idx->goff, idx->h_goff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
     idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
     if (total > 0) {

@@ -85,9 +85,11 @@ struct pa_index {
     uint64_t device_bytes = 0;
     // align scratch
     pa::Workspace ws;
-    uint32_t *queue = nullptr;         // deferred read indices
+    uint32_t *queue = nullptr;         // read indices deferred to the exact kernel
+    uint32_t *queue_hard = nullptr;    // read indices the lane kernel leaves to the wave kernel
     uint64_t queue_cap = 0;
-    uint64_t *counters = nullptr;      // [0] queue length, [1] deferred total, [2] error flags
+    uint64_t *counters = nullptr;      // [0] queue length, [1] deferred total, [2] error flags, [3] hard reads,
+                                       // [4..23] PA_STATS counters
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
