@@ -480,8 +480,9 @@ pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
 
 pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
-    const size_t shm = a.G <= kLdsGenomeCap ? (size_t)a.G * 12 : 0;
+    const size_t shm = lane_lds_bytes(a.G);
     auto kern = need_q ? k_align_lane<true> : k_align_lane<false>;
+    if (shm > 64 * 1024) PA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     int per_cu = 0, dev = 0, cus = 256;
     PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, shm));
     PA_HIP(hipGetDevice(&dev));
@@ -536,7 +537,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.goff = idx->goff;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
-    a.lane_maxpend = 64;
+    a.lane_maxpend = 96;
     if (const char *e = std::getenv("PA_LANE_MAXPEND")) a.lane_maxpend = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("PA_WALK_ROUNDS")) a.walk_rounds = std::atoi(e);
     if (const char *e = std::getenv("PA_DBG_MODE")) a.dbg_mode = std::atoi(e);

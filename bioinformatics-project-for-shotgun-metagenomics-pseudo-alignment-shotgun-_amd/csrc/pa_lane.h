@@ -16,8 +16,12 @@
 //   3. the read's packed bases XOR the genome's from the anchor on give the
 //      mismatching bases; every window without a mismatch whose genome window
 //      is indexed resolves to tile_cls[anchor + w], exactly the table's class;
-//   4. the other windows (sequencing errors, N in the genome) are probed; they
-//      must all be absent.
+//   4. the other windows (sequencing errors, N in the genome) are probed by the
+//      whole wave together: each lane lists its unwalked windows, the lists are
+//      concatenated in LDS and every lane probes four entries per pass, so a
+//      lane with many unwalked windows does not hold its wave back.  A found
+//      specific k-mer names the read's genome: the read is walked again from
+//      it (once).
 // If so, every included k-mer occurs in the anchor genome g, the walked
 // windows hold no k-mer twice (no PA_TILE_REP flag, the windows of one read are
 // < 127 apart), every specific k-mer is specific to g, and the reference's
@@ -33,8 +37,18 @@ constexpr int kLaneMaxW = 128;    // windows per read on the lane path
 constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
 constexpr int kLaneChunks = 12;   // 16-B chunks covering shift + kLaneMaxLen bases
 constexpr int kLaneWords = 6;     // 64-bit words of the packed read (32 bases each)
+constexpr int kPassEntries = 256; // unwalked windows probed per cooperative pass (4 per lane)
 
-enum : int { LANE_UNIQUE = 0, LANE_AMB = 1, LANE_UNMAPPED = 2, LANE_DROP = 3, LANE_HARD = 4 };
+// Per-wave LDS of the lane kernel.
+struct __align__(16) LaneWave {
+    uint64_t R[64][kLaneWords + 1];  // every lane's packed read (+ a zero word), for keys of listed windows
+    unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 32) | tpos
+    uint32_t flags[64];              // bit 0: specific k-mer found off the walk, bit 1: unspecific one
+    uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
+    uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
+};
+
+enum : int { LANE_UNIQUE = 0, LANE_AMB = 1, LANE_UNMAPPED = 2, LANE_DROP = 3, LANE_HARD = 4, LANE_WALK = 5 };
 
 // Word q of a register array by a runtime index (selects; no scratch).
 template <int N>
@@ -112,21 +126,27 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
     }
 }
 
-struct LaneOut {
-    int kind;
-    uint32_t genome;  // LANE_UNIQUE
-    uint32_t hr;      // windows filtered by --max-genomes
-};
-
 #ifdef PA_STATS
 #define LANE_HARD_WHY(i) atomicAdd(&a.dbg[4 + (i)], 1ull)
 #else
 #define LANE_HARD_WHY(i) ((void)0)
 #endif
 
+// Lane state of one read between the phases of k_align_lane.
+struct LaneRead {
+    int kind;                          // LANE_* (LANE_WALK: still resolving)
+    uint32_t len, W;
+    uint64_t R[kLaneWords];            // packed read from base 0 (MSB-first)
+    uint32_t atp, acls, aw;            // anchor: first occurrence, class, window
+    uint32_t g, nspec, nincl, hr;      // walk results (anchor genome, counts)
+    uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
+};
+
+// Phase 1: qualities, packing, seeds -> anchor.
 template <bool NEED_Q>
-__device__ __forceinline__ LaneOut lane_read(const AlignArgs &a, uint64_t r) {
-    LaneOut out{LANE_HARD, 0, 0};
+__device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, LaneRead &S) {
+    S.kind = LANE_HARD;
+    S.hr = S.nspec = S.nincl = 0;
     const int k = a.k;
     const uint32_t flags = a.prm.flags;
     const uint64_t o = a.off[r];
@@ -134,7 +154,8 @@ __device__ __forceinline__ LaneOut lane_read(const AlignArgs &a, uint64_t r) {
     const uint64_t o0 = o & ~15ull;
     const uint32_t shift = (uint32_t)(o & 15);
     const uint32_t nch = (shift + len + 15) >> 4;
-    if (len > (uint32_t)kLaneMaxLen) return LANE_HARD_WHY(0), out;
+    S.len = len;
+    if (len > (uint32_t)kLaneMaxLen) return (void)LANE_HARD_WHY(0);
     // ---- qualities: read mean (src/kmer.py:399, 587) and the k-mer filter bound
     if (NEED_Q) {
         const uint4 *qp = (const uint4 *)(a.qual + o0);
@@ -157,18 +178,19 @@ __device__ __forceinline__ LaneOut lane_read(const AlignArgs &a, uint64_t r) {
             }
         }
         if ((flags & F_MRQ) && (int64_t)sum < (int64_t)a.prm.mrq * (int64_t)len) {
-            out.kind = LANE_DROP;  // dropped, not unmapped (src/kmer.py:587-589)
-            return out;
+            S.kind = LANE_DROP;  // dropped, not unmapped (src/kmer.py:587-589)
+            return;
         }
         // a window's mean is >= the read's minimum: if that passes, no window can fail
-        if ((flags & F_MKQ) && len >= (uint32_t)k && (int64_t)qmin < (int64_t)a.prm.mkq) return LANE_HARD_WHY(1), out;
+        if ((flags & F_MKQ) && len >= (uint32_t)k && (int64_t)qmin < (int64_t)a.prm.mkq) return (void)LANE_HARD_WHY(1);
     }
     if (len < (uint32_t)k) {
-        out.kind = LANE_UNMAPPED;  // no windows (src/kmer.py:91-92, 516-517)
-        return out;
+        S.kind = LANE_UNMAPPED;  // no windows (src/kmer.py:91-92, 516-517)
+        return;
     }
     const uint32_t W = len - k + 1;
-    if (W > (uint32_t)kLaneMaxW) return LANE_HARD_WHY(0), out;
+    S.W = W;
+    if (W > (uint32_t)kLaneMaxW) return (void)LANE_HARD_WHY(0);
     // ---- 2-bit pack (staged coordinates: base p of the 16-B aligned stretch)
     uint64_t P[kLaneWords + 1];
     uint32_t bad = 0;
@@ -196,20 +218,18 @@ __device__ __forceinline__ LaneOut lane_read(const AlignArgs &a, uint64_t r) {
             P[c >> 1] = (uint64_t)half << 32;
     }
     P[kLaneWords] = 0;
-    if (bad) return LANE_HARD_WHY(2), out;  // non-ACGT base: the wave kernel poisons its windows
-    // the read's words from base 0 on
-    uint64_t R[kLaneWords];
+    if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
 #pragma unroll
     for (int i = 0; i < kLaneWords; i++) {
         const uint32_t s2 = 2 * shift;
-        R[i] = s2 ? ((P[i] << s2) | (P[i + 1] >> (64 - s2))) : P[i];
+        S.R[i] = s2 ? ((P[i] << s2) | (P[i + 1] >> (64 - s2))) : P[i];
     }
     const int sh = 64 - 2 * k;
     // ---- seeds: first, middle, last window
     const uint32_t sw[3] = {0u, (W - 1) >> 1, W - 1};
     uint64_t skey[3];
 #pragma unroll
-    for (int i = 0; i < 3; i++) skey[i] = bits_at(R, 2 * sw[i]) >> sh;
+    for (int i = 0; i < 3; i++) skey[i] = bits_at(S.R, 2 * sw[i]) >> sh;
     uint32_t sfound, scls[3], stp[3];
     lane_probe<3>(a, skey, 7u, sfound, scls, stp);
     int at = -1;
@@ -218,77 +238,88 @@ __device__ __forceinline__ LaneOut lane_read(const AlignArgs &a, uint64_t r) {
 #pragma unroll
         for (int i = 0; i < 3; i++)
             if (at < 0 && bit(sfound, i) && stp[i] != NONE && (pass == 1 || scls[i] < a.G)) at = i;
-    if (at < 0) return LANE_HARD_WHY(3), out;  // no anchor
-    uint32_t atp = stp[0], acls = scls[0], aw = sw[0];
+    if (at < 0) return (void)LANE_HARD_WHY(3);  // no anchor
+    S.atp = stp[0];
+    S.acls = scls[0];
+    S.aw = sw[0];
 #pragma unroll
     for (int i = 1; i < 3; i++)
         if (at == i) {
-            atp = stp[i];
-            acls = scls[i];
-            aw = sw[i];
+            S.atp = stp[i];
+            S.acls = scls[i];
+            S.aw = sw[i];
         }
-    // ---- walk from the anchor; a found window off the walk (the read's own
-    // genome when a multi-genome seed placed it in another family member) becomes
-    // the anchor of a second walk
-    uint32_t nspec = 0, nincl = 0, hr = 0, g = 0;
+    S.kind = LANE_WALK;
+}
+
+// Phase 2: walk from the anchor; walked windows resolve from the tile, the
+// others are left in P0 / P1 for the cooperative probes.
+__device__ __forceinline__ void lane_walk(const AlignArgs &a, LaneRead &S) {
+    const int k = a.k;
+    const uint32_t W = S.W, len = S.len;
+    const int64_t A = (int64_t)S.atp - (int64_t)S.aw;  // genome position of window 0
+    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.G, S.atp);
+    S.g = g;
+    const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
+    // every window of the read must lie inside the anchor genome
+    if (A < (int64_t)gs || (uint64_t)A + W - 1 + k > ge) {
+        S.kind = LANE_HARD;
+        return (void)LANE_HARD_WHY(4);
+    }
+    // ---- mismatching bases against the genome from A on
+    uint64_t U0 = 0, U1 = 0;  // windows touching a mismatch: [e - k + 1, e] for every mismatching base e
+    uint32_t nmis = 0;
+#pragma unroll
+    for (int i = 0; i < kLaneWords; i++) {
+        uint64_t d = 0;
+        if (32 * i < (int)len) {
+            d = S.R[i] ^ get64_at(a.tile_pk, 2 * (uint64_t)A + 64u * i);
+            const uint32_t rest = len - 32 * i;  // bases of the read in this word
+            if (rest < 32) d &= ~0ull << (64 - 2 * rest);
+        }
+        uint64_t m = (d | (d >> 1)) & 0x5555555555555555ull;  // one bit per mismatching base
+        while (m) {
+            const uint32_t e = 32 * i + (__builtin_clzll(m) >> 1);
+            m &= ~(1ull << (62 - 2 * (e & 31)));
+            if (++nmis > 8) {  // a wrong stretch, not a few sequencing errors
+                S.kind = LANE_HARD;
+                return (void)LANE_HARD_WHY(5);
+            }
+            const int32_t lo = (int32_t)e - k + 1 < 0 ? 0 : (int32_t)e - k + 1;
+            const int32_t hi = (int32_t)e < (int32_t)W - 1 ? (int32_t)e : (int32_t)W - 1;
+            if (lo > hi) continue;
+            U0 |= lo < 64 ? ((~0ull << lo) & (hi >= 63 ? ~0ull : ((2ull << hi) - 1))) : 0ull;
+            U1 |= hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) & (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
+                           : 0ull;
+        }
+    }
+    // ---- walked windows: classes from the tile
+    const bool has_mg = a.prm.flags & F_MG;
+    uint32_t nspec = 0, nincl = 0, hr = 0;
+    uint64_t P0 = 0, P1 = 0;
+    uint32_t last_c = NONE, last_big = 0;
+    const uint32_t *tc = a.tile_cls + A;
+    // 32 windows per step: their tile entries are loaded together (one round trip)
 #pragma unroll 1
-    for (int attempt = 0;; attempt++) {
-        const int64_t A = (int64_t)atp - (int64_t)aw;  // genome position of window 0
-        g = acls < a.G ? acls : genome_of(a.goff, a.G, atp);
-        const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
-        // every window of the read must lie inside the anchor genome
-        if (A < (int64_t)gs || (uint64_t)A + W - 1 + k > ge) return LANE_HARD_WHY(4), out;
-        // ---- mismatching bases against the genome from A on
-        uint64_t mm[kLaneWords];
+    for (uint32_t w0 = 0; w0 < W; w0 += 32) {
+        uint32_t v32[32];
 #pragma unroll
-        for (int i = 0; i < kLaneWords; i++) {
-            uint64_t d = 0;
-            if (32 * i < (int)len) {
-                d = R[i] ^ get64_at(a.tile_pk, 2 * (uint64_t)A + 64u * i);
-                const uint32_t rest = len - 32 * i;  // bases of the read in this word
-                if (rest < 32) d &= ~0ull << (64 - 2 * rest);
-            }
-            mm[i] = (d | (d >> 1)) & 0x5555555555555555ull;  // one bit per mismatching base
-        }
-        // windows touching a mismatch: [e - k + 1, e] for every mismatching base e
-        uint64_t U0 = 0, U1 = 0;  // windows 0-63, 64-127
-        uint32_t nmis = 0;
+        for (int i = 0; i < 32; i++) v32[i] = (w0 + i < W) ? tc[w0 + i] : NONE;
+        const uint64_t um = (w0 < 64 ? U0 : U1) >> (w0 & 63);  // unmatched windows of the step
+        uint32_t pend = 0;
 #pragma unroll
-        for (int i = 0; i < kLaneWords; i++) {
-            uint64_t m = mm[i];
-            while (m) {
-                const uint32_t e = 32 * i + (__builtin_clzll(m) >> 1);
-                m &= ~(1ull << (62 - 2 * (e & 31)));
-                if (++nmis > 8) return LANE_HARD_WHY(5), out;  // a wrong stretch, not a few errors
-                const int32_t lo = (int32_t)e - k + 1 < 0 ? 0 : (int32_t)e - k + 1;
-                const int32_t hi = (int32_t)e < (int32_t)W - 1 ? (int32_t)e : (int32_t)W - 1;
-                if (lo > hi) continue;
-                // bits [lo, hi] of the 128-bit mask
-                const uint64_t m0 = lo < 64 ? ((~0ull << lo) & (hi >= 63 ? ~0ull : ((2ull << hi) - 1))) : 0ull;
-                const uint64_t m1 = hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) &
-                                                (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
-                                             : 0ull;
-                U0 |= m0;
-                U1 |= m1;
-            }
-        }
-        // ---- walked windows: classes from the tile
-        const bool has_mg = flags & F_MG;
-        nspec = nincl = hr = 0;
-        uint64_t P0 = 0, P1 = 0;  // windows to probe
-        uint32_t last_c = NONE, last_big = 0;
-        const uint32_t *tc = a.tile_cls + A;
-        for (uint32_t w = 0; w < W; w++) {
-            const bool unmatched = w < 64 ? ((U0 >> w) & 1) : ((U1 >> (w - 64)) & 1);
-            const uint32_t v = unmatched ? NONE : tc[w];
+        for (int i = 0; i < 32; i++) {
+            const uint32_t w = w0 + i;
+            if (w >= W) break;
+            const uint32_t v = ((um >> i) & 1) ? NONE : v32[i];
             if (v == NONE) {
-                if (w < 64)
-                    P0 |= 1ull << w;
-                else
-                    P1 |= 1ull << (w - 64);
+                pend |= 1u << i;
                 continue;
             }
-            if (v & PA_TILE_REP) return LANE_HARD_WHY(6), out;  // the k-mer may repeat inside the read
+            if (v & PA_TILE_REP) {  // the k-mer may repeat inside the read
+                S.kind = LANE_HARD;
+                return (void)LANE_HARD_WHY(6);
+            }
             if (has_mg) {
                 if (v != last_c) {
                     last_c = v;
@@ -301,85 +332,106 @@ __device__ __forceinline__ LaneOut lane_read(const AlignArgs &a, uint64_t r) {
             }
             nincl++;
             if (v < a.G) {
-                if (v != g) return out;  // (cannot happen inside genome g; kept as a guard)
+                if (v != g) {  // (cannot happen inside genome g; kept as a guard)
+                    S.kind = LANE_HARD;
+                    return;
+                }
                 nspec++;
             }
         }
-        // a read with many unwalked windows is cheaper in the wave kernel (a lane
-        // would probe them one after the other while the rest of its wave waits)
-        if ((uint32_t)(__popcll(P0) + __popcll(P1)) > a.lane_maxpend) return LANE_HARD_WHY(8), out;
-        // ---- the other windows: absent, or found off the walk.  A found
-        // specific k-mer names the read's genome: walk again from it (once).
-        // Found unspecific k-mers alone keep the decision simple only if no
-        // specific k-mer is included at all -- then the read is AMBIGUOUS with
-        // an empty list whatever the sets (src/kmer.py:458-461).
-        bool reanchor = false, off_multi = false;
-        while (P0 | P1) {
-            uint64_t key4[4];
-            uint32_t w4[4], act = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                key4[i] = 0;
-                w4[i] = 0;
-                if (P0 | P1) {
-                    uint32_t w;
-                    if (P0) {
-                        w = __builtin_ctzll(P0);
-                        P0 &= P0 - 1;
-                    } else {
-                        w = 64 + __builtin_ctzll(P1);
-                        P1 &= P1 - 1;
-                    }
-                    key4[i] = bits_at(R, 2 * w) >> sh;
-                    w4[i] = w;
-                    act |= 1u << i;
-                }
+        if (w0 < 64)
+            P0 |= (uint64_t)pend << w0;
+        else
+            P1 |= (uint64_t)pend << (w0 - 64);
+    }
+    S.nspec = nspec;
+    S.nincl = nincl;
+    S.hr = hr;
+    S.P0 = P0;
+    S.P1 = P1;
+    // a read with very many unwalked windows is left to the wave kernel
+    if ((uint32_t)(__popcll(P0) + __popcll(P1)) > a.lane_maxpend) {
+        S.kind = LANE_HARD;
+        return (void)LANE_HARD_WHY(8);
+    }
+}
+
+// Phase 3 (whole wave): probe the unwalked windows of every walking lane.
+__device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW, const LaneRead &S) {
+    const int lane = lane_id();
+    const int sh = 64 - 2 * a.k;
+    const bool walking = S.kind == LANE_WALK;
+    LW.flags[lane] = 0;
+    LW.hr[lane] = 0;
+    LW.cand[lane] = ~0ull;
+    const uint32_t c = walking ? (uint32_t)(__popcll(S.P0) + __popcll(S.P1)) : 0u;
+    const uint32_t incl = wave_incl_scan(c);
+    const uint32_t pre = incl - c;
+    const uint32_t total = __shfl(incl, 63);
+    uint64_t Q0 = walking ? S.P0 : 0, Q1 = walking ? S.P1 : 0;
+    for (uint32_t base = 0; base < total; base += kPassEntries) {
+        // this pass's entries of the lane: global indices [max(pre, base), min(pre + c, base + 256))
+        const uint32_t lo = max(pre, base), hi = min(pre + c, base + (uint32_t)kPassEntries);
+        for (uint32_t e = lo; e < hi; e++) {
+            uint32_t w;
+            if (Q0) {
+                w = __builtin_ctzll(Q0);
+                Q0 &= Q0 - 1;
+            } else {
+                w = 64 + __builtin_ctzll(Q1);
+                Q1 &= Q1 - 1;
             }
-            uint32_t f, c4[4], t4[4];
-            lane_probe<4>(a, key4, act, f, c4, t4);
+            LW.list[e - base] = (uint16_t)((lane << 8) | w);
+        }
+        wave_sync();
+        const uint32_t cnt = min(total - base, (uint32_t)kPassEntries);
+        uint64_t key4[4];
+        uint32_t tag4[4], act = 0;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if (!bit(f, i)) continue;
-                const uint32_t c = c4[i];
-                if (has_mg && (int64_t)class_size_of(c, a.G, a.class_genomes) > (int64_t)a.prm.mg) {
-                    hr++;  // highly redundant: counted, never included
-                } else if (c >= a.G) {
-                    off_multi = true;
-                } else if (!reanchor) {
-                    if (attempt > 0 || t4[i] == NONE) return LANE_HARD_WHY(7), out;
-                    reanchor = true;
-                    atp = t4[i];
-                    acls = c;
-                    aw = w4[i];
-                }
+        for (int i = 0; i < 4; i++) {
+            const uint32_t e = 4 * lane + i;
+            key4[i] = 0;
+            tag4[i] = 0;
+            if (e < cnt) {
+                const uint32_t t = LW.list[e];
+                const uint64_t *row = LW.R[t >> 8];
+                const uint32_t o = 2 * (t & 255), q = o >> 6, rr = o & 63;
+                const uint64_t hi64 = row[q] << rr;
+                key4[i] = (rr ? (hi64 | (row[q + 1] >> (64 - rr))) : hi64) >> sh;
+                tag4[i] = t;
+                act |= 1u << i;
             }
         }
-        if (reanchor) continue;
-        if (off_multi) {
-            if (nspec > 0) return LANE_HARD_WHY(7), out;
-            nincl++;  // (only its being nonzero matters below)
+        uint32_t f, c4[4], t4[4];
+        lane_probe<4>(a, key4, act, f, c4, t4);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (!bit(f, i)) continue;
+            const uint32_t o = tag4[i] >> 8, w = tag4[i] & 255;
+            const uint32_t cl = c4[i];
+            if ((a.prm.flags & F_MG) && (int64_t)class_size_of(cl, a.G, a.class_genomes) > (int64_t)a.prm.mg) {
+                atomicAdd(&LW.hr[o], 1u);  // highly redundant: counted, never included
+            } else if (cl >= a.G) {
+                atomicOr(&LW.flags[o], 2u);
+            } else {
+                atomicOr(&LW.flags[o], 1u);
+                atomicMin(&LW.cand[o], ((unsigned long long)w << 32) | t4[i]);
+            }
         }
-        break;
+        wave_sync();  // the list is rewritten by the next pass
     }
-    out.hr = hr;
-    if (nincl == 0)
-        out.kind = LANE_UNMAPPED;
-    else if (nspec == 0)
-        out.kind = LANE_AMB;  // only unspecific k-mers: AMBIGUOUS, empty list
-    else {
-        out.kind = LANE_UNIQUE;
-        out.genome = g;
-    }
-    return out;
 }
 
 template <bool NEED_Q>
 __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const uint32_t G = a.G;
+    const int lane = lane_id();
     const bool lds = G <= kLdsGenomeCap;
+    const size_t cnt_bytes = lds ? ((size_t)G * 12 + 15) / 16 * 16 : 0;
     unsigned long long *first = (unsigned long long *)smem;
     uint32_t *uniq = (uint32_t *)(first + (lds ? G : 0));
+    LaneWave &LW = ((LaneWave *)(smem + cnt_bytes))[threadIdx.x >> 6];
     if (lds) {
         for (uint32_t i = threadIdx.x; i < G; i += kBlock) {
             first[i] = (unsigned long long)PA_NO_FIRST_KEY;
@@ -389,41 +441,86 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
     }
     uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0, n_hr = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    const uint64_t n_iter = (a.n + stride - 1) / stride;  // uniform trip count (wave-aggregated queueing)
+    const uint64_t n_iter = (a.n + stride - 1) / stride;  // uniform trip count (wave-wide phases)
     for (uint64_t it = 0; it < n_iter; it++) {
         const uint64_t r = it * stride + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-        LaneOut res{LANE_UNMAPPED + 100, 0, 0};
-        if (r < a.n) res = lane_read<NEED_Q>(a, r);
-        const bool hard = res.kind == LANE_HARD;
-        const uint64_t hb = __ballot(hard);
-        if (hb) {  // one queue allocation per wave
-            uint64_t base = 0;
-            if (lane_id() == __builtin_ctzll(hb)) base = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
-            base = shfl64(base, __builtin_ctzll(hb));
-            if (hard) a.queue_hard[base + lanes_below(hb)] = (uint32_t)r;
+        LaneRead S;
+        S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
+        if (r < a.n) {
+            if (NEED_Q)
+                lane_prep<true>(a, r, S);
+            else
+                lane_prep<false>(a, r, S);
         }
-        if (res.kind == LANE_UNIQUE) {
-            const uint64_t key = first_key(a.base + r, 0);
-            if (lds) {
-                atomicAdd(&uniq[res.genome], 1u);
-                if (key < first[res.genome]) atomicMin(&first[res.genome], (unsigned long long)key);
-            } else {
-                atomicAdd(&a.uniq[res.genome], 1ull);
-                atomicMin(&a.first[res.genome], (unsigned long long)key);
+        wave_sync();  // the previous read's rows are done with
+        if (S.kind == LANE_WALK) {
+#pragma unroll
+            for (int i = 0; i < kLaneWords; i++) LW.R[lane][i] = S.R[i];
+            LW.R[lane][kLaneWords] = 0;
+        }
+#pragma unroll 1
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (S.kind == LANE_WALK) lane_walk(a, S);
+            if (!__ballot(S.kind == LANE_WALK)) break;
+            lane_probe_wave(a, LW, S);
+            if (S.kind == LANE_WALK) {
+                const uint32_t fl = LW.flags[lane];
+                if (fl & 1u) {  // a specific k-mer off the walk: walk again from it (once)
+                    if (attempt == 0) {
+                        const unsigned long long cd = LW.cand[lane];
+                        S.atp = (uint32_t)cd;
+                        S.aw = (uint32_t)(cd >> 32);
+                        S.acls = NONE;  // genome from the position
+                    } else {
+                        S.kind = LANE_HARD;
+                        LANE_HARD_WHY(7);
+                    }
+                } else {
+                    S.hr += LW.hr[lane];
+                    if (fl & 2u) {  // unspecific k-mers off the walk: fine only without specific ones
+                        if (S.nspec > 0) {
+                            S.kind = LANE_HARD;
+                            LANE_HARD_WHY(7);
+                        } else {
+                            S.kind = LANE_AMB;
+                        }
+                    } else {
+                        S.kind = S.nincl == 0 ? LANE_UNMAPPED : (S.nspec == 0 ? LANE_AMB : LANE_UNIQUE);
+                    }
+                }
             }
         }
-        n_uniq += res.kind == LANE_UNIQUE;
-        n_amb += res.kind == LANE_AMB;
-        n_unm += res.kind == LANE_UNMAPPED;
-        n_drop += res.kind == LANE_DROP;
-        n_hr += (res.kind <= LANE_UNMAPPED) ? res.hr : 0u;
+        if (S.kind == LANE_WALK) S.kind = LANE_HARD;  // (a second re-anchoring is not attempted)
+        const bool hard = S.kind == LANE_HARD;
+        const uint64_t hb = __ballot(hard);
+        if (hb) {  // one queue allocation per wave
+            uint64_t qbase = 0;
+            if (lane == __builtin_ctzll(hb)) qbase = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
+            qbase = shfl64(qbase, __builtin_ctzll(hb));
+            if (hard) a.queue_hard[qbase + lanes_below(hb)] = (uint32_t)r;
+        }
+        if (S.kind == LANE_UNIQUE) {
+            const uint64_t key = first_key(a.base + r, 0);
+            if (lds) {
+                atomicAdd(&uniq[S.g], 1u);
+                if (key < first[S.g]) atomicMin(&first[S.g], (unsigned long long)key);
+            } else {
+                atomicAdd(&a.uniq[S.g], 1ull);
+                atomicMin(&a.first[S.g], (unsigned long long)key);
+            }
+        }
+        n_uniq += S.kind == LANE_UNIQUE;
+        n_amb += S.kind == LANE_AMB;
+        n_unm += S.kind == LANE_UNMAPPED;
+        n_drop += S.kind == LANE_DROP;
+        n_hr += (S.kind == LANE_UNIQUE || S.kind == LANE_AMB || S.kind == LANE_UNMAPPED) ? S.hr : 0u;
     }
     n_uniq = wave_sum(n_uniq);
     n_amb = wave_sum(n_amb);
     n_unm = wave_sum(n_unm);
     n_drop = wave_sum(n_drop);
     n_hr = wave_sum(n_hr);
-    if (lane_id() == 0) {
+    if (lane == 0) {
         if (n_uniq) atomicAdd(&a.stats[0], (unsigned long long)n_uniq);
         if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
         if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
@@ -437,4 +534,8 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
             if (first[i] != (unsigned long long)PA_NO_FIRST_KEY) atomicMin(&a.first[i], first[i]);
         }
     }
+}
+
+constexpr size_t lane_lds_bytes(uint32_t G) {
+    return (G <= kLdsGenomeCap ? ((size_t)G * 12 + 15) / 16 * 16 : 0) + (size_t)kWaves * sizeof(LaneWave);
 }
