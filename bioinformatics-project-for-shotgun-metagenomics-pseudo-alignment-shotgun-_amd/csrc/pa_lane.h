@@ -37,7 +37,13 @@ constexpr int kLaneMaxW = 128;    // windows per read on the lane path
 constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
 constexpr int kLaneChunks = 12;   // 16-B chunks covering shift + kLaneMaxLen bases
 constexpr int kLaneWords = 6;     // 64-bit words of the packed read (32 bases each)
-constexpr int kPassEntries = 256; // unwalked windows probed per cooperative pass (4 per lane)
+#ifndef PA_LANE_PROBES
+#define PA_LANE_PROBES 4  // unwalked windows probed per lane and cooperative pass
+#endif
+#ifndef PA_LANE_SLOTS
+#define PA_LANE_SLOTS 1   // table slots per probe step in the cooperative passes
+#endif
+constexpr int kPassEntries = 64 * PA_LANE_PROBES;
 
 // Per-wave LDS of the lane kernel.
 struct __align__(16) LaneWave {
@@ -80,9 +86,9 @@ __device__ __forceinline__ uint32_t genome_of(const uint64_t *goff, uint32_t G, 
     return lo;
 }
 
-// Up to NP table probes of one lane in flight together, two slots (one 32-B
-// aligned pair) per step; linear-probing order is kept exactly.
-template <int NP>
+// Up to NP table probes of one lane in flight together, NS slots (an aligned
+// NS x 16-B group) per step; linear-probing order is kept exactly.
+template <int NP, int NS = 2>
 __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&key)[NP], uint32_t act,
                                            uint32_t &found, uint32_t (&cls)[NP], uint32_t (&tpos)[NP]) {
     const Slot<1> *table = (const Slot<1> *)a.table;
@@ -95,21 +101,21 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
     }
     found = 0;
     while (act) {
-        Slot<1> s[NP][2];
+        Slot<1> s[NP][NS];
 #pragma unroll
         for (int i = 0; i < NP; i++)
             if (bit(act, i)) {
-                const uint64_t b = pos[i] & ~1ull;
-                s[i][0] = table[b];
-                s[i][1] = table[b + 1];
+                const uint64_t b = pos[i] & ~(uint64_t)(NS - 1);
+#pragma unroll
+                for (int h = 0; h < NS; h++) s[i][h] = table[b + h];
             }
 #pragma unroll
         for (int i = 0; i < NP; i++) {
             if (!bit(act, i)) continue;
-            const uint64_t b = pos[i] & ~1ull;
+            const uint64_t b = pos[i] & ~(uint64_t)(NS - 1);
             bool done = false;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
+            for (int h = 0; h < NS; h++) {
                 if (done || b + h < pos[i]) continue;
                 if (s[i][h].key[0] == EMPTY) {
                     done = true;
@@ -121,7 +127,7 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
                 }
             }
             if (done) act &= ~(1u << i);
-            pos[i] = (b + 2 == a.cap) ? 0 : b + 2;
+            pos[i] = (b + NS == a.cap) ? 0 : b + NS;
         }
     }
 }
@@ -132,19 +138,34 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
 #define LANE_HARD_WHY(i) ((void)0)
 #endif
 
-// Lane state of one read between the phases of k_align_lane.
+// Lane state of one read between the phases of k_align_lane.  The packed read
+// itself lives in the lane's LDS row (LW.R[lane]): every lane of the wave needs
+// it for the keys of listed windows, and rolled loops over LDS words keep the
+// register footprint (and so the occupancy) of this latency-bound kernel low.
 struct LaneRead {
     int kind;                          // LANE_* (LANE_WALK: still resolving)
     uint32_t len, W;
-    uint64_t R[kLaneWords];            // packed read from base 0 (MSB-first)
     uint32_t atp, acls, aw;            // anchor: first occurrence, class, window
     uint32_t g, nspec, nincl, hr;      // walk results (anchor genome, counts)
     uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
 };
 
-// Phase 1: qualities, packing, seeds -> anchor.
+// 64 bits of an LDS row of MSB-first packed words starting at bit o.
+__device__ __forceinline__ uint64_t row_bits(const uint64_t *row, uint32_t o) {
+    const uint32_t q = o >> 6, r = o & 63;
+    const uint64_t hi = row[q] << r;
+    return r ? (hi | (row[q + 1] >> (64 - r))) : hi;
+}
+
+// Bytes [lo, hi) of a dword at staged position p0 that belong to the read.
+__device__ __forceinline__ uint32_t in_read_mask(uint32_t p0, uint32_t shift, uint32_t len) {
+    const uint32_t lo = shift > p0 ? shift - p0 : 0u, hi = shift + len > p0 ? shift + len - p0 : 0u;
+    return (hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1)) & (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
+}
+
+// Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor.
 template <bool NEED_Q>
-__device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, LaneRead &S) {
+__device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64_t *row, LaneRead &S) {
     S.kind = LANE_HARD;
     S.hr = S.nspec = S.nincl = 0;
     const int k = a.k;
@@ -160,18 +181,17 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, LaneRe
     if (NEED_Q) {
         const uint4 *qp = (const uint4 *)(a.qual + o0);
         uint32_t sum = 0, qmin = 255;
+#pragma unroll 1
+        for (uint32_t c = 0; c < nch; c += 2) {
+            const uint4 v0 = qp[c], v1 = qp[c + 1];  // (buffers are padded past the last read)
+            const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-        for (int c = 0; c < kLaneChunks; c++) {
-            if (c >= (int)nch) break;
-            const uint4 v = qp[c];
-            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
+            for (int e = 0; e < 8; e++) {
+                const uint32_t inr = in_read_mask(16 * c + 4 * e, shift, len);
 #pragma unroll
                 for (int b = 0; b < 4; b++) {
-                    const uint32_t p = 16 * c + 4 * e + b;
                     const uint32_t q = (d[e] >> (8 * b)) & 255u;
-                    const bool in = p >= shift && p < shift + len;
+                    const bool in = (inr >> (8 * b)) & 1u;
                     sum += in ? q : 0u;
                     qmin = in ? min(qmin, q) : qmin;
                 }
@@ -191,45 +211,36 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, LaneRe
     const uint32_t W = len - k + 1;
     S.W = W;
     if (W > (uint32_t)kLaneMaxW) return (void)LANE_HARD_WHY(0);
-    // ---- 2-bit pack (staged coordinates: base p of the 16-B aligned stretch)
-    uint64_t P[kLaneWords + 1];
-    uint32_t bad = 0;
+    // ---- 2-bit pack: staged word q (32 bases from the 16-B aligned start) from
+    // chunks 2q, 2q+1; row word q-1 = the read's bases from 0 on, shifted
     const uint4 *sp = (const uint4 *)(a.seq + o0);
+    const uint32_t s2 = 2 * shift;
+    uint32_t bad = 0;
+    uint64_t prev = 0;
+#pragma unroll 1
+    for (int q = 0; q <= kLaneWords; q++) {
+        uint64_t P = 0;
+        if (q < kLaneWords && 32u * q < shift + len) {
+            const uint4 v0 = sp[2 * q], v1 = sp[2 * q + 1];
+            const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-    for (int c = 0; c < kLaneChunks; c++) {
-        uint32_t half = 0;
-        if (c < (int)nch) {
-            const uint4 v = sp[c];
-            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
+            for (int e = 0; e < 8; e++) {
                 const uint32_t cd = swar_codes(d[e]);
-                const uint32_t p0 = 16 * c + 4 * e;
-                const uint32_t lo = shift > p0 ? shift - p0 : 0u, hi = shift + len > p0 ? shift + len - p0 : 0u;
-                const uint32_t inr =
-                    (hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1)) & (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
-                bad |= swar_bad_bytes(d[e], cd) & inr;
-                half |= swar_pack_byte(cd) << (24 - 8 * e);
+                bad |= swar_bad_bytes(d[e], cd) & in_read_mask(32 * q + 4 * e, shift, len);
+                P |= (uint64_t)swar_pack_byte(cd) << (56 - 8 * e);
             }
         }
-        if (c & 1)
-            P[c >> 1] |= half;
-        else
-            P[c >> 1] = (uint64_t)half << 32;
+        if (q > 0) row[q - 1] = s2 ? ((prev << s2) | (P >> (64 - s2))) : prev;
+        prev = P;
     }
-    P[kLaneWords] = 0;
+    row[kLaneWords] = 0;
     if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
-#pragma unroll
-    for (int i = 0; i < kLaneWords; i++) {
-        const uint32_t s2 = 2 * shift;
-        S.R[i] = s2 ? ((P[i] << s2) | (P[i + 1] >> (64 - s2))) : P[i];
-    }
     const int sh = 64 - 2 * k;
     // ---- seeds: first, middle, last window
     const uint32_t sw[3] = {0u, (W - 1) >> 1, W - 1};
     uint64_t skey[3];
 #pragma unroll
-    for (int i = 0; i < 3; i++) skey[i] = bits_at(S.R, 2 * sw[i]) >> sh;
+    for (int i = 0; i < 3; i++) skey[i] = row_bits(row, 2 * sw[i]) >> sh;
     uint32_t sfound, scls[3], stp[3];
     lane_probe<3>(a, skey, 7u, sfound, scls, stp);
     int at = -1;
@@ -254,7 +265,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, LaneRe
 
 // Phase 2: walk from the anchor; walked windows resolve from the tile, the
 // others are left in P0 / P1 for the cooperative probes.
-__device__ __forceinline__ void lane_walk(const AlignArgs &a, LaneRead &S) {
+__device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *row, LaneRead &S) {
     const int k = a.k;
     const uint32_t W = S.W, len = S.len;
     const int64_t A = (int64_t)S.atp - (int64_t)S.aw;  // genome position of window 0
@@ -266,17 +277,22 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, LaneRead &S) {
         S.kind = LANE_HARD;
         return (void)LANE_HARD_WHY(4);
     }
-    // ---- mismatching bases against the genome from A on
+    // ---- mismatching bases against the genome from A on (the genome words of
+    // the read's span are loaded together; tile_pk is padded)
+    const uint64_t gb = 2 * (uint64_t)A;
+    const uint64_t *gp = a.tile_pk + (gb >> 6);
+    const uint32_t gr = (uint32_t)(gb & 63);
+    uint64_t gw[kLaneWords + 1];
+#pragma unroll
+    for (int i = 0; i <= kLaneWords; i++) gw[i] = gp[i];
     uint64_t U0 = 0, U1 = 0;  // windows touching a mismatch: [e - k + 1, e] for every mismatching base e
     uint32_t nmis = 0;
 #pragma unroll
     for (int i = 0; i < kLaneWords; i++) {
-        uint64_t d = 0;
-        if (32 * i < (int)len) {
-            d = S.R[i] ^ get64_at(a.tile_pk, 2 * (uint64_t)A + 64u * i);
-            const uint32_t rest = len - 32 * i;  // bases of the read in this word
-            if (rest < 32) d &= ~0ull << (64 - 2 * rest);
-        }
+        if (32 * i >= (int)len) break;
+        uint64_t d = row[i] ^ (gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i]);
+        const uint32_t rest = len - 32 * i;  // bases of the read in this word
+        if (rest < 32) d &= ~0ull << (64 - 2 * rest);
         uint64_t m = (d | (d >> 1)) & 0x5555555555555555ull;  // one bit per mismatching base
         while (m) {
             const uint32_t e = 32 * i + (__builtin_clzll(m) >> 1);
@@ -385,11 +401,12 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
         }
         wave_sync();
         const uint32_t cnt = min(total - base, (uint32_t)kPassEntries);
-        uint64_t key4[4];
-        uint32_t tag4[4], act = 0;
+        constexpr int NPR = PA_LANE_PROBES;
+        uint64_t key4[NPR];
+        uint32_t tag4[NPR], act = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t e = 4 * lane + i;
+        for (int i = 0; i < NPR; i++) {
+            const uint32_t e = NPR * lane + i;
             key4[i] = 0;
             tag4[i] = 0;
             if (e < cnt) {
@@ -402,10 +419,10 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
                 act |= 1u << i;
             }
         }
-        uint32_t f, c4[4], t4[4];
-        lane_probe<4>(a, key4, act, f, c4, t4);
+        uint32_t f, c4[NPR], t4[NPR];
+        lane_probe<NPR, PA_LANE_SLOTS>(a, key4, act, f, c4, t4);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < NPR; i++) {
             if (!bit(f, i)) continue;
             const uint32_t o = tag4[i] >> 8, w = tag4[i] & 255;
             const uint32_t cl = c4[i];
@@ -446,21 +463,11 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
         const uint64_t r = it * stride + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
         LaneRead S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
-        if (r < a.n) {
-            if (NEED_Q)
-                lane_prep<true>(a, r, S);
-            else
-                lane_prep<false>(a, r, S);
-        }
         wave_sync();  // the previous read's rows are done with
-        if (S.kind == LANE_WALK) {
-#pragma unroll
-            for (int i = 0; i < kLaneWords; i++) LW.R[lane][i] = S.R[i];
-            LW.R[lane][kLaneWords] = 0;
-        }
+        if (r < a.n) lane_prep<NEED_Q>(a, r, LW.R[lane], S);
 #pragma unroll 1
         for (int attempt = 0; attempt < 2; attempt++) {
-            if (S.kind == LANE_WALK) lane_walk(a, S);
+            if (S.kind == LANE_WALK) lane_walk(a, LW.R[lane], S);
             if (!__ballot(S.kind == LANE_WALK)) break;
             lane_probe_wave(a, LW, S);
             if (S.kind == LANE_WALK) {
