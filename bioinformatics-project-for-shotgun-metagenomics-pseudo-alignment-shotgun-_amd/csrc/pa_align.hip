@@ -65,6 +65,7 @@ struct AlignArgs {
     const uint64_t *tile_pk;
     uint64_t tile_n;
     const uint64_t *goff;           // genome start positions [G + 1] (concatenated coordinates)
+    const uint16_t *tile16;         // lane kernel tile (null: no lane kernel)
     int walk_rounds;
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
     int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
@@ -535,6 +536,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_cls = idx->tile_cls;
     a.tile_pk = idx->tile_pk;
     a.goff = idx->goff;
+    a.tile16 = idx->tile_cls ? idx->tile16 : nullptr;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
     a.lane_maxpend = 96;
@@ -633,7 +635,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     const bool fast_ok = idx->k > 0 && idx->nw <= 2 && idx->n_kmers > 0;
     // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
     const char *no_lane = std::getenv("PA_NO_LANE");
-    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && !(no_lane && no_lane[0] == '1');
+    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile16 && !(no_lane && no_lane[0] == '1');
     if (fast_ok) {
         const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
         const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4

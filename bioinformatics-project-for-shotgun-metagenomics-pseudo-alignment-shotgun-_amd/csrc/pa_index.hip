@@ -437,6 +437,25 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
     }
 }
 
+// Compact tile for the lane kernel (pa_lane.h): per position 0 (no indexed
+// window) or PA_T16_VALID | [PA_T16_REP] | [PA_T16_SPEC] | min(set size, 8191).
+__global__ void k_tile16(const uint32_t *__restrict__ tile_cls, uint64_t n, uint32_t G,
+                         const uint32_t *__restrict__ class_genomes, uint16_t *__restrict__ t16) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; t < n; t += stride) {
+        const uint32_t v = tile_cls[t];
+        uint16_t o = 0;
+        if (v != NONE) {
+            const uint32_t c = v & ~PA_TILE_REP;
+            const uint32_t sz = class_size_of(c, G, class_genomes);
+            o = (uint16_t)(PA_T16_VALID | ((v & PA_TILE_REP) ? PA_T16_REP : 0u) | (c < G ? PA_T16_SPEC : 0u) |
+                           (sz < PA_T16_SIZE ? sz : PA_T16_SIZE));
+        }
+        t16[t] = o;
+    }
+}
+
 // ---- EXTSIM statistics ------------------------------------------------------
 
 template <int NW>
@@ -686,6 +705,12 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         if (k <= 31)
             hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
                                st, idx->tile_pk, idx->tile_cls, n, k);
+        if (k <= 31 && G < PA_T16_SIZE) {  // set sizes fit 13 bits exactly
+            B_HIP(hipMalloc(&idx->tile16, n * 2));
+            hipLaunchKernelGGL(k_tile16, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
+                               idx->tile_cls, n, G, idx->class_genomes, idx->tile16);
+            idx->device_bytes += n * 2;
+        }
         B_HIP(hipGetLastError());
         B_HIP(hipStreamSynchronize(st));
         idx->device_bytes += n * 4 + nwords * 8;
@@ -730,8 +755,10 @@ void index_release(pa_index *idx) {
     hipFree(idx->goff);
     hipFree(idx->tile_cls);
     hipFree(idx->tile_pk);
+    hipFree(idx->tile16);
     idx->tile_cls = nullptr;
     idx->tile_pk = nullptr;
+    idx->tile16 = nullptr;
     hipFree(idx->ws.ptr);
     hipFree(idx->queue);
     hipFree(idx->queue_hard);
@@ -777,7 +804,16 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     const char *no_tile = std::getenv("PA_NO_TILE");
     idx->tile_n = (idx->nw == 1 && k > 0 && total > 0 && total < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
                       ? total : 0;
+    // load factor 1/4 when the table fits a third of the free device memory
+    // (absent keys -- the sequencing-error windows -- then end in their home
+    // slot 3 times out of 4), else 1/2
     uint64_t cap_mult = 2;
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+            (4 * windows + 64) * (uint64_t)slot_bytes(idx->nw) <= free_b / 3)
+            cap_mult = 4;
+    }
     if (const char *e = std::getenv("PA_CAP_MULT")) cap_mult = std::max(2, std::atoi(e));
     uint64_t cap = std::max<uint64_t>(64, cap_mult * windows + 64);
     const uint64_t align = std::max<uint64_t>(4, R);  // whole 64-B lines (the fast kernel probes a line per step)

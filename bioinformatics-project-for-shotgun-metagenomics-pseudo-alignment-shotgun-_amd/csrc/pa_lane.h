@@ -313,47 +313,35 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     const bool has_mg = a.prm.flags & F_MG;
     uint32_t nspec = 0, nincl = 0, hr = 0;
     uint64_t P0 = 0, P1 = 0;
-    uint32_t last_c = NONE, last_big = 0;
-    const uint32_t *tc = a.tile_cls + A;
+    const uint16_t *tc = a.tile16 + A;
     // 32 windows per step: their tile entries are loaded together (one round trip)
 #pragma unroll 1
     for (uint32_t w0 = 0; w0 < W; w0 += 32) {
         uint32_t v32[32];
 #pragma unroll
-        for (int i = 0; i < 32; i++) v32[i] = (w0 + i < W) ? tc[w0 + i] : NONE;
+        for (int i = 0; i < 32; i++) v32[i] = (w0 + i < W) ? (uint32_t)tc[w0 + i] : 0u;
         const uint64_t um = (w0 < 64 ? U0 : U1) >> (w0 & 63);  // unmatched windows of the step
         uint32_t pend = 0;
 #pragma unroll
         for (int i = 0; i < 32; i++) {
             const uint32_t w = w0 + i;
             if (w >= W) break;
-            const uint32_t v = ((um >> i) & 1) ? NONE : v32[i];
-            if (v == NONE) {
+            const uint32_t v = ((um >> i) & 1) ? 0u : v32[i];
+            if (!(v & PA_T16_VALID)) {
                 pend |= 1u << i;
                 continue;
             }
-            if (v & PA_TILE_REP) {  // the k-mer may repeat inside the read
+            if (v & PA_T16_REP) {  // the k-mer may repeat inside the read
                 S.kind = LANE_HARD;
                 return (void)LANE_HARD_WHY(6);
             }
-            if (has_mg) {
-                if (v != last_c) {
-                    last_c = v;
-                    last_big = (int64_t)class_size_of(v, a.G, a.class_genomes) > (int64_t)a.prm.mg;
-                }
-                if (last_big) {
-                    hr++;  // highly redundant (src/kmer.py:425-427)
-                    continue;
-                }
+            if (has_mg && (int64_t)(v & PA_T16_SIZE) > (int64_t)a.prm.mg) {
+                hr++;  // highly redundant (src/kmer.py:425-427)
+                continue;
             }
             nincl++;
-            if (v < a.G) {
-                if (v != g) {  // (cannot happen inside genome g; kept as a guard)
-                    S.kind = LANE_HARD;
-                    return;
-                }
-                nspec++;
-            }
+            // a specific k-mer at a position inside genome g is specific to g
+            nspec += (v & PA_T16_SPEC) ? 1u : 0u;
         }
         if (w0 < 64)
             P0 |= (uint64_t)pend << w0;
