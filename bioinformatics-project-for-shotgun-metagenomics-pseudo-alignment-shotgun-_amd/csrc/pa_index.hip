@@ -706,7 +706,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
                                st, idx->tile_pk, idx->tile_cls, n, k);
         if (k <= 31 && G < PA_T16_SIZE) {  // set sizes fit 13 bits exactly
-            B_HIP(hipMalloc(&idx->tile16, n * 2));
+            B_HIP(hipMalloc(&idx->tile16, n * 2 + 512));  // padded: the lane walk loads 2 x 33 dwords
+            B_HIP(hipMemsetAsync(idx->tile16, 0, n * 2 + 512, st));
             hipLaunchKernelGGL(k_tile16, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
                                idx->tile_cls, n, G, idx->class_genomes, idx->tile16);
             idx->device_bytes += n * 2;

@@ -269,22 +269,31 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     const int k = a.k;
     const uint32_t W = S.W, len = S.len;
     const int64_t A = (int64_t)S.atp - (int64_t)S.aw;  // genome position of window 0
-    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.G, S.atp);
-    S.g = g;
-    const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
-    // every window of the read must lie inside the anchor genome
-    if (A < (int64_t)gs || (uint64_t)A + W - 1 + k > ge) {
-        S.kind = LANE_HARD;
-        return (void)LANE_HARD_WHY(4);
-    }
-    // ---- mismatching bases against the genome from A on (the genome words of
-    // the read's span are loaded together; tile_pk is padded)
-    const uint64_t gb = 2 * (uint64_t)A;
+    const bool in_tile = A >= 0 && (uint64_t)A + W <= a.tile_n;
+    const uint64_t Ac = in_tile ? (uint64_t)A : 0;
+    // every load of the walk is issued before anything waits: the genome words
+    // of the read's span (tile_pk is padded), the first 64 tile entries (as
+    // dwords from an even position), and the anchor genome's range
+    const uint64_t gb = 2 * Ac;
     const uint64_t *gp = a.tile_pk + (gb >> 6);
     const uint32_t gr = (uint32_t)(gb & 63);
     uint64_t gw[kLaneWords + 1];
 #pragma unroll
     for (int i = 0; i <= kLaneWords; i++) gw[i] = gp[i];
+    const uint32_t odd = (uint32_t)(Ac & 1);
+    const uint32_t *t32 = (const uint32_t *)(a.tile16 + (Ac - odd));  // (tile16 is padded by a dword)
+    uint32_t td[17];
+#pragma unroll
+    for (int j = 0; j < 17; j++) td[j] = t32[j];
+    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.G, S.atp);
+    S.g = g;
+    const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
+    // every window of the read must lie inside the anchor genome
+    if (!in_tile || A < (int64_t)gs || (uint64_t)A + W - 1 + k > ge) {
+        S.kind = LANE_HARD;
+        return (void)LANE_HARD_WHY(4);
+    }
+    // ---- mismatching bases against the genome from A on
     uint64_t U0 = 0, U1 = 0;  // windows touching a mismatch: [e - k + 1, e] for every mismatching base e
     uint32_t nmis = 0;
 #pragma unroll
@@ -309,24 +318,24 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
                            : 0ull;
         }
     }
-    // ---- walked windows: classes from the tile
+    // ---- walked windows: classes from the tile, 32 windows per step
     const bool has_mg = a.prm.flags & F_MG;
     uint32_t nspec = 0, nincl = 0, hr = 0;
     uint64_t P0 = 0, P1 = 0;
-    const uint16_t *tc = a.tile16 + A;
-    // 32 windows per step: their tile entries are loaded together (one round trip)
 #pragma unroll 1
     for (uint32_t w0 = 0; w0 < W; w0 += 32) {
-        uint32_t v32[32];
+        if (w0) {
 #pragma unroll
-        for (int i = 0; i < 32; i++) v32[i] = (w0 + i < W) ? (uint32_t)tc[w0 + i] : 0u;
-        const uint64_t um = (w0 < 64 ? U0 : U1) >> (w0 & 63);  // unmatched windows of the step
+            for (int j = 0; j < 17; j++) td[j] = t32[(w0 >> 1) + j];
+        }
+        const uint32_t um = (uint32_t)((w0 < 64 ? U0 : U1) >> (w0 & 63));  // unmatched windows of the step
         uint32_t pend = 0;
 #pragma unroll
         for (int i = 0; i < 32; i++) {
             const uint32_t w = w0 + i;
             if (w >= W) break;
-            const uint32_t v = ((um >> i) & 1) ? 0u : v32[i];
+            const uint32_t x = i + odd;  // u16 index from the even start
+            const uint32_t v = ((um >> i) & 1) ? 0u : ((x & 1) ? (td[x >> 1] >> 16) : (td[x >> 1] & 0xFFFFu));
             if (!(v & PA_T16_VALID)) {
                 pend |= 1u << i;
                 continue;
@@ -453,9 +462,15 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows are done with
         if (r < a.n) lane_prep<NEED_Q>(a, r, LW.R[lane], S);
+#ifdef PA_STATS
+        if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
+#endif
 #pragma unroll 1
         for (int attempt = 0; attempt < 2; attempt++) {
             if (S.kind == LANE_WALK) lane_walk(a, LW.R[lane], S);
+#ifdef PA_STATS
+            if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
+#endif
             if (!__ballot(S.kind == LANE_WALK)) break;
             lane_probe_wave(a, LW, S);
             if (S.kind == LANE_WALK) {
