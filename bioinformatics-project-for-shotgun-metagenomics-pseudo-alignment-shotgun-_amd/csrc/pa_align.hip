@@ -66,6 +66,7 @@ struct AlignArgs {
     uint64_t tile_n;
     const uint64_t *goff;           // genome start positions [G + 1] (concatenated coordinates)
     const uint16_t *tile16;         // lane kernel tile (null: no lane kernel)
+    const uint32_t *tile_nb;        // one-substitution neighbour bits (null: none)
     int walk_rounds;
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
     int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
@@ -537,6 +538,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_pk = idx->tile_pk;
     a.goff = idx->goff;
     a.tile16 = idx->tile_cls ? idx->tile16 : nullptr;
+    a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
     a.lane_maxpend = 96;

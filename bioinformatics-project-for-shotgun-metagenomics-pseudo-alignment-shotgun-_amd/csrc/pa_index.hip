@@ -437,6 +437,37 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
     }
 }
 
+// One-substitution neighbours of every indexed genome window, for the lane
+// kernel: bit i of nb[3 p + b] says whether the k-mer starting at p - k + 1 + i
+// with its base at p replaced by the b-th other base ((genome base + 1 + b) & 3)
+// is in the index.  A read window that matches the genome except at one base
+// p is then resolved by one bit -- all k windows around a sequencing error by
+// one word -- instead of k table probes.  Defined on the 2-bit genome string
+// (N packed as A), for windows that are indexed themselves (tile_cls != NONE).
+__global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
+                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t *nb) {
+    const int sh = 64 - 2 * k;
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; t < n; t += stride) {
+        if (tile_cls[t] == NONE) continue;
+        const uint64_t K = get64_at(pk, 2 * t) >> sh;
+        for (int j = 0; j < k; j++) {
+            const int bs = 2 * (k - 1 - j);
+            const uint64_t cj = (K >> bs) & 3;
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                Key<1> key;
+                key.w[0] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
+                uint64_t slot;
+                uint32_t cls, tpos;
+                if (table_find<1>(table, hc.cap, key, home_of<1>(key, key_hash(key), hc), slot, cls, tpos))
+                    atomicOr(&nb[3 * (t + j) + b], 1u << (k - 1 - j));
+            }
+        }
+    }
+}
+
 // Compact tile for the lane kernel (pa_lane.h): per position 0 (no indexed
 // window) or PA_T16_VALID | [PA_T16_REP] | [PA_T16_SPEC] | min(set size, 8191).
 __global__ void k_tile16(const uint32_t *__restrict__ tile_cls, uint64_t n, uint32_t G,
@@ -711,6 +742,17 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_tile16, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
                                idx->tile_cls, n, G, idx->class_genomes, idx->tile16);
             idx->device_bytes += n * 2;
+            // one-substitution neighbours (12 B per base) when they fit a quarter of the free memory;
+            // PA_NO_NB=1 skips them (A/B measurements)
+            size_t free_b = 0, total_b = 0;
+            const char *no_nb = std::getenv("PA_NO_NB");
+            if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess && n * 12 <= free_b / 4) {
+                B_HIP(hipMalloc(&idx->tile_nb, n * 12 + 64));
+                B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 12 + 64, st));
+                hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
+                                   idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, idx->tile_nb);
+                idx->device_bytes += n * 12;
+            }
         }
         B_HIP(hipGetLastError());
         B_HIP(hipStreamSynchronize(st));
@@ -757,6 +799,8 @@ void index_release(pa_index *idx) {
     hipFree(idx->tile_cls);
     hipFree(idx->tile_pk);
     hipFree(idx->tile16);
+    hipFree(idx->tile_nb);
+    idx->tile_nb = nullptr;
     idx->tile_cls = nullptr;
     idx->tile_pk = nullptr;
     idx->tile16 = nullptr;

@@ -293,19 +293,23 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         S.kind = LANE_HARD;
         return (void)LANE_HARD_WHY(4);
     }
-    // ---- mismatching bases against the genome from A on
-    uint64_t U0 = 0, U1 = 0;  // windows touching a mismatch: [e - k + 1, e] for every mismatching base e
+    // ---- mismatching bases against the genome from A on.  U: windows with a
+    // mismatch, V: windows with two or more; with the neighbour bits (tile_nb)
+    // a window with exactly one mismatch is resolved by its bit (NP: the bits set)
+    uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0;
     uint32_t nmis = 0;
+    const bool has_nb = a.tile_nb != nullptr;
 #pragma unroll
     for (int i = 0; i < kLaneWords; i++) {
         if (32 * i >= (int)len) break;
-        uint64_t d = row[i] ^ (gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i]);
+        const uint64_t gwi = gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i];
+        uint64_t d = row[i] ^ gwi;
         const uint32_t rest = len - 32 * i;  // bases of the read in this word
         if (rest < 32) d &= ~0ull << (64 - 2 * rest);
         uint64_t m = (d | (d >> 1)) & 0x5555555555555555ull;  // one bit per mismatching base
         while (m) {
-            const uint32_t e = 32 * i + (__builtin_clzll(m) >> 1);
-            m &= ~(1ull << (62 - 2 * (e & 31)));
+            const uint32_t j = __builtin_clzll(m) >> 1, e = 32 * i + j;
+            m &= ~(1ull << (62 - 2 * j));
             if (++nmis > 8) {  // a wrong stretch, not a few sequencing errors
                 S.kind = LANE_HARD;
                 return (void)LANE_HARD_WHY(5);
@@ -313,10 +317,32 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             const int32_t lo = (int32_t)e - k + 1 < 0 ? 0 : (int32_t)e - k + 1;
             const int32_t hi = (int32_t)e < (int32_t)W - 1 ? (int32_t)e : (int32_t)W - 1;
             if (lo > hi) continue;
-            U0 |= lo < 64 ? ((~0ull << lo) & (hi >= 63 ? ~0ull : ((2ull << hi) - 1))) : 0ull;
-            U1 |= hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) & (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
-                           : 0ull;
+            const uint64_t r0 = lo < 64 ? ((~0ull << lo) & (hi >= 63 ? ~0ull : ((2ull << hi) - 1))) : 0ull;
+            const uint64_t r1 =
+                hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) & (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
+                         : 0ull;
+            V0 |= U0 & r0;
+            V1 |= U1 & r1;
+            U0 |= r0;
+            U1 |= r1;
+            if (has_nb) {
+                // neighbour word of the genome base at A + e and the read's base there
+                const uint32_t cg = (uint32_t)(gwi >> (62 - 2 * j)) & 3u, cr = (uint32_t)(row[i] >> (62 - 2 * j)) & 3u;
+                const uint64_t nbw = a.tile_nb[3 * ((uint64_t)A + e) + ((cr - cg - 1) & 3u)];
+                // bit q <-> window e - k + 1 + q
+                const int32_t sft = (int32_t)e - k + 1;
+                if (sft >= 0) {
+                    NP0 |= sft < 64 ? nbw << sft : 0ull;
+                    NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 32 ? nbw >> (64 - sft) : 0ull);
+                } else {
+                    NP0 |= nbw >> (-sft);
+                }
+            }
         }
+    }
+    if (!has_nb) {
+        NP0 = ~0ull;  // every mismatching window is probed
+        NP1 = ~0ull;
     }
     // ---- walked windows: classes from the tile, 32 windows per step
     const bool has_mg = a.prm.flags & F_MG;
@@ -328,16 +354,24 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
 #pragma unroll
             for (int j = 0; j < 17; j++) td[j] = t32[(w0 >> 1) + j];
         }
-        const uint32_t um = (uint32_t)((w0 < 64 ? U0 : U1) >> (w0 & 63));  // unmatched windows of the step
+        const uint32_t sft = w0 & 63;
+        const uint32_t um = (uint32_t)((w0 < 64 ? U0 : U1) >> sft);   // windows with a mismatch
+        const uint32_t vm = (uint32_t)((w0 < 64 ? V0 : V1) >> sft);   //   with two or more
+        const uint32_t nm = (uint32_t)((w0 < 64 ? NP0 : NP1) >> sft); //   neighbour present
         uint32_t pend = 0;
 #pragma unroll
         for (int i = 0; i < 32; i++) {
             const uint32_t w = w0 + i;
             if (w >= W) break;
             const uint32_t x = i + odd;  // u16 index from the even start
-            const uint32_t v = ((um >> i) & 1) ? 0u : ((x & 1) ? (td[x >> 1] >> 16) : (td[x >> 1] & 0xFFFFu));
-            if (!(v & PA_T16_VALID)) {
+            const uint32_t v = (x & 1) ? (td[x >> 1] >> 16) : (td[x >> 1] & 0xFFFFu);
+            if (!(v & PA_T16_VALID)) {  // not an indexed genome window: probe
                 pend |= 1u << i;
+                continue;
+            }
+            if ((um >> i) & 1) {
+                // one mismatch: absent unless its neighbour bit is set; more: probe
+                if (((vm | nm) >> i) & 1) pend |= 1u << i;
                 continue;
             }
             if (v & PA_T16_REP) {  // the k-mer may repeat inside the read
