@@ -19,10 +19,12 @@ indices rank*10M ...), and value = all ranks' reads / max-over-ranks time.
 
 roofline: algorithmic bytes per read B = L + q*L + (L-k+1)*16 (ASCII bases,
 qualities when a quality filter is on, one 8-B key + 8-B value slot per
-window) x reads per launch / the fast kernel's average
-duration, measured with HIP events recorded by libpa on the stream it launches
-on.  traffic: HBM bytes per launch from rocprofv3 PMC counters when a summary
-for this config is committed under profiles/ (else null).
+window) x reads per pass / the align pass's average
+duration -- the lane kernel plus the wave kernel over the reads the lane kernel
+leaves to it (k_align_lane + k_align_fast) -- measured
+with HIP events recorded by libpa on the stream it launches them on.  traffic:
+HBM-side bytes per pass (FETCH_SIZE of both kernels) from the rocprofv3 PMC
+summary committed under profiles/ for this config (else null).
 
 cpu_baseline (rank 0, N=1): the C restatement oracle/pa_oracle.c (single
 thread) timed on a bounded prefix of the same device-generated reads; the same
@@ -203,7 +205,7 @@ def main():
                    "filters": cfg["params"] or None, "parallelism": f"read-sharded x{world}, index replicated"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_align_fast", "kernel_ms": kern_s * 1e3, "bytes_per_read": b_read},
+                     "kernel": "align pass: k_align_lane + k_align_fast", "kernel_ms": kern_s * 1e3, "bytes_per_read": b_read},
         "deferred_read_fraction": deferred / max(npg * args.steps, 1),
         "index": {"build_s": build_s, "n_kmers": int(info.n_kmers), "multi_genome_sets": int(info.n_multi_classes),
                   "table_bytes": int(info.table_bytes)},
