@@ -627,7 +627,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     a.dbg = (unsigned long long *)idx->counters + 4;
     PA_HIP(hipMemsetAsync(idx->counters, 0, 8, st));
 #ifdef PA_STATS
-    PA_HIP(hipMemsetAsync(a.dbg, 0, 104, st));
+    PA_HIP(hipMemsetAsync(a.dbg, 0, 160, st));
 #endif
     ExactArgs x{};
     unsigned egrid = 0;
@@ -669,13 +669,14 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     launch_exact_nw(idx->nw, x, egrid, st);
     PA_HIP(hipGetLastError());
 #ifdef PA_STATS
-    unsigned long long d[17];
-    PA_HIP(hipMemcpyAsync(d, idx->counters, 136, hipMemcpyDeviceToHost, st));
+    unsigned long long d[24];
+    PA_HIP(hipMemcpyAsync(d, idx->counters, 192, hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
     fprintf(stderr, "[pa_stats] reads %llu lane-hard %llu exact %llu | wave kernel: windows %llu probed %llu walk %llu anchors %llu\n",
             (unsigned long long)r->n, d[3], d[0], d[4], d[5], d[6], d[7]);
     fprintf(stderr, "[pa_stats] lane hard reasons: long %llu mkq %llu bad %llu no-anchor %llu range %llu mismatches %llu rep %llu found %llu pending %llu\n",
             d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], d[16]);
+    fprintf(stderr, "[pa_stats] lane: cooperative probes %llu re-anchors %llu neighbour words %llu\n", d[18], d[19], d[20]);
 #endif
     return PA_OK;
 }

@@ -40,6 +40,9 @@ constexpr int kLaneWords = 6;     // 64-bit words of the packed read (32 bases e
 #ifndef PA_LANE_PROBES
 #define PA_LANE_PROBES 4  // unwalked windows probed per lane and cooperative pass
 #endif
+#ifndef PA_LANE_SEEDS
+#define PA_LANE_SEEDS 5   // seed windows probed per read (first ... last, evenly spread)
+#endif
 #ifndef PA_LANE_SLOTS
 #define PA_LANE_SLOTS 1   // table slots per probe step in the cooperative passes
 #endif
@@ -236,25 +239,30 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
     row[kLaneWords] = 0;
     if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
     const int sh = 64 - 2 * k;
-    // ---- seeds: first, middle, last window
-    const uint32_t sw[3] = {0u, (W - 1) >> 1, W - 1};
-    uint64_t skey[3];
+    // ---- seeds: NSEED windows spread evenly from the first to the last; a
+    // specific one (its genome is the read's) is preferred as the anchor
+    constexpr int NSEED = PA_LANE_SEEDS;
+    uint32_t sw[NSEED];
+    uint64_t skey[NSEED];
 #pragma unroll
-    for (int i = 0; i < 3; i++) skey[i] = row_bits(row, 2 * sw[i]) >> sh;
-    uint32_t sfound, scls[3], stp[3];
-    lane_probe<3>(a, skey, 7u, sfound, scls, stp);
+    for (int i = 0; i < NSEED; i++) {
+        sw[i] = (uint32_t)(((uint64_t)(W - 1) * i) / (NSEED - 1));
+        skey[i] = row_bits(row, 2 * sw[i]) >> sh;
+    }
+    uint32_t sfound, scls[NSEED], stp[NSEED];
+    lane_probe<NSEED>(a, skey, (1u << NSEED) - 1, sfound, scls, stp);
     int at = -1;
 #pragma unroll
     for (int pass = 0; pass < 2; pass++)
 #pragma unroll
-        for (int i = 0; i < 3; i++)
+        for (int i = 0; i < NSEED; i++)
             if (at < 0 && bit(sfound, i) && stp[i] != NONE && (pass == 1 || scls[i] < a.G)) at = i;
     if (at < 0) return (void)LANE_HARD_WHY(3);  // no anchor
     S.atp = stp[0];
     S.acls = scls[0];
     S.aw = sw[0];
 #pragma unroll
-    for (int i = 1; i < 3; i++)
+    for (int i = 1; i < NSEED; i++)
         if (at == i) {
             S.atp = stp[i];
             S.acls = scls[i];
@@ -329,6 +337,9 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
                 // neighbour word of the genome base at A + e and the read's base there
                 const uint32_t cg = (uint32_t)(gwi >> (62 - 2 * j)) & 3u, cr = (uint32_t)(row[i] >> (62 - 2 * j)) & 3u;
                 const uint64_t nbw = a.tile_nb[3 * ((uint64_t)A + e) + ((cr - cg - 1) & 3u)];
+#ifdef PA_STATS
+                atomicAdd(&a.dbg[16], 1ull);
+#endif
                 // bit q <-> window e - k + 1 + q
                 const int32_t sft = (int32_t)e - k + 1;
                 if (sft >= 0) {
@@ -415,6 +426,9 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
     const uint32_t incl = wave_incl_scan(c);
     const uint32_t pre = incl - c;
     const uint32_t total = __shfl(incl, 63);
+#ifdef PA_STATS
+    if (lane == 0 && total) atomicAdd(&a.dbg[14], (unsigned long long)total);
+#endif
     uint64_t Q0 = walking ? S.P0 : 0, Q1 = walking ? S.P1 : 0;
     for (uint32_t base = 0; base < total; base += kPassEntries) {
         // this pass's entries of the lane: global indices [max(pre, base), min(pre + c, base + 256))
@@ -511,6 +525,9 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
                 const uint32_t fl = LW.flags[lane];
                 if (fl & 1u) {  // a specific k-mer off the walk: walk again from it (once)
                     if (attempt == 0) {
+#ifdef PA_STATS
+                        atomicAdd(&a.dbg[15], 1ull);
+#endif
                         const unsigned long long cd = LW.cand[lane];
                         S.atp = (uint32_t)cd;
                         S.aw = (uint32_t)(cd >> 32);
