@@ -365,6 +365,11 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
 #pragma unroll
             for (int j = 0; j < 17; j++) td[j] = t32[(w0 >> 1) + j];
         }
+        // align the step's entries to an even start (no runtime register indexing below)
+        if (odd) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) td[j] = (td[j] >> 16) | (td[j + 1] << 16);
+        }
         const uint32_t sft = w0 & 63;
         const uint32_t um = (uint32_t)((w0 < 64 ? U0 : U1) >> sft);   // windows with a mismatch
         const uint32_t vm = (uint32_t)((w0 < 64 ? V0 : V1) >> sft);   //   with two or more
@@ -374,8 +379,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         for (int i = 0; i < 32; i++) {
             const uint32_t w = w0 + i;
             if (w >= W) break;
-            const uint32_t x = i + odd;  // u16 index from the even start
-            const uint32_t v = (x & 1) ? (td[x >> 1] >> 16) : (td[x >> 1] & 0xFFFFu);
+            const uint32_t v = (i & 1) ? (td[i >> 1] >> 16) : (td[i >> 1] & 0xFFFFu);
             if (!(v & PA_T16_VALID)) {  // not an indexed genome window: probe
                 pend |= 1u << i;
                 continue;
