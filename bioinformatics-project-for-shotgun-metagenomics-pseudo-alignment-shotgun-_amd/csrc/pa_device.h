@@ -118,39 +118,12 @@ __device__ __forceinline__ uint64_t window_bits(const uint64_t *bm, uint32_t w, 
     return v & ((1ull << k) - 1);
 }
 
-// Where a key starts probing.  With m > 0 (k <= 31), the home slot lies in a
-// region of R slots chosen by the key's MINIMIZER -- the m-mer of the k-mer with
-// the smallest hash -- and the key's own hash picks the slot inside the region.
-// Consecutive windows of a read share their minimizer most of the time (a
-// "super-k-mer"), so their probes land in the same few cache lines and one wave
-// load instruction coalesces them into a handful of HBM requests.  Any key's
-// home is a pure function of the key, so build and lookup agree exactly.
-// (HomeCfg: pa_home.h)
-
-__device__ __forceinline__ uint32_t mmer_hash(uint32_t x) {
-    x *= 0x9E3779B1u;
-    x ^= x >> 15;
-    x *= 0x85EBCA77u;
-    x ^= x >> 13;
-    return x;
-}
-
-// Minimizer hash of a single-word k-mer key (m <= 16).
-__device__ __forceinline__ uint32_t minimizer_hash(uint64_t K, int k, int m) {
-    const uint32_t mask = m >= 16 ? 0xFFFFFFFFu : ((1u << (2 * m)) - 1);
-    uint32_t best = 0xFFFFFFFFu;
-    for (int sh = 2 * (k - m); sh >= 0; sh -= 2) best = min(best, mmer_hash((uint32_t)(K >> sh) & mask));
-    return best;
-}
-
+// Where a key starts probing: multiply-high range reduction of its hash over
+// the table's capacity.  (A minimizer-region variant -- keys of one super-k-mer
+// homed in one region -- measured 1.7-3x slower on C2 and was removed; the
+// genome walk of pa_fast.h / pa_lane.h gets the locality instead.)
 template <int NW>
-__device__ __forceinline__ uint64_t home_of(const Key<NW> &key, uint64_t h, const HomeCfg &c) {
-    if constexpr (NW == 1) {
-        if (c.m > 0) {
-            const uint32_t mh = mmer_hash(minimizer_hash(key.w[0], c.k, c.m) ^ 0x5BD1E995u);
-            return (((uint64_t)mh * c.nreg) >> 32) * c.R + (h & (c.R - 1));
-        }
-    }
+__device__ __forceinline__ uint64_t home_of(const Key<NW> &, uint64_t h, const HomeCfg &c) {
     return home_slot(h, c.cap);
 }
 

@@ -5,9 +5,9 @@
 
 namespace pad {
 
-// Where a key starts probing: with m > 0 the home slot lies in a region of R
-// slots chosen by the key's minimizer (see home_of in pa_device.h); m == 0 is
-// plain multiply-high hashing over all cap slots.
+// Where a key starts probing (home_of in pa_device.h): multiply-high hashing
+// over all cap slots.  nreg / R / k / m are kept for the layout of the struct
+// (m is always 0).
 struct HomeCfg {
     uint64_t cap;    // slots (a multiple of R when m > 0)
     uint64_t nreg;   // cap / R

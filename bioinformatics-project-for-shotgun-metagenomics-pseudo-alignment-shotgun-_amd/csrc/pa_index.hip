@@ -827,23 +827,8 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     }
     for (auto &o : idx->h_goff) o -= goff[0];
     idx->total_windows = windows;
-    // Home slots: plain hashing by default.  PA_MINIMIZER_M=m (single-word keys)
-    // places keys in R-slot regions chosen by their minimizer instead; measured
-    // on C2 it is 1.7-3x SLOWER (regions that collect several minimizers
-    // overflow into long linear-probing chains, and a wave waits for its
-    // slowest lane), so it stays an experiment.
-    int m = 0;
-    uint32_t R = 1;
-    if (std::getenv("PA_MINIMIZER_M") && k >= 20 && idx->nw == 1) {
-        R = 32;
-        if (const char *e = std::getenv("PA_MINIMIZER_M")) m = std::atoi(e);
-        if (const char *e = std::getenv("PA_REGION_SLOTS")) R = (uint32_t)std::atoi(e);
-        if (m < 0 || m > 16 || m > k || R == 0 || (R & (R - 1))) {
-            set_error("invalid PA_MINIMIZER_M / PA_REGION_SLOTS");
-            return PA_EINVAL;
-        }
-        if (m == 0) R = 1;
-    }
+    const int m = 0;
+    const uint32_t R = 1;
     // genome tiling for single-word keys while positions fit 32 bits (tpos);
     // PA_NO_TILE=1 turns it off (A/B measurements)
     const char *no_tile = std::getenv("PA_NO_TILE");

@@ -374,33 +374,40 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         const uint32_t um = (uint32_t)((w0 < 64 ? U0 : U1) >> sft);   // windows with a mismatch
         const uint32_t vm = (uint32_t)((w0 < 64 ? V0 : V1) >> sft);   //   with two or more
         const uint32_t nm = (uint32_t)((w0 < 64 ? NP0 : NP1) >> sft); //   neighbour present
-        uint32_t pend = 0;
+        const uint32_t nwin = W - w0 < 32 ? W - w0 : 32u;
+        const uint32_t inw = nwin >= 32 ? ~0u : ((1u << nwin) - 1);
+        // the flags of the step's 32 entries as bit masks (window i = bit i)
+        uint32_t valid = 0, rep = 0, spec = 0;
 #pragma unroll
-        for (int i = 0; i < 32; i++) {
-            const uint32_t w = w0 + i;
-            if (w >= W) break;
-            const uint32_t v = (i & 1) ? (td[i >> 1] >> 16) : (td[i >> 1] & 0xFFFFu);
-            if (!(v & PA_T16_VALID)) {  // not an indexed genome window: probe
-                pend |= 1u << i;
-                continue;
-            }
-            if ((um >> i) & 1) {
-                // one mismatch: absent unless its neighbour bit is set; more: probe
-                if (((vm | nm) >> i) & 1) pend |= 1u << i;
-                continue;
-            }
-            if (v & PA_T16_REP) {  // the k-mer may repeat inside the read
-                S.kind = LANE_HARD;
-                return (void)LANE_HARD_WHY(6);
-            }
-            if (has_mg && (int64_t)(v & PA_T16_SIZE) > (int64_t)a.prm.mg) {
-                hr++;  // highly redundant (src/kmer.py:425-427)
-                continue;
-            }
-            nincl++;
-            // a specific k-mer at a position inside genome g is specific to g
-            nspec += (v & PA_T16_SPEC) ? 1u : 0u;
+        for (int j = 0; j < 16; j++) {
+            const uint32_t x = td[j];
+            valid |= (((x >> 15) & 1u) | ((x >> 30) & 2u)) << (2 * j);
+            rep |= (((x >> 14) & 1u) | ((x >> 29) & 2u)) << (2 * j);
+            spec |= (((x >> 13) & 1u) | ((x >> 28) & 2u)) << (2 * j);
         }
+        valid &= inw;
+        // probe: not an indexed genome window, or a mismatch that the neighbour
+        // bits do not settle (two or more in the window, or the neighbour present)
+        const uint32_t pend = (inw & ~valid) | (valid & um & (vm | nm));
+        const uint32_t walked = valid & ~um;
+        if (walked & rep) {  // a k-mer that may repeat inside the read
+            S.kind = LANE_HARD;
+            return (void)LANE_HARD_WHY(6);
+        }
+        uint32_t big = 0;  // highly redundant walked windows (src/kmer.py:425-427)
+        if (has_mg) {
+#pragma unroll
+            for (int i = 0; i < 32; i++) {
+                const uint32_t v = (i & 1) ? (td[i >> 1] >> 16) : (td[i >> 1] & 0xFFFFu);
+                big |= ((int64_t)(v & PA_T16_SIZE) > (int64_t)a.prm.mg ? 1u : 0u) << i;
+            }
+            big &= walked;
+        }
+        const uint32_t incl = walked & ~big;
+        hr += __popc(big);
+        nincl += __popc(incl);
+        // a specific k-mer at a position inside genome g is specific to g
+        nspec += __popc(incl & spec);
         if (w0 < 64)
             P0 |= (uint64_t)pend << w0;
         else
