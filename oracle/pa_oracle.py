@@ -187,6 +187,41 @@ class OracleIndex:
         return AlignResult(types, qf, hr, lo, lists, stats, uq, am, fk)
 
 
+def align_counts_parallel(index: "OracleIndex", seq: np.ndarray, qual: np.ndarray, read_off: np.ndarray,
+                          threads: int, m=1, p=1, mrq=None, mkq=None, mg=None, read_base: int = 0) -> AlignResult:
+    """Counters of ``index.align(..., detail=False)`` computed by ``threads`` host
+    threads over contiguous read shards (ctypes releases the GIL inside
+    ``ora_align``; the index is read-only).  Sums of the per-shard counters and
+    min of the first keys (shards carry their global read base) equal the
+    single-thread result exactly.  CPU-baseline helper for bench.py."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    n = len(read_off) - 1
+    threads = max(1, min(int(threads), max(n, 1)))
+    cuts = [n * i // threads for i in range(threads + 1)]
+
+    def shard(i):
+        a, b = cuts[i], cuts[i + 1]
+        lo, hi = int(read_off[a]), int(read_off[b])
+        off = (read_off[a:b + 1] - read_off[a]).astype(np.uint64)
+        return index.align(seq[lo:hi].tobytes(), qual[lo:hi].tobytes(), off, m=m, p=p, mrq=mrq, mkq=mkq, mg=mg,
+                           read_base=read_base + a, detail=False)
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        parts = list(ex.map(shard, range(threads)))
+    G = index.n_genomes
+    out = AlignResult(np.zeros(0, np.uint8), np.zeros(0, np.uint32), np.zeros(0, np.uint32),
+                      np.zeros(1, np.uint64), np.zeros(0, np.uint32), np.zeros(6, np.uint64),
+                      np.zeros(G, np.uint64), np.zeros(G, np.uint64),
+                      np.full(G, np.iinfo(np.uint64).max, dtype=np.uint64))
+    for r in parts:
+        out.stats += r.stats
+        out.unique += r.unique
+        out.ambiguous += r.ambiguous
+        np.minimum(out.first_key, r.first_key, out=out.first_key)
+    return out
+
+
 def summary_by_walk(result: AlignResult, identifiers: Sequence[str], mrq=None, mkq=None, mg=None) -> dict:
     """get_summary (src/kmer.py:622-657) computed by walking reads in order."""
     stats = {"unique_mapped_reads": 0, "ambiguous_mapped_reads": 0, "unmapped_reads": 0}

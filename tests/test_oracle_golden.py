@@ -88,3 +88,19 @@ def test_oracle_first_key_matches_walk_order():
         if fk != np.iinfo(np.uint64).max:
             keys[idents[g]] = min(keys.get(idents[g], fk), fk)
     assert list(walk["Summary"].keys()) == sorted(keys, key=keys.get)
+
+
+def test_oracle_parallel_shards_equal_single_thread():
+    """bench.py's multi-thread CPU baseline: sharded counters == one pass."""
+    import synth
+    gens = synth.family_genomes(6, 6000, seed=4, family_size=3, sub_rate=0.02, conserved_len=300)
+    seq, qual, _ = synth.sample_reads(gens, 3001, 100, seed=5, err_rate=0.01)
+    off = np.arange(3002, dtype=np.uint64) * 100
+    ix = O.OracleIndex(gens, 21)
+    for kw in (dict(), dict(m=0, p=0, mrq=58, mkq=59, mg=2)):
+        one = ix.align(seq.tobytes(), qual.tobytes(), off, read_base=9, detail=False, **kw)
+        par = O.align_counts_parallel(ix, seq.reshape(-1), qual.reshape(-1), off, 4, read_base=9, **kw)
+        assert par.stats.tolist() == one.stats.tolist()
+        assert par.unique.tolist() == one.unique.tolist()
+        assert par.ambiguous.tolist() == one.ambiguous.tolist()
+        assert par.first_key.tolist() == one.first_key.tolist()
