@@ -146,11 +146,14 @@ struct ExactWs {
     uint32_t *wcls;
     uint64_t *dh_key;
     uint32_t *dh_min;
+    uint32_t *ch_key, *ch_cnt, *ch_min;  // distinct multi-genome sets of the read: id, k-mers, first window
+    uint32_t *cls_list;                  // their hash positions, in insertion order
     uint32_t *g_spec, *g_specmin, *g_tot, *g_totmin, *touched;
 };
 
 __host__ __device__ inline uint64_t exact_ws_stride(uint32_t wcap, uint32_t dh, uint32_t G) {
-    uint64_t b = (uint64_t)wcap * 8 + (uint64_t)dh * 8 + (uint64_t)wcap * 4 + (uint64_t)dh * 4 + (uint64_t)G * 20;
+    uint64_t b = (uint64_t)wcap * 8 + (uint64_t)dh * 8 + (uint64_t)wcap * 4 + (uint64_t)dh * 4 + (uint64_t)dh * 12 +
+                 (uint64_t)wcap * 4 + (uint64_t)G * 20;
     return (b + 255) / 256 * 256;
 }
 
@@ -160,7 +163,11 @@ __device__ inline ExactWs exact_ws(unsigned char *base, uint32_t wcap, uint32_t 
     w.dh_key = w.wslot + wcap;
     w.wcls = (uint32_t *)(w.dh_key + dh);
     w.dh_min = w.wcls + wcap;
-    w.g_spec = w.dh_min + dh;
+    w.ch_key = w.dh_min + dh;
+    w.ch_cnt = w.ch_key + dh;
+    w.ch_min = w.ch_cnt + dh;
+    w.cls_list = w.ch_min + dh;
+    w.g_spec = w.cls_list + wcap;
     w.g_specmin = w.g_spec + G;
     w.g_tot = w.g_specmin + G;
     w.g_totmin = w.g_tot + G;
@@ -206,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
     const AlignArgs &a = x.a;
     __shared__ uint32_t red[kWaves];
     __shared__ unsigned long long red64[kWaves];
-    __shared__ uint32_t n_touched;
+    __shared__ uint32_t n_touched, n_cls;
     const uint32_t G = a.G;
     const int k = a.k;
     const uint64_t mask0 = k > 0 ? mask0_of(k, NW) : 0;
@@ -220,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
         st_agent(&ws.g_tot[g], 0u);
         st_agent(&ws.g_totmin[g], NONE);
     }
-    if (threadIdx.x == 0) n_touched = 0;
+    if (threadIdx.x == 0) n_touched = n_cls = 0;
     __syncthreads();
     const uint64_t nq = x.use_queue ? *a.qcount : a.n;
     if (blockIdx.x == 0 && threadIdx.x == 0 && x.use_queue && a.deferred_total) atomicAdd(a.deferred_total, nq);
@@ -252,6 +259,9 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
         for (uint32_t i = threadIdx.x; i < x.dh; i += kBlock) {
             st_agent(&ws.dh_key[i], EMPTY);
             st_agent(&ws.dh_min[i], NONE);
+            st_agent(&ws.ch_key[i], NONE);
+            st_agent(&ws.ch_cnt[i], 0u);
+            st_agent(&ws.ch_min[i], NONE);
         }
         __syncthreads();
         // ---- windows
@@ -301,7 +311,12 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
         uint8_t type = PA_UNMAPPED;
         uint32_t list_len = 0;
         if (any) {
-            // ---- distinct k-mers -> specific and total counts per genome
+            // ---- distinct k-mers -> specific and total counts per genome.  A
+            // specific k-mer counts for its genome directly; the others are first
+            // grouped by genome set (a read's k-mers fall in a handful of sets, e.g.
+            // one set of every genome for a conserved stretch), and every set then
+            // adds its k-mer count and first window to its genomes once, the
+            // block striding over the set's genome list.
             for (uint32_t w = threadIdx.x; w < W; w += kBlock) {
                 const uint64_t slot = ws.wslot[w];
                 if (slot == EMPTY) continue;
@@ -309,22 +324,37 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
                 while (ld_agent(&ws.dh_key[p]) != slot) p = (p + 1) & (x.dh - 1);
                 if (ld_agent(&ws.dh_min[p]) != w) continue;
                 const uint32_t c = ws.wcls[w];
-                const uint32_t *gl;
-                uint32_t sz, single = c;
                 if (c < G) {
                     atomicAdd(&ws.g_spec[c], 1u);
                     atomicMin(&ws.g_specmin[c], w);
-                    gl = &single;
-                    sz = 1;
+                    if (atomicAdd(&ws.g_tot[c], 1u) == 0) ws.touched[atomicAdd(&n_touched, 1u)] = c;
+                    atomicMin(&ws.g_totmin[c], w);
                 } else {
-                    const uint32_t *rec = a.class_genomes + (c - G);  // [size, genomes...]
-                    gl = rec + 1;
-                    sz = rec[0];
+                    uint32_t q = (uint32_t)(fmix64(c) & (x.dh - 1));
+                    for (;;) {
+                        const uint32_t old = atomicCAS(&ws.ch_key[q], NONE, c);
+                        if (old == NONE) {
+                            ws.cls_list[atomicAdd(&n_cls, 1u)] = q;
+                            break;
+                        }
+                        if (old == c) break;
+                        q = (q + 1) & (x.dh - 1);
+                    }
+                    atomicAdd(&ws.ch_cnt[q], 1u);
+                    atomicMin(&ws.ch_min[q], w);
                 }
-                for (uint32_t j = 0; j < sz; j++) {
-                    const uint32_t g = gl[j];
-                    if (atomicAdd(&ws.g_tot[g], 1u) == 0) ws.touched[atomicAdd(&n_touched, 1u)] = g;
-                    atomicMin(&ws.g_totmin[g], w);
+            }
+            __syncthreads();
+            const uint32_t ncl = n_cls;
+            for (uint32_t i = 0; i < ncl; i++) {
+                const uint32_t q = ld_agent(&ws.cls_list[i]);
+                const uint32_t c = ld_agent(&ws.ch_key[q]), cnt = ld_agent(&ws.ch_cnt[q]), mw = ld_agent(&ws.ch_min[q]);
+                const uint32_t *rec = a.class_genomes + (c - G);  // [size, genomes...]
+                const uint32_t sz = rec[0];
+                for (uint32_t j = threadIdx.x; j < sz; j += kBlock) {
+                    const uint32_t g = rec[1 + j];
+                    if (atomicAdd(&ws.g_tot[g], cnt) == 0) ws.touched[atomicAdd(&n_touched, 1u)] = g;
+                    atomicMin(&ws.g_totmin[g], mw);
                 }
             }
             __syncthreads();
@@ -434,7 +464,7 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
                 st_agent(&ws.g_totmin[g], NONE);
             }
             __syncthreads();
-            if (threadIdx.x == 0) n_touched = 0;
+            if (threadIdx.x == 0) n_touched = n_cls = 0;
             __syncthreads();
         }
         if (threadIdx.x == 0) {
@@ -483,7 +513,8 @@ pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
 pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
     const size_t shm = lane_lds_bytes(a.G);
-    auto kern = need_q ? k_align_lane<true> : k_align_lane<false>;
+    const bool win_q = (a.prm.flags & F_MKQ) != 0;
+    auto kern = win_q ? k_align_lane<true, true> : need_q ? k_align_lane<true, false> : k_align_lane<false, false>;
     if (shm > 64 * 1024) PA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     int per_cu = 0, dev = 0, cus = 256;
     PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, shm));

@@ -151,6 +151,8 @@ struct LaneRead {
     uint32_t atp, acls, aw;            // anchor: first occurrence, class, window
     uint32_t g, nspec, nincl, hr;      // walk results (anchor genome, counts)
     uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
+    uint64_t F0, F1;                   // windows failing --min-kmer-quality (never looked up)
+    uint32_t qf;                       // their number (src/kmer.py:420-423)
 };
 
 // 64 bits of an LDS row of MSB-first packed words starting at bit o.
@@ -166,11 +168,68 @@ __device__ __forceinline__ uint32_t in_read_mask(uint32_t p0, uint32_t shift, ui
     return (hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1)) & (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
 }
 
+// Windows of the read whose raw-ASCII quality sum is below mkq * k
+// (Read.kmer_quality, src/kmer.py:404-408, gate :420-423) as a 128-bit mask.
+// A running sum over the staged 16-B chunks: byte p enters, byte p - k leaves.
+// The leaving bytes of chunk c are bytes r .. r + 15 of the chunk pair
+// (lc, lc + 1), lc = floor((16c - k) / 16), r = (16c - k) mod 16 = (-k) mod 16
+// -- the same for every chunk and every lane.
+__device__ __forceinline__ void lane_window_quality(const AlignArgs &a, const uint4 *qp, uint32_t shift, uint32_t len,
+                                                    uint32_t nch, LaneRead &S) {
+    const int k = a.k;
+    const int64_t T64 = (int64_t)a.prm.mkq * (int64_t)k;
+    const uint32_t T = T64 <= 0 ? 0u : (T64 > (1 << 24) ? (1u << 24) : (uint32_t)T64);
+    const uint32_t r = (uint32_t)(-k) & 15u, rq = r >> 2, rb = r & 3u;
+    uint64_t F0 = 0, F1 = 0;
+    uint32_t run = 0;
+#pragma unroll 1
+    for (uint32_t c = 0; c < nch; c++) {
+        const uint4 v = qp[c];
+        const uint32_t cur[4] = {v.x, v.y, v.z, v.w};
+        const int32_t lc = ((int32_t)(16 * c) - k) >> 4;  // (floor)
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        const uint4 l0 = lc >= 0 ? qp[lc] : z, l1 = lc + 1 >= 0 ? qp[lc + 1] : z;
+        const uint32_t e[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+        uint32_t lag[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t lo = rq == 0 ? e[u] : rq == 1 ? e[u + 1] : rq == 2 ? e[u + 2] : e[u + 3];
+            const uint32_t hi = rq == 0 ? e[u + 1] : rq == 1 ? e[u + 2] : rq == 2 ? e[u + 3] : e[u + 4];
+            lag[u] = __builtin_amdgcn_alignbyte(hi, lo, rb);
+        }
+        uint32_t m16 = 0;
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const int32_t i = (int32_t)(16 * c + t) - (int32_t)shift;  // read position of the entering byte
+            const uint32_t in = (i >= 0 && i < (int32_t)len) ? ((cur[t >> 2] >> (8 * (t & 3))) & 255u) : 0u;
+            const uint32_t out = (i - k >= 0 && i - k < (int32_t)len) ? ((lag[t >> 2] >> (8 * (t & 3))) & 255u) : 0u;
+            run += in - out;
+            m16 |= ((i >= k - 1 && i < (int32_t)len && run < T) ? 1u : 0u) << t;
+        }
+        // bit t <-> window base + t
+        const int32_t base = (int32_t)(16 * c) - (int32_t)shift - k + 1;
+        const uint64_t m = m16;
+        if (base < 0) {
+            F0 |= base > -16 ? m >> (-base) : 0ull;
+        } else if (base < 64) {
+            F0 |= m << base;
+            F1 |= base > 48 ? m >> (64 - base) : 0ull;
+        } else if (base < 128) {
+            F1 |= m << (base - 64);
+        }
+    }
+    S.F0 = F0;
+    S.F1 = F1;
+    S.qf = (uint32_t)(__popcll(F0) + __popcll(F1));
+}
+
 // Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor.
-template <bool NEED_Q>
+template <bool NEED_Q, bool WIN_Q>
 __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64_t *row, LaneRead &S) {
     S.kind = LANE_HARD;
     S.hr = S.nspec = S.nincl = 0;
+    S.F0 = S.F1 = 0;
+    S.qf = 0;
     const int k = a.k;
     const uint32_t flags = a.prm.flags;
     const uint64_t o = a.off[r];
@@ -205,7 +264,10 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
             return;
         }
         // a window's mean is >= the read's minimum: if that passes, no window can fail
-        if ((flags & F_MKQ) && len >= (uint32_t)k && (int64_t)qmin < (int64_t)a.prm.mkq) return (void)LANE_HARD_WHY(1);
+        if ((flags & F_MKQ) && len >= (uint32_t)k && (int64_t)qmin < (int64_t)a.prm.mkq) {
+            if (!WIN_Q) return (void)LANE_HARD_WHY(1);
+            lane_window_quality(a, qp, shift, len, nch, S);
+        }
     }
     if (len < (uint32_t)k) {
         S.kind = LANE_UNMAPPED;  // no windows (src/kmer.py:91-92, 516-517)
@@ -273,6 +335,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
 
 // Phase 2: walk from the anchor; walked windows resolve from the tile, the
 // others are left in P0 / P1 for the cooperative probes.
+template <bool WIN_Q>
 __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *row, LaneRead &S) {
     const int k = a.k;
     const uint32_t W = S.W, len = S.len;
@@ -385,10 +448,12 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             rep |= (((x >> 14) & 1u) | ((x >> 29) & 2u)) << (2 * j);
             spec |= (((x >> 13) & 1u) | ((x >> 28) & 2u)) << (2 * j);
         }
-        valid &= inw;
+        // windows failing the k-mer quality filter are never looked up (src/kmer.py:420-423)
+        const uint32_t live = WIN_Q ? inw & ~(uint32_t)((w0 < 64 ? S.F0 : S.F1) >> sft) : inw;
+        valid &= live;
         // probe: not an indexed genome window, or a mismatch that the neighbour
         // bits do not settle (two or more in the window, or the neighbour present)
-        const uint32_t pend = (inw & ~valid) | (valid & um & (vm | nm));
+        const uint32_t pend = (live & ~valid) | (valid & um & (vm | nm));
         const uint32_t walked = valid & ~um;
         if (walked & rep) {  // a k-mer that may repeat inside the read
             S.kind = LANE_HARD;
@@ -495,8 +560,16 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
     }
 }
 
-template <bool NEED_Q>
-__global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
+// Waves per SIMD the register allocation must allow.  The kernel is bound by
+// the latency of random table / tile reads, so occupancy pays: 4 (128 VGPRs, a
+// few spilled dwords) measured +6 % on C2 over 3; the k-mer quality variant
+// spills too much at 4 and keeps 3.
+#ifndef PA_LANE_WAVES
+#define PA_LANE_WAVES 4
+#endif
+template <bool NEED_Q, bool WIN_Q>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIN_Q ? 3 : PA_LANE_WAVES)))
+void k_align_lane(AlignArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const uint32_t G = a.G;
     const int lane = lane_id();
@@ -512,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
         }
         __syncthreads();
     }
-    uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0, n_hr = 0;
+    uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0, n_hr = 0, n_qf = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     const uint64_t n_iter = (a.n + stride - 1) / stride;  // uniform trip count (wave-wide phases)
     for (uint64_t it = 0; it < n_iter; it++) {
@@ -520,13 +593,13 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
         LaneRead S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows are done with
-        if (r < a.n) lane_prep<NEED_Q>(a, r, LW.R[lane], S);
+        if (r < a.n) lane_prep<NEED_Q, WIN_Q>(a, r, LW.R[lane], S);
 #ifdef PA_STATS
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
 #pragma unroll 1
         for (int attempt = 0; attempt < 2; attempt++) {
-            if (S.kind == LANE_WALK) lane_walk(a, LW.R[lane], S);
+            if (S.kind == LANE_WALK) lane_walk<WIN_Q>(a, LW.R[lane], S);
 #ifdef PA_STATS
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif
@@ -585,19 +658,23 @@ __global__ __launch_bounds__(kBlock) void k_align_lane(AlignArgs a) {
         n_amb += S.kind == LANE_AMB;
         n_unm += S.kind == LANE_UNMAPPED;
         n_drop += S.kind == LANE_DROP;
-        n_hr += (S.kind == LANE_UNIQUE || S.kind == LANE_AMB || S.kind == LANE_UNMAPPED) ? S.hr : 0u;
+        const bool settled = S.kind == LANE_UNIQUE || S.kind == LANE_AMB || S.kind == LANE_UNMAPPED;
+        n_hr += settled ? S.hr : 0u;
+        if (WIN_Q) n_qf += settled ? S.qf : 0u;
     }
     n_uniq = wave_sum(n_uniq);
     n_amb = wave_sum(n_amb);
     n_unm = wave_sum(n_unm);
     n_drop = wave_sum(n_drop);
     n_hr = wave_sum(n_hr);
+    if (WIN_Q) n_qf = wave_sum(n_qf);
     if (lane == 0) {
         if (n_uniq) atomicAdd(&a.stats[0], (unsigned long long)n_uniq);
         if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
         if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
         if (n_drop) atomicAdd(&a.stats[3], (unsigned long long)n_drop);
         if (n_hr && (a.prm.flags & F_MG)) atomicAdd(&a.stats[5], (unsigned long long)n_hr);
+        if (WIN_Q && n_qf) atomicAdd(&a.stats[4], (unsigned long long)n_qf);
     }
     if (lds) {
         __syncthreads();
