@@ -1,5 +1,7 @@
 """FASTA / FASTQ files (drop-in for src/data_file.py): extension check, plain or
-gzip text, parsed into the containers of records.py."""
+gzip text, parsed into the containers of records.py -- by the native
+multi-threaded parser (libpa.so pa_parse_file) when the file is in its
+canonical subset, else by the exact regex grammar of records.py."""
 
 from __future__ import annotations
 
@@ -36,7 +38,17 @@ class DataFile:
     def get_container_type(self) -> RecordContainer:
         raise NotImplementedError("This method must be implemented in subclasses.")
 
+    NATIVE_KIND: Optional[int] = None  # pa_native.PA_FASTA / PA_FASTQ
+
     def parse_file(self, file_path: str) -> None:
+        # the native parser reads the file itself (mmap / zlib, host threads);
+        # None -> outside its canonical subset or unreadable: the exact path below
+        if self.NATIVE_KIND is not None and len(self.container) == 0:
+            import pa_native
+            cols = pa_native.parse_file(self.NATIVE_KIND, file_path)
+            if cols is not None:
+                self.container.load_columns(cols)
+                return
         try:
             self.container.parse_records(self.load_file(file_path))
         except NoRecordsInData:
@@ -54,6 +66,7 @@ class DataFile:
 
 class FASTAFile(DataFile):
     EXTENSIONS = {".fa", ".fa.gz"}
+    NATIVE_KIND = 0
 
     def get_container_type(self) -> FASTARecordContainer:
         return FASTARecordContainer()
@@ -61,6 +74,7 @@ class FASTAFile(DataFile):
 
 class FASTAQFile(DataFile):
     EXTENSIONS = {".fq", ".fq.gz"}
+    NATIVE_KIND = 1
 
     def get_container_type(self) -> FASTAQRecordContainer:
         return FASTAQRecordContainer()

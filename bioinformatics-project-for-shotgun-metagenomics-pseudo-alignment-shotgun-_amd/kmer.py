@@ -340,7 +340,7 @@ class _Batch:
 
 def _columnar(container) -> Tuple[List[str], np.ndarray, np.ndarray, np.ndarray]:
     if isinstance(container, FASTAQRecordContainer):
-        return container.ids, container.seq, container.qual, container.offsets
+        return container.id_sequence(), container.seq, container.qual, container.offsets
     ids, seqs, quals = [], [], []
     for rec in container:
         ids.append(rec.identifier)

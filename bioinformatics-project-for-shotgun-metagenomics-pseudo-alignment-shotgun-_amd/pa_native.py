@@ -16,7 +16,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PA_LIBRARY", os.path.join(HERE, "libpa.so"))
 
-PA_OK, PA_EINVAL, PA_ETYPE, PA_ENOMEM, PA_EDEVICE, PA_EUNSUPPORTED, PA_EINTERNAL = range(7)
+PA_OK, PA_EINVAL, PA_ETYPE, PA_ENOMEM, PA_EDEVICE, PA_EUNSUPPORTED, PA_EINTERNAL, PA_ENOTCANON, PA_EIO = range(9)
+PA_FASTA, PA_FASTQ = 0, 1
 PA_MAX_K = 159
 HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4
 NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
@@ -31,6 +32,7 @@ EXPORTS = (
     "pa_result_copy_in", "pa_result_free",
     "pa_align", "pa_align_detail", "pa_align_batch",
     "pa_profile_enable", "pa_profile_read",
+    "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free",
 )
 
 
@@ -119,6 +121,11 @@ def lib():
         "pa_align_batch": (I32, [P, P, P, P, U64, U64, ctypes.POINTER(Params), ctypes.POINTER(Stats), P, P, P, P]),
         "pa_profile_enable": (I32, [P, I32]),
         "pa_profile_read": (I32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        "pa_parse_text": (I32, [I32, P, U64, I32, I32, PP]),
+        "pa_parse_file": (I32, [I32, ctypes.c_char_p, I32, PP]),
+        "pa_seqset_sizes": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        "pa_seqset_export": (I32, [P, P, P, P, P]),
+        "pa_seqset_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -168,6 +175,110 @@ def device_count() -> int:
 
 def default_device() -> int:
     return int(os.environ.get("PA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def ingest_threads() -> int:
+    """Host threads for ingest: PA_INGEST_THREADS if set, else this job's CPU
+    share (OMP_NUM_THREADS on the GPU box) capped by the affinity mask, at most 16."""
+    env = os.environ.get("PA_INGEST_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(n, 16))
+
+
+class IdBlob(Sequence):
+    """Read ids held as one ASCII blob (each id followed by a line break), a
+    read-only str sequence that materialises ids only when they are asked for:
+    aligning a container never needs them (only PseudoAlignment.reads does)."""
+
+    __slots__ = ("_blob", "_n", "_ends", "_list")
+
+    def __init__(self, blob: bytes, n: int):
+        self._blob, self._n, self._ends, self._list = blob, int(n), None, None
+
+    def __len__(self) -> int:
+        return self._n
+
+    def _offsets(self):
+        if self._ends is None:
+            self._ends = np.flatnonzero(np.frombuffer(self._blob, dtype=np.uint8) == 10)
+        return self._ends
+
+    def __getitem__(self, i):
+        if self._list is not None:
+            return self._list[i]
+        if isinstance(i, slice):
+            return self.tolist()[i]
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError(i)
+        e = self._offsets()
+        s = int(e[i - 1]) + 1 if i else 0
+        return self._blob[s:int(e[i])].decode("ascii")
+
+    def __iter__(self):
+        return iter(self.tolist())
+
+    def tolist(self):
+        if self._list is None:
+            self._list = self._blob.decode("ascii").split("\n")[:self._n]
+        return self._list
+
+
+class SeqColumns:
+    """Parsed FASTA/FASTQ columns: ``names`` (IdBlob, a str sequence), ``seq`` /
+    ``qual`` (uint8; ``qual`` is None for FASTA) and ``off`` (uint64 CSR, n + 1)."""
+
+    __slots__ = ("names", "seq", "qual", "off")
+
+    def __init__(self, names, seq, qual, off):
+        self.names, self.seq, self.qual, self.off = names, seq, qual, off
+
+
+def _seqset_columns(h, kind: int) -> SeqColumns:
+    n, nb, nn = U64(), U64(), U64()
+    try:
+        _check(lib().pa_seqset_sizes(h, ctypes.byref(n), ctypes.byref(nb), ctypes.byref(nn)))
+        seq = np.empty(nb.value, dtype=np.uint8)
+        qual = np.empty(nb.value, dtype=np.uint8) if kind == PA_FASTQ else None
+        off = np.empty(n.value + 1, dtype=np.uint64)
+        names = ctypes.create_string_buffer(max(1, nn.value))
+        _check(lib().pa_seqset_export(h, _ptr(seq), _ptr(qual), _ptr(off), ctypes.cast(names, P)))
+    finally:
+        lib().pa_seqset_free(h)
+    return SeqColumns(IdBlob(names.raw[:nn.value], n.value), seq, qual, off)
+
+
+def parse_file(kind: int, path: str, threads: Optional[int] = None) -> Optional[SeqColumns]:
+    """Native multi-threaded parse of a FASTA/FASTQ file (pa_parse_file); None if
+    the file is outside the canonical subset or unreadable -- the caller then
+    uses the exact grammar of records.py, which also raises the reference's errors."""
+    h = P()
+    st = lib().pa_parse_file(int(kind), os.fsencode(path), int(threads or ingest_threads()), ctypes.byref(h))
+    if st in (PA_ENOTCANON, PA_EIO):
+        return None
+    _check(st)
+    return _seqset_columns(h, kind)
+
+
+def parse_text(kind: int, text, threads: Optional[int] = None, universal_newlines: bool = False
+               ) -> Optional[SeqColumns]:
+    """Like parse_file, on text (str or bytes) in memory (pa_parse_text); by
+    default the text is taken as is, like the regexes of records.py see a str."""
+    data = text.encode("utf-8") if isinstance(text, str) else bytes(text)
+    h = P()
+    buf = ctypes.create_string_buffer(data, len(data)) if data else None
+    st = lib().pa_parse_text(int(kind), ctypes.cast(buf, P) if buf is not None else None, len(data),
+                             int(threads or ingest_threads()), int(bool(universal_newlines)), ctypes.byref(h))
+    if st == PA_ENOTCANON:
+        return None
+    _check(st)
+    return _seqset_columns(h, kind)
 
 
 def concat(chunks: Sequence) -> Tuple[np.ndarray, np.ndarray]:

@@ -20,6 +20,11 @@ bytes concatenated with uint64 offsets) so that a batch can be handed to the
 GPU without materialising one Python object per read; Records are built on
 iteration.  Parity with the reference on its own edge cases is pinned by
 tests/golden/parser_cases.json.
+
+Both containers first hand the text to the native multi-threaded parser of
+libpa.so (csrc/pa_ingest.cpp), which accepts exactly the canonical subset of
+this grammar and yields the same records; any other text (and every text the
+reference rejects) is parsed by the regular expressions below.
 """
 
 from __future__ import annotations
@@ -131,12 +136,35 @@ class RecordContainer:
         return len(self._records)
 
 
+def _native_columns(kind: int, data):
+    """Columns from the native multi-threaded parser (pa_parse_text), or None
+    when the text is outside its canonical subset (then the regex grammar below
+    decides, exactly as the reference)."""
+    import pa_native
+    return pa_native.parse_text(kind, data)
+
+
 class FASTARecordContainer(RecordContainer):
     """Genomes: sections ``description`` and ``genome`` (src/records.py:212-233)."""
 
     SECTION_NAMES = ("description", "genome")
 
+    def load_columns(self, cols) -> None:
+        """Records from native parser columns (pa_native.SeqColumns)."""
+        seq, off = cols.seq, cols.off
+        for i, name in enumerate(cols.names):
+            genome = seq[int(off[i]):int(off[i + 1])].tobytes().decode("ascii")
+            self._records.append(Record([Section("description", name), Section("genome", genome)]))
+
     def parse_records(self, data: str) -> None:
+        if not self._records:
+            cols = _native_columns(0, data)
+            if cols is not None:
+                self.load_columns(cols)
+                return
+        self._parse_regex(data)
+
+    def _parse_regex(self, data: str) -> None:
         spans = []
         for m in _FASTA_RE.finditer(data):
             spans.append(m.span())
@@ -159,13 +187,44 @@ class FASTAQRecordContainer(RecordContainer):
 
     def __init__(self) -> None:
         super().__init__()
-        self.ids: List[str] = []
+        self._ids: List[str] = []
+        self._id_view = None  # native parse: pa_native.IdBlob, materialised on first use of .ids
         self.seq = np.zeros(0, dtype=np.uint8)
         self.qual = np.zeros(0, dtype=np.uint8)
         self.offsets = np.zeros(1, dtype=np.uint64)
         self._spaces: Dict[int, str] = {}
 
+    @property
+    def ids(self) -> List[str]:
+        if self._id_view is not None:
+            self._ids = self._id_view.tolist()
+            self._id_view = None
+        return self._ids
+
+    @ids.setter
+    def ids(self, value: List[str]) -> None:
+        self._ids, self._id_view = value, None
+
+    def id_sequence(self):
+        """The ids as a sequence, without materialising a native blob."""
+        return self._id_view if self._id_view is not None else self._ids
+
+    def load_columns(self, cols) -> None:
+        """Reads from native parser columns (pa_native.SeqColumns) into an empty
+        container (the parser has checked that the ids are unique)."""
+        assert len(self) == 0
+        self._ids, self._id_view = [], cols.names
+        self.seq, self.qual, self.offsets = cols.seq, cols.qual, cols.off
+
     def parse_records(self, data: str) -> None:
+        if len(self) == 0:
+            cols = _native_columns(1, data)
+            if cols is not None:
+                self.load_columns(cols)
+                return
+        self._parse_regex(data)
+
+    def _parse_regex(self, data: str) -> None:
         ids: List[str] = list(self.ids)
         seen = set(ids)
         seqs: List[str] = []
@@ -227,13 +286,13 @@ class FASTAQRecordContainer(RecordContainer):
         self.ids.extend(ids)
 
     def __len__(self) -> int:
-        return len(self.ids)
+        return len(self._id_view) if self._id_view is not None else len(self._ids)
 
     def record(self, i: int) -> Record:
         a, b = int(self.offsets[i]), int(self.offsets[i + 1])
-        return Record([Section("identifier", self.ids[i]), Section("sequence", self.seq[a:b].tobytes().decode()),
+        return Record([Section("identifier", self.id_sequence()[i]), Section("sequence", self.seq[a:b].tobytes().decode()),
                        Section("space", self._spaces.get(i, "")),
                        Section("quality_sequence", self.qual[a:b].tobytes().decode())])
 
     def __iter__(self) -> Iterator[Record]:
-        return (self.record(i) for i in range(len(self.ids)))
+        return (self.record(i) for i in range(len(self)))

@@ -17,6 +17,10 @@
  *                            genomes_mapped_to (PseudoAlignment.reads)      src/kmer.py:542, 551-561
  *   pa_result_fetch          PseudoAlignment.get_summary inputs             src/kmer.py:622-657
  *   pa_align_batch           one-shot host-buffer form of pa_align
+ *   pa_parse_file/_text      FASTAFile / FASTAQFile -> FASTARecordContainer /
+ *                            FASTAQRecordContainer.parse_records (host
+ *                            threads, canonical subset of the grammar)     src/data_file.py:117-158,
+ *                                                                          src/records.py:141-302
  *
  * Conventions
  *   - Every function returns PA_OK (0) or an error code; pa_last_error()
@@ -53,6 +57,8 @@ typedef int32_t pa_status;
 #define PA_EDEVICE 4       /* HIP runtime error */
 #define PA_EUNSUPPORTED 5  /* e.g. k > PA_MAX_K */
 #define PA_EINTERNAL 6     /* invariant violated (reported, never silent) */
+#define PA_ENOTCANON 7     /* ingest: text outside the canonical FASTA/FASTQ subset (use the exact grammar) */
+#define PA_EIO 8           /* ingest: file could not be opened / read */
 
 #define PA_MAX_K 159       /* k-mers up to 159 bases: keys of up to 5 x 64-bit words */
 
@@ -188,6 +194,32 @@ pa_status pa_align_batch(const pa_index *idx, const uint8_t *seq, const uint8_t 
  * (deferred) path since the last read. */
 pa_status pa_profile_enable(pa_index *idx, int32_t enable);
 pa_status pa_profile_read(pa_index *idx, double *main_ms, uint64_t *launches, uint64_t *deferred_reads);
+
+/* ---- ingest (host only, no device) ---------------------------------------------- */
+
+/* Multi-threaded parse of FASTA (kind PA_FASTA) or FASTQ (PA_FASTQ) text into
+ * column buffers, for the canonical subset of the reference grammar
+ * (src/records.py:141-302; csrc/pa_ingest.cpp states the subset).  Returns
+ * PA_ENOTCANON for any text outside it -- including every text the reference
+ * rejects (no records, unparsed data, duplicate ids, length mismatch) -- so
+ * that the caller parses it with the exact grammar, which reproduces the
+ * reference's acceptance and errors.  pa_parse_file reads plain files by mmap
+ * and ".gz" files through zlib; PA_EIO if the file cannot be read.
+ * A pa_seqset holds n records: FASTA genomes with whitespace removed and
+ * stripped descriptions; FASTQ sequences, qualities and stripped ids. */
+#define PA_FASTA 0
+#define PA_FASTQ 1
+typedef struct pa_seqset pa_seqset;
+/* universal_newlines: 1 = the text was read from a file in text mode by the
+ * reference (CRLF / lone final CR are line breaks), 0 = raw text (parse_records(str)) */
+pa_status pa_parse_text(int32_t kind, const char *text, uint64_t len, int32_t threads, int32_t universal_newlines,
+                        pa_seqset **out);
+pa_status pa_parse_file(int32_t kind, const char *path, int32_t threads, pa_seqset **out);
+/* n_bases: total sequence bytes; name_bytes: names joined by '\n' (one after each name) */
+pa_status pa_seqset_sizes(const pa_seqset *set, uint64_t *n_records, uint64_t *n_bases, uint64_t *name_bytes);
+/* seq[n_bases], qual[n_bases] (FASTQ; may be NULL), off[n_records + 1] (CSR), names[name_bytes] (may be NULL) */
+pa_status pa_seqset_export(const pa_seqset *set, uint8_t *seq, uint8_t *qual, uint64_t *off, char *names);
+void pa_seqset_free(pa_seqset *set);
 
 #ifdef __cplusplus
 }

@@ -136,3 +136,167 @@ def test_synth_shapes():
     s, q, o = synth.sample_reads(g, 50, 80, seed=2)
     assert s.shape == (50, 80) and set(np.unique(s).tolist()) <= set(b"ACGT")
     assert q.min() >= 35 and q.max() <= 74
+
+
+# ---- native ingest (csrc/pa_ingest.cpp) == the regex grammar on its subset -------
+
+def _records_of(c, kind):
+    import records as R
+    cls = R.FASTARecordContainer if kind == 0 else R.FASTAQRecordContainer
+    return [(r.identifier, [r[n] for n in cls.SECTION_NAMES]) for r in c]
+
+
+def _regex(kind, text):
+    import records as R
+    c = R.FASTARecordContainer() if kind == 0 else R.FASTAQRecordContainer()
+    try:
+        c._parse_regex(text)
+    except Exception as e:  # noqa: BLE001
+        return type(e).__name__
+    return _records_of(c, kind)
+
+
+def _native(kind, text, threads):
+    import records as R
+    cols = N.parse_text(kind, text, threads=threads)
+    if cols is None:
+        return None
+    c = R.FASTARecordContainer() if kind == 0 else R.FASTAQRecordContainer()
+    c.load_columns(cols)
+    return _records_of(c, kind)
+
+
+def _random_fasta(rng):
+    parts = []
+    for g in range(int(rng.integers(1, 5))):
+        hdr = "".join(rng.choice(list("ab c\tXY_:|>1"), size=int(rng.integers(1, 8))))
+        body = "".join(rng.choice(list("ACGTN"), size=int(rng.integers(1, 200))))
+        w = int(rng.integers(5, 70))
+        body = "\n".join(body[i:i + w] for i in range(0, len(body), w))
+        parts.append(f">{hdr}\n{body}\n")
+    return "".join(parts)
+
+
+def _random_fastq(rng):
+    parts = []
+    for r in range(int(rng.integers(1, 6))):
+        n = int(rng.integers(1, 40))
+        rid = "".join(rng.choice(list("ab c\t1_:"), size=int(rng.integers(1, 6))))
+        seq = "".join(rng.choice(list("ACGT"), size=n))
+        q = "".join(chr(int(x)) for x in rng.integers(33, 127, size=n))
+        parts.append(f"@{rid}\n{seq}\n+\n{q}\n")
+    return "".join(parts)
+
+
+POOL = list("ACGTNacgtn>@+.!~ \t\n\r\x0b\x0c\x1c") + ["\r\n", "\n\n", "é", "\x00"]
+
+
+def _mutate(rng, text):
+    t = list(text)
+    for _ in range(int(rng.integers(0, 3))):
+        op = int(rng.integers(0, 4))
+        i = int(rng.integers(0, len(t) + 1))
+        if op == 0:
+            t.insert(i, str(rng.choice(POOL)))
+        elif op == 1 and t:
+            del t[min(i, len(t) - 1)]
+        elif op == 2 and t:
+            t[min(i, len(t) - 1)] = str(rng.choice(POOL))
+        else:
+            t = list("".join(t).replace("\n", "\r\n"))
+    return "".join(t)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_native_parser_matches_regex_grammar(kind):
+    """Differential check: wherever the native parser accepts a text, the regex
+    grammar accepts it with the same records; it rejects (None) everything else
+    the grammar rejects.  Random canonical texts plus random mutations."""
+    rng = np.random.Generator(np.random.PCG64(123 + kind))
+    accepted = rejected = 0
+    for it in range(3000):
+        base = _random_fasta(rng) if kind == 0 else _random_fastq(rng)
+        if it % 7 == 3:
+            base = base.rstrip("\n")
+        if it % 11 == 5 and kind == 1:
+            base = base + base  # duplicate ids
+        text = base if it % 3 == 0 else _mutate(rng, base)
+        nat = _native(kind, text, threads=1 + it % 4)
+        ref = _regex(kind, text)
+        if nat is None:
+            rejected += 1
+            continue
+        accepted += 1
+        assert nat == ref, repr(text)
+    assert accepted > 800 and rejected > 300
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_native_parser_golden_cases(kind):
+    name = "fasta" if kind == 0 else "fastq"
+    for text, exp in PARSER[name]:
+        nat = _native(kind, text, threads=2)
+        if nat is not None:
+            assert "records" in exp, repr(text)
+            assert nat == [(r["identifier"], list(r["sections"].values())) for r in exp["records"]], repr(text)
+
+
+def test_native_parse_file_large_multithread(tmp_path):
+    """A multi-chunk FASTQ and FASTA through pa_parse_file (plain and .gz)."""
+    import synth
+    from data_file import FASTAQFile, FASTAFile
+    gens = synth.family_genomes(3, 300000, seed=7, family_size=3, n_rate=1e-3, n_run=4)
+    seq, qual, _ = synth.sample_reads(gens, 40000, 100, seed=8)
+    fq = synth.fastq_text([f"r{i}" for i in range(len(seq))], seq, qual)
+    fa = synth.fasta_text(["g0 a", "g1", "g2\t"], gens, width=61)
+    (tmp_path / "r.fq").write_text(fq)
+    (tmp_path / "g.fa").write_text(fa)
+    with gzip.open(tmp_path / "r.fq.gz", "wt") as f:
+        f.write(fq)
+    for path in ("r.fq", "r.fq.gz"):
+        cols = N.parse_file(N.PA_FASTQ, str(tmp_path / path), threads=8)
+        assert cols is not None
+        assert list(cols.names) == [f"r{i}" for i in range(len(seq))]
+        assert cols.names[7] == "r7" and cols.names[-1] == f"r{len(seq) - 1}"
+        assert np.array_equal(cols.seq, seq.reshape(-1)) and np.array_equal(cols.qual, qual.reshape(-1))
+        assert cols.off.tolist() == list(range(0, 100 * len(seq) + 1, 100))
+    c = FASTAQFile(str(tmp_path / "r.fq")).container
+    assert c.ids[:3] == ["r0", "r1", "r2"] and np.array_equal(c.seq, seq.reshape(-1))
+    cols = N.parse_file(N.PA_FASTA, str(tmp_path / "g.fa"), threads=8)
+    assert list(cols.names) == ["g0 a", "g1", "g2"]
+    for i, g in enumerate(gens):
+        assert np.array_equal(cols.seq[int(cols.off[i]):int(cols.off[i + 1])], g)
+    recs = list(FASTAFile(str(tmp_path / "g.fa")).container)
+    assert [r.identifier for r in recs] == ["g0 a", "g1", "g2"] and recs[1]["genome"] == bytes(gens[1]).decode()
+    # duplicate ids -> not canonical; the regex grammar raises the reference's error
+    (tmp_path / "d.fq").write_text("@a\nAC\n+\nII\n@a\nAC\n+\nII\n")
+    assert N.parse_file(N.PA_FASTQ, str(tmp_path / "d.fq")) is None
+    import records as R
+    with pytest.raises(R.DuplicateRecordError):
+        FASTAQFile(str(tmp_path / "d.fq"))
+    assert N.parse_file(N.PA_FASTQ, str(tmp_path / "missing.fq")) is None
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_native_parse_file_matches_universal_newlines(kind, tmp_path):
+    """Files: the reference reads them as UTF-8 text with universal newlines
+    (src/data_file.py:117-158); pa_parse_file must agree wherever it accepts."""
+    import records as R
+    rng = np.random.Generator(np.random.PCG64(555 + kind))
+    path = tmp_path / "x"
+    accepted = 0
+    for it in range(1500):
+        base = _random_fasta(rng) if kind == 0 else _random_fastq(rng)
+        if it % 5 == 1:
+            base = base.replace("\n", "\r\n")
+        text = _mutate(rng, base) if it % 2 else base
+        path.write_bytes(text.encode("utf-8"))
+        cols = N.parse_file(kind, str(path), threads=1 + it % 4)
+        if cols is None:
+            continue
+        accepted += 1
+        c = R.FASTARecordContainer() if kind == 0 else R.FASTAQRecordContainer()
+        c.load_columns(cols)
+        with open(path, "r", encoding="utf-8") as f:
+            assert _records_of(c, kind) == _regex(kind, f.read()), repr(text)
+    assert accepted > 500
