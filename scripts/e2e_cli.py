@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""End-to-end dumpalign figure (host parse, index build
+and the CLI measured separately from the device-resident bench).
+
+    python scripts/e2e_cli.py [--reads N] [--dir DIR]
+
+Writes the C2 genomes (FASTA, 80-column lines) and N x 150 bp reads (FASTQ)
+to DIR, then
+  1. times each phase of the drop-in API in one process: FASTAFile (native
+     ingest), KmerReference (device index build), FASTAQFile (native ingest),
+     PseudoAlignment.align_reads_from_container (upload + align), get_summary;
+  2. runs `main.py -t dumpalign` as a subprocess and times the whole command,
+     checking that its stdout equals the in-process summary.
+Prints one JSON line.
+"""
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "bioinformatics-project-for-shotgun-metagenomics-pseudo-alignment-shotgun-_amd")
+sys.path.insert(0, PKG)
+
+import synth  # noqa: E402
+
+
+def write_fastq(path, genomes, n, chunk=1_000_000):
+    """Fixed-width records '@r%09d' / 150 bases / '+' / 150 qualities."""
+    L = 150
+    rec = 12 + L + 1 + 2 + L + 1
+    with open(path, "wb") as f:
+        for b in range(0, n, chunk):
+            m = min(chunk, n - b)
+            seq, qual, _ = synth.sample_reads(genomes, m, L, seed=2 + b // chunk, err_rate=0.005)
+            buf = np.empty((m, rec), dtype=np.uint8)
+            ids = np.char.zfill(np.arange(b, b + m).astype(str), 9).astype("S9")
+            buf[:, 0] = ord("@")
+            buf[:, 1] = ord("r")
+            buf[:, 2:11] = np.frombuffer(ids.tobytes(), dtype=np.uint8).reshape(m, 9)
+            buf[:, 11] = 10
+            buf[:, 12:12 + L] = seq
+            buf[:, 12 + L] = 10
+            buf[:, 13 + L] = ord("+")
+            buf[:, 14 + L] = 10
+            buf[:, 15 + L:15 + 2 * L] = qual
+            buf[:, 15 + 2 * L] = 10
+            buf.tofile(f)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--dir", default="/tmp/pa_e2e")
+    args = ap.parse_args()
+    os.makedirs(args.dir, exist_ok=True)
+    fa, fq = os.path.join(args.dir, "c2.fa"), os.path.join(args.dir, "c2.fq")
+    t0 = time.perf_counter()
+    genomes = synth.family_genomes(50, 2_000_000, seed=1, family_size=5, sub_rate=0.01, conserved_len=5000,
+                                   n_rate=1e-4, n_run=10)
+    with open(fa, "w") as f:
+        f.write(synth.fasta_text([f"genome_{i} synthetic C2" for i in range(50)], genomes, width=80))
+    write_fastq(fq, genomes, args.reads)
+    gen_s = time.perf_counter() - t0
+    print(f"files written in {gen_s:.1f}s: {os.path.getsize(fq) / 1e9:.2f} GB FASTQ", file=sys.stderr, flush=True)
+
+    from data_file import FASTAFile, FASTAQFile
+    from kmer import KmerReference, PseudoAlignment
+    ph = {}
+    t = time.perf_counter()
+    gc = FASTAFile(fa).container
+    ph["parse_fasta_s"] = time.perf_counter() - t
+    t = time.perf_counter()
+    ref = KmerReference(31, gc)
+    ref.index  # noqa: B018  (device build happens here)
+    import pa_native as N
+    N.lib()
+    ph["index_build_s"] = time.perf_counter() - t
+    t = time.perf_counter()
+    rc = FASTAQFile(fq).container
+    ph["parse_fastq_s"] = time.perf_counter() - t
+    t = time.perf_counter()
+    pa = PseudoAlignment(ref)
+    pa.align_reads_from_container(rc)
+    ph["upload_align_s"] = time.perf_counter() - t
+    t = time.perf_counter()
+    summary = json.dumps(pa.get_summary(), indent=4)
+    ph["summary_s"] = time.perf_counter() - t
+    del rc, pa
+
+    t = time.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(PKG, "main.py"), "-t", "dumpalign", "-g", fa, "-k", "31",
+                        "--reads", fq], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    cli_s = time.perf_counter() - t
+    out = {"workload": f"dumpalign C2: 50 x 2 Mbp FASTA, {args.reads} x 150 bp FASTQ, k=31",
+           "fastq_bytes": os.path.getsize(fq), "cli_wall_s": cli_s, "cli_reads_per_s": args.reads / cli_s,
+           "cli_rc": r.returncode, "cli_stdout_equals_api": r.stdout == summary + "\n",
+           "phases": ph, "ingest_threads": N.ingest_threads(),
+           "fastq_parse_GBps": os.path.getsize(fq) / ph["parse_fastq_s"] / 1e9}
+    if r.returncode:
+        out["cli_stderr"] = r.stderr[-2000:]
+    print(json.dumps(out), flush=True)
+    for p in (fa, fq):
+        os.remove(p)
+
+
+if __name__ == "__main__":
+    main()
