@@ -65,7 +65,9 @@ struct AlignArgs {
     const uint64_t *tile_pk;
     uint64_t tile_n;
     const uint64_t *goff;           // genome start positions [G + 1] (concatenated coordinates)
-    const uint16_t *tile16;         // lane kernel tile (null: no lane kernel)
+    const uint16_t *tile16;         // lane kernel tile (null: no lane kernel); set sizes for --max-genomes
+    const uint64_t *tile_fl;        // lane kernel flag planes (pairs per 64 positions)
+    const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
     const uint32_t *tile_nb;        // one-substitution neighbour bits (null: none)
     int walk_rounds;
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
@@ -121,6 +123,22 @@ __device__ __forceinline__ void count_genome(const AlignArgs &a, const WgCounter
 
 #include "pa_fast.h"
 #include "pa_lane.h"
+
+// Plane of the windows whose genome set is larger than mg (--max-genomes,
+// src/kmer.py:425-427), bit i of word j <-> position 64 j + i, from tile16's
+// set sizes: the lane walk then tests a walked window with one bit instead of
+// a 2-byte tile entry.  Made once per (index, mg) and cached in the index.
+__global__ __launch_bounds__(256) void k_tile_big(const uint16_t *__restrict__ t16, uint64_t n, int32_t mg,
+                                                  uint64_t *__restrict__ big, uint64_t n_words) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n_words; j += nw) {
+        const uint64_t t = 64 * j + lane;
+        const uint32_t v = t < n ? t16[t] : 0u;
+        const uint64_t b = __ballot((v & PA_T16_VALID) && (int32_t)(v & PA_T16_SIZE) > mg);
+        if (lane == 0) big[j] = b;
+    }
+}
 
 
 // ---------------------------------------------------------------------------
@@ -569,6 +587,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_pk = idx->tile_pk;
     a.goff = idx->goff;
     a.tile16 = idx->tile_cls ? idx->tile16 : nullptr;
+    a.tile_fl = idx->tile_cls ? idx->tile_fl : nullptr;
     a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
@@ -668,7 +687,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     const bool fast_ok = idx->k > 0 && idx->nw <= 2 && idx->n_kmers > 0;
     // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
     const char *no_lane = std::getenv("PA_NO_LANE");
-    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile16 && !(no_lane && no_lane[0] == '1');
+    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile16 && a.tile_fl && !(no_lane && no_lane[0] == '1');
     if (fast_ok) {
         const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
         const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4
@@ -679,6 +698,17 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
             PA_HIP(hipEventRecord(e0, st));
         }
         if (lane_ok) {
+            if ((a.prm.flags & F_MG) && a.prm.mg >= 2) {
+                const uint64_t n_words = a.tile_n / 64 + 4;
+                if (!idx->tile_big) PA_HIP(hipMalloc(&idx->tile_big, n_words * 8));
+                if (idx->tile_big_mg != a.prm.mg) {
+                    hipLaunchKernelGGL(k_tile_big, dim3((unsigned)std::min<uint64_t>((n_words + 3) / 4, 1u << 20)),
+                                       dim3(256), 0, st, idx->tile16, a.tile_n, (int32_t)a.prm.mg, idx->tile_big, n_words);
+                    PA_HIP(hipGetLastError());
+                    idx->tile_big_mg = a.prm.mg;
+                }
+                a.tile_big = idx->tile_big;
+            }
             a.queue_hard = idx->queue_hard;
             a.queue_hard_count = (unsigned long long *)idx->counters + 3;
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));

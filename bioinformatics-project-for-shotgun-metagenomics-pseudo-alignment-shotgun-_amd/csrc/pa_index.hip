@@ -487,6 +487,29 @@ __global__ void k_tile16(const uint32_t *__restrict__ tile_cls, uint64_t n, uint
     }
 }
 
+// Flag planes of the lane walk (pa_lane.h): per 64 positions a word pair
+// (A, B), bit i <-> position 64 j + i: (0,0) no indexed window, (1,0) a
+// multi-genome k-mer, (1,1) a specific one, (0,1) a k-mer that repeats within
+// 127 positions (PA_TILE_REP).  0.25 B per base: the 120 windows of a read
+// are one or two 64-B lines, where the 2-byte tile16 is four or five.
+// One wave per word pair, the planes by ballot.
+__global__ __launch_bounds__(256) void k_tile_planes(const uint32_t *__restrict__ tile_cls, uint64_t n, uint32_t G,
+                                                     uint64_t *__restrict__ fl, uint64_t n_pairs) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n_pairs; j += nw) {
+        const uint64_t t = 64 * j + lane;
+        const uint32_t v = t < n ? tile_cls[t] : NONE;
+        const bool ok = v != NONE, rep = ok && (v & PA_TILE_REP);
+        const bool spec = ok && !rep && (v & ~PA_TILE_REP) < G;
+        const uint64_t a = __ballot(ok && !rep), b = __ballot(rep || spec);
+        if (lane == 0) {
+            fl[2 * j] = a;
+            fl[2 * j + 1] = b;
+        }
+    }
+}
+
 // ---- EXTSIM statistics ------------------------------------------------------
 
 template <int NW>
@@ -742,6 +765,11 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_tile16, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
                                idx->tile_cls, n, G, idx->class_genomes, idx->tile16);
             idx->device_bytes += n * 2;
+            const uint64_t n_pairs = n / 64 + 4;  // padded: the walk reads three pairs from any position
+            B_HIP(hipMalloc(&idx->tile_fl, n_pairs * 16));
+            hipLaunchKernelGGL(k_tile_planes, dim3((unsigned)std::min<uint64_t>((n_pairs + 3) / 4, 1u << 20)), dim3(256),
+                               0, st, idx->tile_cls, n, G, idx->tile_fl, n_pairs);
+            idx->device_bytes += n_pairs * 16;
             // one-substitution neighbours (12 B per base) when they fit a quarter of the free memory;
             // PA_NO_NB=1 skips them (A/B measurements)
             size_t free_b = 0, total_b = 0;
@@ -799,6 +827,11 @@ void index_release(pa_index *idx) {
     hipFree(idx->tile_cls);
     hipFree(idx->tile_pk);
     hipFree(idx->tile16);
+    hipFree(idx->tile_fl);
+    idx->tile_fl = nullptr;
+    hipFree(idx->tile_big);
+    idx->tile_big = nullptr;
+    idx->tile_big_mg = -1;
     hipFree(idx->tile_nb);
     idx->tile_nb = nullptr;
     idx->tile_cls = nullptr;

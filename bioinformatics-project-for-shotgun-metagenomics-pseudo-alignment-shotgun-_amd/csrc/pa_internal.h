@@ -83,6 +83,9 @@ struct pa_index {
     uint32_t *tile_cls = nullptr;      // [tile_n]
     uint64_t *tile_pk = nullptr;       // [tile_n / 32 + 32] MSB-first 2-bit words (padded)
     uint16_t *tile16 = nullptr;        // [tile_n] lane-kernel tile: valid | rep | specific | set size (G < 8191)
+    uint64_t *tile_fl = nullptr;       // [2 (tile_n / 64 + 4)] lane-kernel flag planes (k_tile_planes)
+    uint64_t *tile_big = nullptr;      // [tile_n / 64 + 4] plane "set size > tile_big_mg" (pa_align, cached)
+    int64_t tile_big_mg = -1;          // the --max-genomes value tile_big was made for (-1: none)
     uint32_t *tile_nb = nullptr;       // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional
     uint64_t device_bytes = 0;
     // align scratch

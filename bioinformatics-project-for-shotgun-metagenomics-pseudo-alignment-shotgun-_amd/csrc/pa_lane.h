@@ -351,11 +351,15 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     uint64_t gw[kLaneWords + 1];
 #pragma unroll
     for (int i = 0; i <= kLaneWords; i++) gw[i] = gp[i];
-    const uint32_t odd = (uint32_t)(Ac & 1);
-    const uint32_t *t32 = (const uint32_t *)(a.tile16 + (Ac - odd));  // (tile16 is padded by a dword)
-    uint32_t td[17];
+    // flag planes of windows 0..127 (bit w <-> genome position A + w): three
+    // word pairs from the pair holding A (tile_fl is padded)
+    const uint64_t *fp = a.tile_fl + 2 * (Ac >> 6);
+    uint64_t pa3[3], pb3[3];
 #pragma unroll
-    for (int j = 0; j < 17; j++) td[j] = t32[j];
+    for (int i = 0; i < 3; i++) {
+        pa3[i] = fp[2 * i];
+        pb3[i] = fp[2 * i + 1];
+    }
     const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.G, S.atp);
     S.g = g;
     const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
@@ -418,66 +422,53 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         NP0 = ~0ull;  // every mismatching window is probed
         NP1 = ~0ull;
     }
-    // ---- walked windows: classes from the tile, 32 windows per step
-    const bool has_mg = a.prm.flags & F_MG;
-    uint32_t nspec = 0, nincl = 0, hr = 0;
-    uint64_t P0 = 0, P1 = 0;
-#pragma unroll 1
-    for (uint32_t w0 = 0; w0 < W; w0 += 32) {
-        if (w0) {
-#pragma unroll
-            for (int j = 0; j < 17; j++) td[j] = t32[(w0 >> 1) + j];
-        }
-        // align the step's entries to an even start (no runtime register indexing below)
-        if (odd) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) td[j] = (td[j] >> 16) | (td[j + 1] << 16);
-        }
-        const uint32_t sft = w0 & 63;
-        const uint32_t um = (uint32_t)((w0 < 64 ? U0 : U1) >> sft);   // windows with a mismatch
-        const uint32_t vm = (uint32_t)((w0 < 64 ? V0 : V1) >> sft);   //   with two or more
-        const uint32_t nm = (uint32_t)((w0 < 64 ? NP0 : NP1) >> sft); //   neighbour present
-        const uint32_t nwin = W - w0 < 32 ? W - w0 : 32u;
-        const uint32_t inw = nwin >= 32 ? ~0u : ((1u << nwin) - 1);
-        // the flags of the step's 32 entries as bit masks (window i = bit i)
-        uint32_t valid = 0, rep = 0, spec = 0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t x = td[j];
-            valid |= (((x >> 15) & 1u) | ((x >> 30) & 2u)) << (2 * j);
-            rep |= (((x >> 14) & 1u) | ((x >> 29) & 2u)) << (2 * j);
-            spec |= (((x >> 13) & 1u) | ((x >> 28) & 2u)) << (2 * j);
-        }
-        // windows failing the k-mer quality filter are never looked up (src/kmer.py:420-423)
-        const uint32_t live = WIN_Q ? inw & ~(uint32_t)((w0 < 64 ? S.F0 : S.F1) >> sft) : inw;
-        valid &= live;
-        // probe: not an indexed genome window, or a mismatch that the neighbour
-        // bits do not settle (two or more in the window, or the neighbour present)
-        const uint32_t pend = (live & ~valid) | (valid & um & (vm | nm));
-        const uint32_t walked = valid & ~um;
-        if (walked & rep) {  // a k-mer that may repeat inside the read
-            S.kind = LANE_HARD;
-            return (void)LANE_HARD_WHY(6);
-        }
-        uint32_t big = 0;  // highly redundant walked windows (src/kmer.py:425-427)
-        if (has_mg) {
-#pragma unroll
-            for (int i = 0; i < 32; i++) {
-                const uint32_t v = (i & 1) ? (td[i >> 1] >> 16) : (td[i >> 1] & 0xFFFFu);
-                big |= ((int64_t)(v & PA_T16_SIZE) > (int64_t)a.prm.mg ? 1u : 0u) << i;
-            }
-            big &= walked;
-        }
-        const uint32_t incl = walked & ~big;
-        hr += __popc(big);
-        nincl += __popc(incl);
-        // a specific k-mer at a position inside genome g is specific to g
-        nspec += __popc(incl & spec);
-        if (w0 < 64)
-            P0 |= (uint64_t)pend << w0;
-        else
-            P1 |= (uint64_t)pend << (w0 - 64);
+    // ---- walked windows: 128-bit masks from the planes.  valid: an indexed
+    // genome window, spec: its k-mer is specific (to g, the genome it lies in),
+    // rep: it may repeat inside the read
+    const uint32_t fr = (uint32_t)(Ac & 63);
+    const uint64_t PA0 = fr ? (pa3[0] >> fr) | (pa3[1] << (64 - fr)) : pa3[0];
+    const uint64_t PA1 = fr ? (pa3[1] >> fr) | (pa3[2] << (64 - fr)) : pa3[1];
+    const uint64_t PB0 = fr ? (pb3[0] >> fr) | (pb3[1] << (64 - fr)) : pb3[0];
+    const uint64_t PB1 = fr ? (pb3[1] >> fr) | (pb3[2] << (64 - fr)) : pb3[1];
+    const uint64_t in0 = W >= 64 ? ~0ull : ((1ull << W) - 1);
+    const uint64_t in1 = W <= 64 ? 0ull : (W >= 128 ? ~0ull : ((1ull << (W - 64)) - 1));
+    // windows failing the k-mer quality filter are never looked up (src/kmer.py:420-423)
+    const uint64_t live0 = WIN_Q ? in0 & ~S.F0 : in0, live1 = WIN_Q ? in1 & ~S.F1 : in1;
+    const uint64_t valid0 = (PA0 | PB0) & live0, valid1 = (PA1 | PB1) & live1;
+    // probe: not an indexed genome window, or a mismatch that the neighbour
+    // bits do not settle (two or more in the window, or the neighbour present)
+    const uint64_t P0 = (live0 & ~valid0) | (valid0 & U0 & (V0 | NP0));
+    const uint64_t P1 = (live1 & ~valid1) | (valid1 & U1 & (V1 | NP1));
+    const uint64_t walked0 = valid0 & ~U0, walked1 = valid1 & ~U1;
+    if ((walked0 & PB0 & ~PA0) | (walked1 & PB1 & ~PA1)) {  // a k-mer that may repeat inside the read
+        S.kind = LANE_HARD;
+        return (void)LANE_HARD_WHY(6);
     }
+    const uint64_t spec0 = PA0 & PB0, spec1 = PA1 & PB1;
+    // highly redundant walked windows (src/kmer.py:425-427): set size > mg.  A
+    // specific k-mer has size 1, a multi-genome one at least 2, so only mg >= 2
+    // needs the sizes of the multi-genome windows (one bit plane per mg)
+    uint64_t big0 = 0, big1 = 0;
+    if (a.prm.flags & F_MG) {
+        const int32_t mg = a.prm.mg;
+        if (mg < 1) {
+            big0 = walked0;
+            big1 = walked1;
+        } else if (mg == 1) {
+            big0 = walked0 & ~spec0;
+            big1 = walked1 & ~spec1;
+        } else {  // the plane "set size > mg" of this mg (k_tile_big)
+            const uint64_t *bp = a.tile_big + (Ac >> 6);
+            const uint64_t b0 = bp[0], b1 = bp[1], b2 = bp[2];
+            big0 = walked0 & ~spec0 & (fr ? (b0 >> fr) | (b1 << (64 - fr)) : b0);
+            big1 = walked1 & ~spec1 & (fr ? (b1 >> fr) | (b2 << (64 - fr)) : b1);
+        }
+    }
+    const uint64_t incl0 = walked0 & ~big0, incl1 = walked1 & ~big1;
+    const uint32_t hr = (uint32_t)(__popcll(big0) + __popcll(big1));
+    const uint32_t nincl = (uint32_t)(__popcll(incl0) + __popcll(incl1));
+    // a specific k-mer at a position inside genome g is specific to g
+    const uint32_t nspec = (uint32_t)(__popcll(incl0 & spec0) + __popcll(incl1 & spec1));
     S.nspec = nspec;
     S.nincl = nincl;
     S.hr = hr;
@@ -562,13 +553,16 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
 
 // Waves per SIMD the register allocation must allow.  The kernel is bound by
 // the latency of random table / tile reads, so occupancy pays: 4 (128 VGPRs, a
-// few spilled dwords) measured +6 % on C2 over 3; the k-mer quality variant
-// spills too much at 4 and keeps 3.
+// few spilled dwords) measured +6 % on C2 over 3, and the k-mer quality
+// variant (168 VGPRs at 3) +2-4 % on C3 at 4 despite its spills.
 #ifndef PA_LANE_WAVES
 #define PA_LANE_WAVES 4
 #endif
+#ifndef PA_LANE_WAVES_Q
+#define PA_LANE_WAVES_Q 4
+#endif
 template <bool NEED_Q, bool WIN_Q>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIN_Q ? 3 : PA_LANE_WAVES)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIN_Q ? PA_LANE_WAVES_Q : PA_LANE_WAVES)))
 void k_align_lane(AlignArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const uint32_t G = a.G;
