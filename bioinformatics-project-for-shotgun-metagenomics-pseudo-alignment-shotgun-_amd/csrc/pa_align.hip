@@ -68,7 +68,7 @@ struct AlignArgs {
     const uint16_t *tile16;         // lane kernel tile (null: no lane kernel); set sizes for --max-genomes
     const uint64_t *tile_fl;        // lane kernel flag planes (pairs per 64 positions)
     const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
-    const uint32_t *tile_nb;        // one-substitution neighbour bits (null: none)
+    const uint64_t *tile_nb;        // one-substitution neighbour bits, any | specific << 32 (null: none)
     int walk_rounds;
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
     int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
@@ -737,7 +737,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
             (unsigned long long)r->n, d[3], d[0], d[4], d[5], d[6], d[7]);
     fprintf(stderr, "[pa_stats] lane hard reasons: long %llu mkq %llu bad %llu no-anchor %llu range %llu mismatches %llu rep %llu found %llu pending %llu\n",
             d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], d[16]);
-    fprintf(stderr, "[pa_stats] lane: cooperative probes %llu re-anchors %llu neighbour words %llu\n", d[18], d[19], d[20]);
+    fprintf(stderr, "[pa_stats] lane: cooperative probes %llu re-anchors %llu neighbour words %llu | pending: invalid %llu "
+            "2+ mismatches %llu neighbour present %llu\n", d[18], d[19], d[20], d[21], d[22], d[23]);
 #endif
     return PA_OK;
 }

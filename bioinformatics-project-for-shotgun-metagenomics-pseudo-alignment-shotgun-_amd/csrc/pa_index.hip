@@ -438,14 +438,18 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 }
 
 // One-substitution neighbours of every indexed genome window, for the lane
-// kernel: bit i of nb[3 p + b] says whether the k-mer starting at p - k + 1 + i
-// with its base at p replaced by the b-th other base ((genome base + 1 + b) & 3)
-// is in the index.  A read window that matches the genome except at one base
-// p is then resolved by one bit -- all k windows around a sequencing error by
-// one word -- instead of k table probes.  Defined on the 2-bit genome string
-// (N packed as A), for windows that are indexed themselves (tile_cls != NONE).
+// kernel: bit i of the low half of nb[3 p + b] says whether the k-mer starting
+// at p - k + 1 + i with its base at p replaced by the b-th other base
+// ((genome base + 1 + b) & 3) is in the index, bit i of the high half whether
+// it is there as a specific k-mer.  A read window that matches the genome
+// except at one base p is then resolved by one bit -- all k windows around a
+// sequencing error by one word -- instead of k table probes; and a read walked
+// on a sibling of its genome (a family variant, not an error, at p) learns
+// that the variant k-mer is shared, which is all an ambiguous read needs.
+// Defined on the 2-bit genome string (N packed as A), for windows that are
+// indexed themselves (tile_cls != NONE).
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
-                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t *nb) {
+                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, unsigned long long *nb) {
     const int sh = 64 - 2 * k;
     uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -462,7 +466,7 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
                 uint64_t slot;
                 uint32_t cls, tpos;
                 if (table_find<1>(table, hc.cap, key, home_of<1>(key, key_hash(key), hc), slot, cls, tpos))
-                    atomicOr(&nb[3 * (t + j) + b], 1u << (k - 1 - j));
+                    atomicOr(&nb[3 * (t + j) + b], (cls < G ? 0x100000001ull : 1ull) << (k - 1 - j));
             }
         }
     }
@@ -774,12 +778,13 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             // PA_NO_NB=1 skips them (A/B measurements)
             size_t free_b = 0, total_b = 0;
             const char *no_nb = std::getenv("PA_NO_NB");
-            if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess && n * 12 <= free_b / 4) {
-                B_HIP(hipMalloc(&idx->tile_nb, n * 12 + 64));
-                B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 12 + 64, st));
+            if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess && n * 24 <= free_b / 4) {
+                B_HIP(hipMalloc(&idx->tile_nb, n * 24 + 64));
+                B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 24 + 64, st));
                 hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
-                                   idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, idx->tile_nb);
-                idx->device_bytes += n * 12;
+                                   idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                   (unsigned long long *)idx->tile_nb);
+                idx->device_bytes += n * 24;
             }
         }
         B_HIP(hipGetLastError());

@@ -86,7 +86,7 @@ struct pa_index {
     uint64_t *tile_fl = nullptr;       // [2 (tile_n / 64 + 4)] lane-kernel flag planes (k_tile_planes)
     uint64_t *tile_big = nullptr;      // [tile_n / 64 + 4] plane "set size > tile_big_mg" (pa_align, cached)
     int64_t tile_big_mg = -1;          // the --max-genomes value tile_big was made for (-1: none)
-    uint32_t *tile_nb = nullptr;       // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional
+    uint64_t *tile_nb = nullptr;       // [3 tile_n] one-substitution neighbour bits, any | specific << 32 (k_nb_build), optional
     uint64_t device_bytes = 0;
     // align scratch
     pa::Workspace ws;

@@ -153,6 +153,7 @@ struct LaneRead {
     uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
     uint64_t F0, F1;                   // windows failing --min-kmer-quality (never looked up)
     uint32_t qf;                       // their number (src/kmer.py:420-423)
+    uint32_t uoff;                     // a walk window's k-mer is off the walk, present and multi-genome (neighbour bits)
 };
 
 // 64 bits of an LDS row of MSB-first packed words starting at bit o.
@@ -223,6 +224,29 @@ __device__ __forceinline__ void lane_window_quality(const AlignArgs &a, const ui
     S.qf = (uint32_t)(__popcll(F0) + __popcll(F1));
 }
 
+// Mismatching bases between the read (LDS row, len bases) and the genome
+// string from concatenated position A on; ~0u when the read does not fit.
+__device__ __forceinline__ uint32_t lane_mismatches(const AlignArgs &a, const uint64_t *row, uint32_t len, int64_t A) {
+    if (A < 0 || (uint64_t)A + len > a.tile_n) return ~0u;
+    const uint64_t gb = 2 * (uint64_t)A;
+    const uint64_t *gp = a.tile_pk + (gb >> 6);
+    const uint32_t gr = (uint32_t)(gb & 63);
+    uint64_t gw[kLaneWords + 1];
+#pragma unroll
+    for (int i = 0; i <= kLaneWords; i++) gw[i] = gp[i];
+    uint32_t n = 0;
+#pragma unroll
+    for (int i = 0; i < kLaneWords; i++) {
+        if (32 * i >= (int)len) break;
+        const uint64_t gwi = gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i];
+        uint64_t d = row[i] ^ gwi;
+        const uint32_t rest = len - 32 * i;
+        if (rest < 32) d &= ~0ull << (64 - 2 * rest);
+        n += __popcll((d | (d >> 1)) & 0x5555555555555555ull);
+    }
+    return n;
+}
+
 // Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor.
 template <bool NEED_Q, bool WIN_Q>
 __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64_t *row, LaneRead &S) {
@@ -230,6 +254,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
     S.hr = S.nspec = S.nincl = 0;
     S.F0 = S.F1 = 0;
     S.qf = 0;
+    S.uoff = 0;
     const int k = a.k;
     const uint32_t flags = a.prm.flags;
     const uint64_t o = a.off[r];
@@ -330,6 +355,47 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
             S.acls = scls[i];
             S.aw = sw[i];
         }
+    // no specific seed: the first occurrence of a multi-genome seed k-mer may
+    // lie in a sibling of the read's genome (a family member), whose variants
+    // would leave many windows unwalked.  Other found seeds may point to other
+    // stretches: walk the one with the fewest mismatching bases (up to three)
+    if (S.acls >= a.G) {
+        // distinct candidate stretches (selects only: no runtime register indexing)
+        const int64_t e0 = (int64_t)S.atp - S.aw;
+        int64_t e1 = INT64_MIN, e2 = INT64_MIN;
+        uint32_t t1 = 0, w1 = 0, c1 = 0, t2 = 0, w2 = 0, c2 = 0;
+#pragma unroll
+        for (int i = 0; i < NSEED; i++) {
+            const int64_t Ai = (int64_t)stp[i] - sw[i];
+            if (!bit(sfound, i) || stp[i] == NONE || Ai == e0 || Ai == e1 || e2 != INT64_MIN) continue;
+            if (e1 == INT64_MIN) {
+                e1 = Ai;
+                t1 = stp[i], w1 = sw[i], c1 = scls[i];
+            } else {
+                e2 = Ai;
+                t2 = stp[i], w2 = sw[i], c2 = scls[i];
+            }
+        }
+        if (e1 != INT64_MIN) {
+            uint32_t best = ~0u, bj = 0;
+#pragma unroll 1
+            for (uint32_t j = 0; j < 3; j++) {
+                const int64_t Aj = j == 0 ? e0 : (j == 1 ? e1 : e2);
+                if (Aj == INT64_MIN) break;
+                const uint32_t m = lane_mismatches(a, row, len, Aj);
+                if (m < best) {
+                    best = m;
+                    bj = j;
+                }
+                if (best == 0) break;
+            }
+            if (bj == 1) {
+                S.atp = t1, S.aw = w1, S.acls = c1;
+            } else if (bj == 2) {
+                S.atp = t2, S.aw = w2, S.acls = c2;
+            }
+        }
+    }
     S.kind = LANE_WALK;
 }
 
@@ -371,7 +437,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     // ---- mismatching bases against the genome from A on.  U: windows with a
     // mismatch, V: windows with two or more; with the neighbour bits (tile_nb)
     // a window with exactly one mismatch is resolved by its bit (NP: the bits set)
-    uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0;
+    uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0, NS0 = 0, NS1 = 0;
     uint32_t nmis = 0;
     const bool has_nb = a.tile_nb != nullptr;
 #pragma unroll
@@ -403,7 +469,8 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             if (has_nb) {
                 // neighbour word of the genome base at A + e and the read's base there
                 const uint32_t cg = (uint32_t)(gwi >> (62 - 2 * j)) & 3u, cr = (uint32_t)(row[i] >> (62 - 2 * j)) & 3u;
-                const uint64_t nbw = a.tile_nb[3 * ((uint64_t)A + e) + ((cr - cg - 1) & 3u)];
+                const uint64_t nbq = a.tile_nb[3 * ((uint64_t)A + e) + ((cr - cg - 1) & 3u)];
+                const uint64_t nbw = nbq & 0xFFFFFFFFull, nbs = nbq >> 32;  // present, present and specific
 #ifdef PA_STATS
                 atomicAdd(&a.dbg[16], 1ull);
 #endif
@@ -412,16 +479,25 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
                 if (sft >= 0) {
                     NP0 |= sft < 64 ? nbw << sft : 0ull;
                     NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 32 ? nbw >> (64 - sft) : 0ull);
+                    NS0 |= sft < 64 ? nbs << sft : 0ull;
+                    NS1 |= sft >= 64 ? nbs << (sft - 64) : (sft > 32 ? nbs >> (64 - sft) : 0ull);
                 } else {
                     NP0 |= nbw >> (-sft);
+                    NS0 |= nbs >> (-sft);
                 }
             }
         }
     }
     if (!has_nb) {
-        NP0 = ~0ull;  // every mismatching window is probed
-        NP1 = ~0ull;
+        NP0 = NS0 = ~0ull;  // every mismatching window is probed
+        NP1 = NS1 = ~0ull;
     }
+    // a window with one mismatch whose k-mer is present but multi-genome needs
+    // no probe unless --max-genomes asks for its set size: it only makes the
+    // read ambiguous (if no specific k-mer is included) or sends it to the wave
+    // kernel (if one is)
+    const bool has_mg = a.prm.flags & F_MG;
+    const uint64_t NQ0 = has_mg ? NP0 : NS0, NQ1 = has_mg ? NP1 : NS1;
     // ---- walked windows: 128-bit masks from the planes.  valid: an indexed
     // genome window, spec: its k-mer is specific (to g, the genome it lies in),
     // rep: it may repeat inside the read
@@ -437,9 +513,15 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     const uint64_t valid0 = (PA0 | PB0) & live0, valid1 = (PA1 | PB1) & live1;
     // probe: not an indexed genome window, or a mismatch that the neighbour
     // bits do not settle (two or more in the window, or the neighbour present)
-    const uint64_t P0 = (live0 & ~valid0) | (valid0 & U0 & (V0 | NP0));
-    const uint64_t P1 = (live1 & ~valid1) | (valid1 & U1 & (V1 | NP1));
+    const uint64_t P0 = (live0 & ~valid0) | (valid0 & U0 & (V0 | NQ0));
+    const uint64_t P1 = (live1 & ~valid1) | (valid1 & U1 & (V1 | NQ1));
+    S.uoff = ((valid0 & U0 & ~V0 & NP0 & ~NQ0) | (valid1 & U1 & ~V1 & NP1 & ~NQ1)) != 0;
     const uint64_t walked0 = valid0 & ~U0, walked1 = valid1 & ~U1;
+#ifdef PA_STATS
+    atomicAdd(&a.dbg[17], (unsigned long long)(__popcll(live0 & ~valid0) + __popcll(live1 & ~valid1)));
+    atomicAdd(&a.dbg[18], (unsigned long long)(__popcll(valid0 & U0 & V0) + __popcll(valid1 & U1 & V1)));
+    atomicAdd(&a.dbg[19], (unsigned long long)(__popcll(valid0 & U0 & NQ0 & ~V0) + __popcll(valid1 & U1 & NQ1 & ~V1)));
+#endif
     if ((walked0 & PB0 & ~PA0) | (walked1 & PB1 & ~PA1)) {  // a k-mer that may repeat inside the read
         S.kind = LANE_HARD;
         return (void)LANE_HARD_WHY(6);
@@ -449,7 +531,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     // specific k-mer has size 1, a multi-genome one at least 2, so only mg >= 2
     // needs the sizes of the multi-genome windows (one bit plane per mg)
     uint64_t big0 = 0, big1 = 0;
-    if (a.prm.flags & F_MG) {
+    if (has_mg) {
         const int32_t mg = a.prm.mg;
         if (mg < 1) {
             big0 = walked0;
@@ -481,22 +563,26 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     }
 }
 
-// Phase 3 (whole wave): probe the unwalked windows of every walking lane.
-__device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW, const LaneRead &S) {
+// Phase 3 (whole wave): probe windows (Q0, Q1) of the walking lanes; `reset`
+// clears the lanes' outcomes first (LW.flags / hr / cand accumulate otherwise).
+__device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW, const LaneRead &S, uint64_t Q0,
+                                                uint64_t Q1, bool reset) {
     const int lane = lane_id();
     const int sh = 64 - 2 * a.k;
     const bool walking = S.kind == LANE_WALK;
-    LW.flags[lane] = 0;
-    LW.hr[lane] = 0;
-    LW.cand[lane] = ~0ull;
-    const uint32_t c = walking ? (uint32_t)(__popcll(S.P0) + __popcll(S.P1)) : 0u;
+    if (reset) {
+        LW.flags[lane] = 0;
+        LW.hr[lane] = 0;
+        LW.cand[lane] = ~0ull;
+    }
+    if (!walking) Q0 = Q1 = 0;
+    const uint32_t c = (uint32_t)(__popcll(Q0) + __popcll(Q1));
     const uint32_t incl = wave_incl_scan(c);
     const uint32_t pre = incl - c;
     const uint32_t total = __shfl(incl, 63);
 #ifdef PA_STATS
     if (lane == 0 && total) atomicAdd(&a.dbg[14], (unsigned long long)total);
 #endif
-    uint64_t Q0 = walking ? S.P0 : 0, Q1 = walking ? S.P1 : 0;
     for (uint32_t base = 0; base < total; base += kPassEntries) {
         // this pass's entries of the lane: global indices [max(pre, base), min(pre + c, base + 256))
         const uint32_t lo = max(pre, base), hi = min(pre + c, base + (uint32_t)kPassEntries);
@@ -598,7 +684,13 @@ void k_align_lane(AlignArgs a) {
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif
             if (!__ballot(S.kind == LANE_WALK)) break;
-            lane_probe_wave(a, LW, S);
+            // a multi-genome k-mer off the walk next to walked specific ones: the
+            // wave kernel, without probing
+            if (S.kind == LANE_WALK && S.uoff && S.nspec > 0) {
+                S.kind = LANE_HARD;
+                LANE_HARD_WHY(7);
+            }
+            lane_probe_wave(a, LW, S, S.P0, S.P1, true);
             if (S.kind == LANE_WALK) {
                 const uint32_t fl = LW.flags[lane];
                 if (fl & 1u) {  // a specific k-mer off the walk: walk again from it (once)
@@ -616,7 +708,7 @@ void k_align_lane(AlignArgs a) {
                     }
                 } else {
                     S.hr += LW.hr[lane];
-                    if (fl & 2u) {  // unspecific k-mers off the walk: fine only without specific ones
+                    if ((fl & 2u) || S.uoff) {  // unspecific k-mers off the walk: fine only without specific ones
                         if (S.nspec > 0) {
                             S.kind = LANE_HARD;
                             LANE_HARD_WHY(7);
