@@ -677,7 +677,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     a.dbg = (unsigned long long *)idx->counters + 4;
     PA_HIP(hipMemsetAsync(idx->counters, 0, 8, st));
 #ifdef PA_STATS
-    PA_HIP(hipMemsetAsync(a.dbg, 0, 160, st));
+    PA_HIP(hipMemsetAsync(a.dbg, 0, 224, st));
 #endif
     ExactArgs x{};
     unsigned egrid = 0;
@@ -730,8 +730,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     launch_exact_nw(idx->nw, x, egrid, st);
     PA_HIP(hipGetLastError());
 #ifdef PA_STATS
-    unsigned long long d[24];
-    PA_HIP(hipMemcpyAsync(d, idx->counters, 192, hipMemcpyDeviceToHost, st));
+    unsigned long long d[32];
+    PA_HIP(hipMemcpyAsync(d, idx->counters, 256, hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
     fprintf(stderr, "[pa_stats] reads %llu lane-hard %llu exact %llu | wave kernel: windows %llu probed %llu walk %llu anchors %llu\n",
             (unsigned long long)r->n, d[3], d[0], d[4], d[5], d[6], d[7]);
@@ -739,6 +739,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
             d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], d[16]);
     fprintf(stderr, "[pa_stats] lane: cooperative probes %llu re-anchors %llu neighbour words %llu | pending: invalid %llu "
             "2+ mismatches %llu neighbour present %llu\n", d[18], d[19], d[20], d[21], d[22], d[23]);
+    fprintf(stderr, "[pa_stats] lane found: shared-neighbour+specific %llu second-walk specific %llu probed-shared+specific %llu\n",
+            d[24], d[25], d[26]);
 #endif
     return PA_OK;
 }

@@ -893,8 +893,8 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
     PA_HIP(hipMalloc(&idx->codes, std::max<uint64_t>(total, 1)));
     PA_HIP(hipMalloc(&idx->goff, (n + 1) * 8));
-    PA_HIP(hipMalloc(&idx->counters, 24 * 8));
-    PA_HIP(hipMemsetAsync(idx->counters, 0, 24 * 8, st));
+    PA_HIP(hipMalloc(&idx->counters, 32 * 8));
+    PA_HIP(hipMemsetAsync(idx->counters, 0, 32 * 8, st));
     PA_HIP(hipMemcpyAsync(idx->goff, idx->h_goff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
     idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
     if (total > 0) {

@@ -94,7 +94,7 @@ struct pa_index {
     uint32_t *queue_hard = nullptr;    // read indices the lane kernel leaves to the wave kernel
     uint64_t queue_cap = 0;
     uint64_t *counters = nullptr;      // [0] queue length, [1] deferred total, [2] error flags, [3] hard reads,
-                                       // [4..23] PA_STATS counters
+                                       // [4..31] PA_STATS counters
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> ev_start, ev_stop;

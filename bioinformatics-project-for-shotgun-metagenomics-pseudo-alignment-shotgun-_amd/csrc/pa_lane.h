@@ -434,9 +434,18 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         S.kind = LANE_HARD;
         return (void)LANE_HARD_WHY(4);
     }
+    const uint32_t fr = (uint32_t)(Ac & 63);
+    const uint64_t PA0 = fr ? (pa3[0] >> fr) | (pa3[1] << (64 - fr)) : pa3[0];
+    const uint64_t PA1 = fr ? (pa3[1] >> fr) | (pa3[2] << (64 - fr)) : pa3[1];
+    const uint64_t PB0 = fr ? (pb3[0] >> fr) | (pb3[1] << (64 - fr)) : pb3[0];
+    const uint64_t PB1 = fr ? (pb3[1] >> fr) | (pb3[2] << (64 - fr)) : pb3[1];
+    const uint64_t IX0 = PA0 | PB0, IX1 = PA1 | PB1;  // indexed genome windows
     // ---- mismatching bases against the genome from A on.  U: windows with a
     // mismatch, V: windows with two or more; with the neighbour bits (tile_nb)
-    // a window with exactly one mismatch is resolved by its bit (NP: the bits set)
+    // a window with exactly one mismatch is resolved by its bit (NP: the bits set).
+    // A mismatch inside no indexed window (an N run of the genome, where the
+    // read has some base) changes nothing that is decided here -- unindexed
+    // windows are probed anyway -- and does not count toward the cap
     uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0, NS0 = 0, NS1 = 0;
     uint32_t nmis = 0;
     const bool has_nb = a.tile_nb != nullptr;
@@ -451,10 +460,6 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         while (m) {
             const uint32_t j = __builtin_clzll(m) >> 1, e = 32 * i + j;
             m &= ~(1ull << (62 - 2 * j));
-            if (++nmis > 8) {  // a wrong stretch, not a few sequencing errors
-                S.kind = LANE_HARD;
-                return (void)LANE_HARD_WHY(5);
-            }
             const int32_t lo = (int32_t)e - k + 1 < 0 ? 0 : (int32_t)e - k + 1;
             const int32_t hi = (int32_t)e < (int32_t)W - 1 ? (int32_t)e : (int32_t)W - 1;
             if (lo > hi) continue;
@@ -462,6 +467,11 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             const uint64_t r1 =
                 hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) & (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
                          : 0ull;
+            if (!((r0 & IX0) | (r1 & IX1))) continue;
+            if (++nmis > 8) {  // a wrong stretch, not a few sequencing errors
+                S.kind = LANE_HARD;
+                return (void)LANE_HARD_WHY(5);
+            }
             V0 |= U0 & r0;
             V1 |= U1 & r1;
             U0 |= r0;
@@ -501,16 +511,11 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     // ---- walked windows: 128-bit masks from the planes.  valid: an indexed
     // genome window, spec: its k-mer is specific (to g, the genome it lies in),
     // rep: it may repeat inside the read
-    const uint32_t fr = (uint32_t)(Ac & 63);
-    const uint64_t PA0 = fr ? (pa3[0] >> fr) | (pa3[1] << (64 - fr)) : pa3[0];
-    const uint64_t PA1 = fr ? (pa3[1] >> fr) | (pa3[2] << (64 - fr)) : pa3[1];
-    const uint64_t PB0 = fr ? (pb3[0] >> fr) | (pb3[1] << (64 - fr)) : pb3[0];
-    const uint64_t PB1 = fr ? (pb3[1] >> fr) | (pb3[2] << (64 - fr)) : pb3[1];
     const uint64_t in0 = W >= 64 ? ~0ull : ((1ull << W) - 1);
     const uint64_t in1 = W <= 64 ? 0ull : (W >= 128 ? ~0ull : ((1ull << (W - 64)) - 1));
     // windows failing the k-mer quality filter are never looked up (src/kmer.py:420-423)
     const uint64_t live0 = WIN_Q ? in0 & ~S.F0 : in0, live1 = WIN_Q ? in1 & ~S.F1 : in1;
-    const uint64_t valid0 = (PA0 | PB0) & live0, valid1 = (PA1 | PB1) & live1;
+    const uint64_t valid0 = IX0 & live0, valid1 = IX1 & live1;
     // probe: not an indexed genome window, or a mismatch that the neighbour
     // bits do not settle (two or more in the window, or the neighbour present)
     const uint64_t P0 = (live0 & ~valid0) | (valid0 & U0 & (V0 | NQ0));
@@ -689,6 +694,7 @@ void k_align_lane(AlignArgs a) {
             if (S.kind == LANE_WALK && S.uoff && S.nspec > 0) {
                 S.kind = LANE_HARD;
                 LANE_HARD_WHY(7);
+                LANE_HARD_WHY(16);
             }
             lane_probe_wave(a, LW, S, S.P0, S.P1, true);
             if (S.kind == LANE_WALK) {
@@ -705,6 +711,7 @@ void k_align_lane(AlignArgs a) {
                     } else {
                         S.kind = LANE_HARD;
                         LANE_HARD_WHY(7);
+                        LANE_HARD_WHY(17);
                     }
                 } else {
                     S.hr += LW.hr[lane];
@@ -712,6 +719,7 @@ void k_align_lane(AlignArgs a) {
                         if (S.nspec > 0) {
                             S.kind = LANE_HARD;
                             LANE_HARD_WHY(7);
+                            LANE_HARD_WHY(18);
                         } else {
                             S.kind = LANE_AMB;
                         }
