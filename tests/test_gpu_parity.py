@@ -397,3 +397,31 @@ def test_walk_adversarial_vs_oracle(n_genomes, k):
         assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
         ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
         assert fk.tolist() == ofk.tolist(), ps
+
+
+@pytest.mark.gpu
+def test_full_size_shards_equal_one_pass():
+    """C2-sized reference (50 x 2 Mbp): reads aligned as two shards with their
+    global read bases (the multi-GPU split of pa_dist) accumulate to exactly the
+    one-pass counters, first keys included; and a repeated pass is identical."""
+    gens = synth.family_genomes(50, 2_000_000, seed=1, family_size=5, sub_rate=0.01, conserved_len=5000,
+                                n_rate=1e-4, n_run=10)
+    index = N.Index(gens, 31)
+    n = 2_000_000
+    prm = N.Params.make(1, 1, None, None, 10)
+    one = N.Result(index)
+    reads = N.Reads.synthesize(index, n, 150, first_read=0, seed=2, sub_rate=0.005)
+    N.align(index, reads, prm, 0, one)
+    a = one.fetch()
+    two = N.Result(index)
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        part = N.Reads.synthesize(index, hi - lo, 150, first_read=lo, seed=2, sub_rate=0.005)
+        N.align(index, part, prm, lo, two)
+    b = two.fetch()
+    for x, y in zip(a, b):
+        assert x.tolist() == y.tolist()
+    again = N.Result(index)
+    N.align(index, reads, prm, 0, again)
+    for x, y in zip(a, again.fetch()):
+        assert x.tolist() == y.tolist()
+    assert int(a[0][0]) + int(a[0][1]) + int(a[0][2]) == n
