@@ -739,8 +739,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
             d[8], d[9], d[10], d[11], d[12], d[13], d[14], d[15], d[16]);
     fprintf(stderr, "[pa_stats] lane: cooperative probes %llu re-anchors %llu neighbour words %llu | pending: invalid %llu "
             "2+ mismatches %llu neighbour present %llu\n", d[18], d[19], d[20], d[21], d[22], d[23]);
-    fprintf(stderr, "[pa_stats] lane found: shared-neighbour+specific %llu second-walk specific %llu probed-shared+specific %llu\n",
-            d[24], d[25], d[26]);
+    fprintf(stderr, "[pa_stats] lane found: shared-neighbour+specific %llu second-walk specific %llu probed-shared+specific %llu"
+            " | unique by bound %llu\n", d[24], d[25], d[26], d[27]);
 #endif
     return PA_OK;
 }

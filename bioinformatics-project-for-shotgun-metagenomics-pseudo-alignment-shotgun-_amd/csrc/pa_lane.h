@@ -153,7 +153,7 @@ struct LaneRead {
     uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
     uint64_t F0, F1;                   // windows failing --min-kmer-quality (never looked up)
     uint32_t qf;                       // their number (src/kmer.py:420-423)
-    uint32_t uoff;                     // a walk window's k-mer is off the walk, present and multi-genome (neighbour bits)
+    uint32_t uoff;                     // walk windows whose k-mer is off the walk, present and multi-genome (neighbour bits)
 };
 
 // 64 bits of an LDS row of MSB-first packed words starting at bit o.
@@ -520,7 +520,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     // bits do not settle (two or more in the window, or the neighbour present)
     const uint64_t P0 = (live0 & ~valid0) | (valid0 & U0 & (V0 | NQ0));
     const uint64_t P1 = (live1 & ~valid1) | (valid1 & U1 & (V1 | NQ1));
-    S.uoff = ((valid0 & U0 & ~V0 & NP0 & ~NQ0) | (valid1 & U1 & ~V1 & NP1 & ~NQ1)) != 0;
+    S.uoff = (uint32_t)(__popcll(valid0 & U0 & ~V0 & NP0 & ~NQ0) + __popcll(valid1 & U1 & ~V1 & NP1 & ~NQ1));
     const uint64_t walked0 = valid0 & ~U0, walked1 = valid1 & ~U1;
 #ifdef PA_STATS
     atomicAdd(&a.dbg[17], (unsigned long long)(__popcll(live0 & ~valid0) + __popcll(live1 & ~valid1)));
@@ -689,6 +689,24 @@ void k_align_lane(AlignArgs a) {
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif
             if (!__ballot(S.kind == LANE_WALK)) break;
+            // Enough walked specific k-mers decide the read whatever the windows
+            // off the walk hold.  X = windows whose k-mer may be in the index off
+            // the walk (unwalked, not known absent).  Any other genome h has at
+            // most X specific k-mers and at most (nincl - nspec) + X in total,
+            // while g has at least nspec and nincl (src/kmer.py:444-480): with
+            // nspec >= X + max(m, 1) g is the strict top and unique, and with
+            // X - nspec <= p no genome's total exceeds g's by more than p.  Set
+            // sizes (--max-genomes) are not known off the walk: not then.
+            if (S.kind == LANE_WALK && S.nspec > 0 && !(a.prm.flags & F_MG)) {
+                const int64_t X = (int64_t)(__popcll(S.P0) + __popcll(S.P1) + S.uoff);
+                const int64_t ns = (int64_t)S.nspec;
+                if (ns >= X + (a.prm.m > 0 ? a.prm.m : 1) && (a.prm.p < 0 || X - ns <= a.prm.p)) {
+                    S.kind = LANE_UNIQUE;
+#ifdef PA_STATS
+                    atomicAdd(&a.dbg[23], 1ull);
+#endif
+                }
+            }
             // a multi-genome k-mer off the walk next to walked specific ones: the
             // wave kernel, without probing
             if (S.kind == LANE_WALK && S.uoff && S.nspec > 0) {
