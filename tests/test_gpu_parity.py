@@ -191,6 +191,10 @@ SYNTH = [
     (4, 5000, 2, 0.02, 64, 800, 150, 0.005, [dict(), dict(m=0, p=0)]),  # 3-word keys, exact path
     (3, 4000, 1, 0.0, 17, 1500, 40, 0.02, [dict(), dict(mkq=55)]),
     (70, 3000, 10, 0.01, 15, 3000, 80, 0.01, [dict(), dict(m=0, p=0)]),  # many genomes per class
+    # families (1% apart) and 1.5% read errors: off-walk k-mers, sibling walks,
+    # the lane kernel's bound decision under several (m, p)
+    (25, 40000, 5, 0.01, 31, 20000, 150, 0.015, [dict(m=2, p=0), dict(m=10, p=10), dict(m=0, p=-1),
+                                                  dict(m=1, p=0), dict(m=5, p=1)]),
     # C4-shaped: 500 genomes (hash decision path, LDS counters), k=31, 150 bp
     (500, 20000, 5, 0.01, 31, 20000, 150, 0.005, [dict(), dict(m=0, p=0), dict(mrq=58, mkq=59, mg=10)]),
     # more genomes than the per-workgroup LDS counters hold (global counters)
