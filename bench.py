@@ -65,6 +65,10 @@ CONFIGS = {
     # C4 (BASELINE configs[3]): 500 genomes, 500M reads over 8 GPUs = 62.5M reads per GPU (weak scaling)
     "c4": dict(BASE, n_genomes=500, reads_per_gpu=62_500_000,
                name="C4: 500 x 2 Mbp synthetic genomes, 62.5M x 150 bp reads per GPU (500M on 8), k=31"),
+    # C5 (BASELINE configs[4]): EXTSIM over 2000 x 4 Mbp genomes in families, then 100M reads
+    "c5": dict(BASE, n_genomes=2000, genome_len=4_000_000, reads_per_gpu=100_000_000, generator="fast",
+               extsim=0.95, name="C5: EXTSIM (threshold 0.95) over 2000 x 4 Mbp synthetic genomes, "
+                                 "then 100M x 150 bp reads, k=31"),
     "c1": dict(BASE, n_genomes=3, genome_len=5000, family=3, sub=0.02, conserved=300, k=21, reads_per_gpu=1000,
                read_len=100, read_err=0.01, name="C1: 3 x 5 kb genomes, 1k x 100 bp reads, k=21"),
 }
@@ -162,15 +166,35 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
     t0 = time.perf_counter()
-    genomes = synth.family_genomes(cfg["n_genomes"], cfg["genome_len"], seed=1, family_size=cfg["family"],
-                                   sub_rate=cfg["sub"], conserved_len=cfg["conserved"], n_rate=cfg["n_rate"],
-                                   n_run=cfg["n_run"])
+    gen = synth.family_genomes_fast if cfg.get("generator") == "fast" else synth.family_genomes
+    genomes = gen(cfg["n_genomes"], cfg["genome_len"], seed=1, family_size=cfg["family"], sub_rate=cfg["sub"],
+                  conserved_len=cfg["conserved"], n_rate=cfg["n_rate"], n_run=cfg["n_run"])
     gen_s = time.perf_counter() - t0
+    log(f"[rank {rank}] genomes: {len(genomes)} x {cfg['genome_len']} in {gen_s:.1f}s")
     stream = torch.cuda.current_stream(dev)
     t0 = time.perf_counter()
     index = N.Index(genomes, cfg["k"], device=local, stream=stream)
     torch.cuda.synchronize(dev)
     build_s = time.perf_counter() - t0
+    extsim = None
+    if cfg.get("extsim") is not None:
+        # EXTSIM (src/kmer.py:152-263): GPU statistics + the greedy pass; a
+        # genome dropped -> the index of the kept genomes
+        import kmer
+        t0 = time.perf_counter()
+        idents = [f"genome_{i}" for i in range(len(genomes))]
+        keep, sim_info = kmer.extsim_filter(index, idents, [len(g) for g in genomes], cfg["extsim"])
+        stats_s = time.perf_counter() - t0
+        if len(keep) != len(idents):
+            index.close()
+            genomes = [g for i, g in zip(idents, genomes) if i in keep]
+            index = N.Index(genomes, cfg["k"], device=local, stream=stream)
+            torch.cuda.synchronize(dev)
+        scores = [v["similarity_score"] for v in sim_info.values() if v["kept"] == "no"]
+        extsim = {"threshold": cfg["extsim"], "genomes_in": len(idents), "genomes_kept": len(keep),
+                  "stats_and_greedy_s": stats_s, "total_s": time.perf_counter() - t0,
+                  "min_dropped_score": min(scores) if scores else None}
+        log(f"[rank {rank}] EXTSIM: kept {len(keep)} of {len(idents)} in {extsim['total_s']:.1f}s")
     info = index.info()
     npg = cfg["reads_per_gpu"]
     reads = N.Reads.synthesize(index, npg, cfg["read_len"], first_read=rank * npg, seed=2, sub_rate=cfg["read_err"],
@@ -228,12 +252,14 @@ def main():
                      "kernel": "align pass: k_align_lane + k_align_fast", "kernel_ms": kern_s * 1e3, "bytes_per_read": b_read},
         "deferred_read_fraction": deferred / max(npg * args.steps, 1),
         "index": {"build_s": build_s, "n_kmers": int(info.n_kmers), "multi_genome_sets": int(info.n_multi_classes),
-                  "table_bytes": int(info.table_bytes)},
+                  "table_bytes": int(info.table_bytes), "table_slots": int(info.table_slots)},
+        "extsim": extsim,
         "cpu_baseline": None,
     }
-    if args.config == "c4" and not args.no_cpu_baseline:
+    if args.config in ("c4", "c5") and not args.no_cpu_baseline:
         # the oracle's 1 Gbp index needs ~90 GB of host memory and minutes to build
-        out["cpu_baseline_note"] = "skipped for C4 (oracle index of 1 Gbp: ~90 GB, minutes); see the C2 line"
+        out["cpu_baseline_note"] = ("skipped for C4/C5 (the oracle index of a 1 / 8 Gbp reference: ~90 GB / too large "
+                                    "for host memory, minutes); see the C2 line and scripts/verify_full.py")
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize(dev)
         base, parity = cpu_baseline(cfg, genomes, index, reads, pk, args.cpu_seconds)

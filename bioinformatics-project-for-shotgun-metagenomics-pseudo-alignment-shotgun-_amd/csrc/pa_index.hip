@@ -162,6 +162,38 @@ __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstar
     }
 }
 
+// Distinct k-mer estimate (HyperLogLog, 2^16 registers, ~0.4 % error) of one
+// genome's windows, to size the table of references whose windows would not
+// fit at the default load (e.g. 2000 x 4 Mbp: 8 G windows, ~3.8 G distinct).
+constexpr int kHllBits = 16;
+template <int NW>
+__global__ void k_hll(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k, uint64_t mask0,
+                      uint32_t *reg) {
+    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+    if (w0 >= nwin) return;
+    uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
+    const uint8_t *s = codes + gstart + w0;
+    Key<NW> key;
+#pragma unroll
+    for (int j = 0; j < NW; j++) key.w[j] = 0;
+    int run = 0;
+    for (int i = 0; i < k - 1; i++) {
+        uint32_t c = s[i];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+    }
+    for (uint64_t w = w0; w < w1; w++) {
+        uint32_t c = s[w - w0 + k - 1];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+        if (run < k) continue;  // (the index skips these windows too)
+        const uint64_t h = fmix64(key_hash(key) ^ 0x243F6A8885A308D3ull);
+        const uint32_t r = (uint32_t)(h >> (64 - kHllBits));
+        const uint32_t rho = (uint32_t)__builtin_clzll((h << kHllBits) | (1ull << (kHllBits - 1))) + 1;
+        if (reg[r] < rho) atomicMax(&reg[r], rho);  // (a stale plain load only costs an atomic)
+    }
+}
+
 // Singletons -> final slot values; multi slots -> list storage.
 template <int NW>
 __global__ void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg, uint32_t *aux,
@@ -746,6 +778,10 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         idx->device_bytes += n_multi * 12 + std::max<uint64_t>(entries, 1) * 4;
     }
     if (idx->tile_n > 0 && (uint64_t)G + idx->class_entries >= PA_TILE_REP) idx->tile_n = 0;  // ids need bit 31
+    cleanup();  // the build scratch (20 B per slot) is not needed by the tiles
+    deg = last_g = aux = lists = cs_id = err = nullptr;
+    off = cs_key = cs_rep = rep_of = nullptr;
+    cnt = nullptr;
     if (idx->tile_n > 0) {  // step 6: genome tiling
         const uint64_t n = idx->tile_n, nwords = n / 32 + 32;  // padded: the walk reads up to 18 words past a position
         B_HIP(hipMalloc(&idx->tile_cls, n * 4));
@@ -872,34 +908,13 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     const char *no_tile = std::getenv("PA_NO_TILE");
     idx->tile_n = (idx->nw == 1 && k > 0 && total > 0 && total < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
                       ? total : 0;
-    // load factor 1/4 when the table fits a third of the free device memory
-    // (absent keys -- the sequencing-error windows -- then end in their home
-    // slot 3 times out of 4), else 1/2
-    uint64_t cap_mult = 2;
-    {
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-            (4 * windows + 64) * (uint64_t)slot_bytes(idx->nw) <= free_b / 3)
-            cap_mult = 4;
-    }
-    if (const char *e = std::getenv("PA_CAP_MULT")) cap_mult = std::max(2, std::atoi(e));
-    uint64_t cap = std::max<uint64_t>(64, cap_mult * windows + 64);
-    const uint64_t align = std::max<uint64_t>(4, R);  // whole 64-B lines (the fast kernel probes a line per step)
-    cap = (cap + align - 1) / align * align;
-    idx->cap = cap;
-    idx->home = pad::HomeCfg{cap, m > 0 ? cap / R : 0, R, (int)std::max<int64_t>(k, 0), m};
-    const int sb = slot_bytes(idx->nw);
-    PA_HIP(hipMalloc(&idx->table, idx->cap * sb));
-    PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
     PA_HIP(hipMalloc(&idx->codes, std::max<uint64_t>(total, 1)));
     PA_HIP(hipMalloc(&idx->goff, (n + 1) * 8));
     PA_HIP(hipMalloc(&idx->counters, 32 * 8));
     PA_HIP(hipMemsetAsync(idx->counters, 0, 32 * 8, st));
     PA_HIP(hipMemcpyAsync(idx->goff, idx->h_goff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
     if (total > 0) {
-        // stage the ASCII genomes through the table memory's tail? keep it simple: a temp buffer
-        uint8_t *ascii = nullptr;
+        uint8_t *ascii = nullptr;  // ASCII staging buffer, freed before the table is allocated
         PA_HIP(hipMalloc(&ascii, total));
         hipError_t e = hipMemcpyAsync(ascii, genomes + goff[0], total, hipMemcpyHostToDevice, st);
         if (e == hipSuccess) {
@@ -910,6 +925,87 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         hipFree(ascii);
         PA_HIP(e);
     }
+    // Table capacity (whole 64-B lines).  Load 1/4 of the genome windows when
+    // the table fits a third of the free device memory (absent keys -- the
+    // sequencing-error windows -- then end in their home slot 3 times out of
+    // 4), else 1/2 of the windows if table + build scratch fit; a reference
+    // too large for either is sized on its distinct k-mers (HyperLogLog
+    // estimate + 3 %): 4, 2 or 1.43 slots per distinct k-mer, the largest that
+    // fits.  The build needs 20 B of scratch per slot and at most 4 B per
+    // genome window for the genome lists.
+    const int sb = slot_bytes(idx->nw);
+    const uint64_t per_slot = (uint64_t)sb + 20;
+    size_t free_b = 0, total_b = 0;
+    PA_HIP(hipMemGetInfo(&free_b, &total_b));
+    const uint64_t reserve = windows * 4 + (1ull << 30);
+    auto fits = [&](uint64_t c) { return c * per_slot + reserve <= (uint64_t)free_b; };
+    uint64_t cap = 0;
+    if ((4 * windows + 64) * (uint64_t)sb <= free_b / 3 && fits(4 * windows + 64))
+        cap = 4 * windows + 64;
+    else if (fits(2 * windows + 64))
+        cap = 2 * windows + 64;
+    if (const char *e = std::getenv("PA_CAP_MULT")) cap = (uint64_t)std::max(2, std::atoi(e)) * windows + 64;
+    if (const char *e = std::getenv("PA_CAP_HLL")) {  // tests / A-B: size on the distinct estimate, at 1.43 per k-mer
+        if (e[0] == '1') cap = 0, free_b = (size_t)0;
+    }
+    if (cap == 0 && k > 0 && windows > 0) {
+        uint32_t *reg = nullptr;
+        PA_HIP(hipMalloc(&reg, (4ull << kHllBits)));
+        PA_HIP(hipMemsetAsync(reg, 0, (4ull << kHllBits), st));
+        const uint64_t mask0 = (2 * k - 64 * (idx->nw - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (idx->nw - 1))) - 1);
+        for (uint32_t g = 0; g < n; g++) {
+            const uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
+            if ((uint64_t)k > len) continue;
+            const uint64_t nwin = len - k + 1;
+            const dim3 grid(grid_for((nwin + kRun - 1) / kRun));
+            switch (idx->nw) {
+                case 1: hipLaunchKernelGGL(k_hll<1>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                case 2: hipLaunchKernelGGL(k_hll<2>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                case 3: hipLaunchKernelGGL(k_hll<3>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                case 4: hipLaunchKernelGGL(k_hll<4>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                default: hipLaunchKernelGGL(k_hll<5>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+            }
+        }
+        std::vector<uint32_t> h(1u << kHllBits);
+        hipError_t e = hipMemcpyAsync(h.data(), reg, (4ull << kHllBits), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        hipFree(reg);
+        PA_HIP(e);
+        const double mm = (double)(1u << kHllBits);
+        double z = 0;
+        uint32_t zeros = 0;
+        for (uint32_t v : h) {
+            z += std::ldexp(1.0, -(int)v);
+            zeros += v == 0;
+        }
+        double est = (0.7213 / (1.0 + 1.079 / mm)) * mm * mm / z;
+        if (est < 2.5 * mm && zeros) est = mm * std::log(mm / zeros);
+        const uint64_t distinct = (uint64_t)(est * 1.03) + 64;
+        idx->distinct_estimate = distinct;
+        const bool forced = free_b == 0;
+        if (forced) PA_HIP(hipMemGetInfo(&free_b, &total_b));
+        for (double mult : {4.0, 2.0, 1.43}) {
+            const uint64_t c = (uint64_t)(mult * (double)distinct) + 64;
+            if (forced && mult > 1.5) continue;
+            if (fits(c)) {
+                cap = c;
+                break;
+            }
+        }
+        if (cap == 0) {
+            set_error("index build: the k-mer table of ~" + std::to_string(distinct) +
+                      " distinct k-mers does not fit the free device memory");
+            return PA_ENOMEM;
+        }
+    }
+    if (cap == 0) cap = 64;
+    const uint64_t align = std::max<uint64_t>(4, R);  // whole 64-B lines (the fast kernel probes a line per step)
+    cap = (cap + align - 1) / align * align;
+    idx->cap = cap;
+    idx->home = pad::HomeCfg{cap, m > 0 ? cap / R : 0, R, (int)std::max<int64_t>(k, 0), m};
+    PA_HIP(hipMalloc(&idx->table, idx->cap * sb));
+    PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
+    idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
     if (k <= 0 || windows == 0) return PA_OK;
     switch (idx->nw) {
         case 1: return build_nw<1>(idx, st);

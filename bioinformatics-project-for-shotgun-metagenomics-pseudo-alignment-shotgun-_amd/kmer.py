@@ -107,6 +107,51 @@ def _check_align_args(kmer_reference, m, p, mrq, mkq, mg, debug=False) -> Option
     return None
 
 
+def extsim_filter(index: N.Index, identifiers: Sequence[str], genome_lengths: Sequence[int],
+                  similarity_threshold: float) -> Tuple[Set[str], Dict[str, Dict[str, Union[str, int, float]]]]:
+    """EXTSIM greedy similar-genome filter (src/kmer.py:152-230) on a device index.
+
+    Per-identifier statistics and pairwise intersections come from the GPU
+    (``pa_index_extsim_stats``: distinct k-mers, specific k-mers, and shared
+    k-mers of every pair of identifiers, src/kmer.py:152-177); the greedy pass
+    is the reference's: genomes sorted ascending by (unique, total, length,
+    order), each compared with the kept ones in keep order by the overlap
+    coefficient |A & B| / min(|A|, |B|) (0 if min is 0) and dropped on the first
+    score strictly above the threshold.  Returns (kept identifiers,
+    similarity_info).  Duplicate identifiers form one group, later records
+    overwriting the length/order of earlier ones, as in the reference."""
+    gid: Dict[str, int] = {}
+    group_of = [gid.setdefault(i, len(gid)) for i in identifiers]
+    total, uniq, inter = index.extsim_stats(group_of, len(gid))
+    stats: Dict[str, Dict[str, int]] = {}
+    for order, (ident, glen) in enumerate(zip(identifiers, genome_lengths)):
+        a = gid[ident]
+        stats[ident] = {"unique_kmers": int(uniq[a]), "total_kmers": int(total[a]), "genome_length": int(glen),
+                        "order": order}
+    ordered = sorted(stats.items(), key=lambda x: (x[1]["unique_kmers"], x[1]["total_kmers"],
+                                                   x[1]["genome_length"], x[1]["order"]))
+    kept: List[str] = []
+    info: Dict[str, Dict[str, Union[str, int, float]]] = {}
+    for ident, st in ordered:
+        a = gid[ident]
+        similar_to = None
+        for kid in kept:
+            b = gid[kid]
+            min_count = min(int(total[a]), int(total[b]))
+            score = (int(inter[a, b]) / min_count) if min_count > 0 else 0
+            if score > similarity_threshold:  # overlap coefficient, strict (src/kmer.py:206-208)
+                similar_to = (kid, score)
+                break
+        base = {"unique_kmers": st["unique_kmers"], "total_kmers": st["total_kmers"],
+                "genome_length": st["genome_length"]}
+        if similar_to is None:
+            info[ident] = {"kept": "yes", **base, "similar_to": "NA", "similarity_score": "NA"}
+            kept.append(ident)
+        else:
+            info[ident] = {"kept": "no", **base, "similar_to": similar_to[0], "similarity_score": similar_to[1]}
+    return set(kept), info
+
+
 class KmerReference:
     """Device-resident k-mer reference of a FASTA container (src/kmer.py:109-351)."""
 
@@ -141,38 +186,9 @@ class KmerReference:
     # -- EXTSIM (src/kmer.py:152-263) --------------------------------------
 
     def _filter_similar_genomes(self, similarity_threshold: float) -> None:
-        idents = [g.identifier for g in self.genomes]
-        gid: Dict[str, int] = {}
-        group_of = [gid.setdefault(i, len(gid)) for i in idents]
-        total, uniq, inter = self._index.extsim_stats(group_of, len(gid))
-        stats: Dict[str, Dict[str, int]] = {}
-        for order, genome in enumerate(self.genomes):  # later duplicates overwrite, as in the reference
-            a = gid[genome.identifier]
-            stats[genome.identifier] = {"unique_kmers": int(uniq[a]), "total_kmers": int(total[a]),
-                                        "genome_length": len(genome["genome"]), "order": order}
-        ordered = sorted(stats.items(), key=lambda x: (x[1]["unique_kmers"], x[1]["total_kmers"],
-                                                       x[1]["genome_length"], x[1]["order"]))
-        kept: List[str] = []
-        info: Dict[str, Dict[str, Union[str, int, float]]] = {}
-        for ident, st in ordered:
-            a = gid[ident]
-            similar_to = None
-            for kid in kept:
-                b = gid[kid]
-                min_count = min(int(total[a]), int(total[b]))
-                score = (int(inter[a, b]) / min_count) if min_count > 0 else 0
-                if score > similarity_threshold:  # overlap coefficient, strict (src/kmer.py:206-208)
-                    similar_to = (kid, score)
-                    break
-            base = {"unique_kmers": st["unique_kmers"], "total_kmers": st["total_kmers"],
-                    "genome_length": st["genome_length"]}
-            if similar_to is None:
-                info[ident] = {"kept": "yes", **base, "similar_to": "NA", "similarity_score": "NA"}
-                kept.append(ident)
-            else:
-                info[ident] = {"kept": "no", **base, "similar_to": similar_to[0], "similarity_score": similar_to[1]}
-        keep = set(kept)
-        if len(keep) != len(gid):
+        keep, info = extsim_filter(self._index, [g.identifier for g in self.genomes],
+                                   [len(g["genome"]) for g in self.genomes], similarity_threshold)
+        if len(keep) != len({g.identifier for g in self.genomes}):
             self._index.close()
             self.genomes = [g for g in self.genomes if g.identifier in keep]
             self._build()  # pruning dropped genomes == building from the kept ones

@@ -58,6 +58,36 @@ def family_genomes(n_genomes: int, length: int, seed: int = 1, family_size: int 
     return out
 
 
+def family_genomes_fast(n_genomes: int, length: int, seed: int = 1, family_size: int = 5,
+                        sub_rate: float = 0.01, conserved_len: int = 5000,
+                        n_rate: float = 1e-4, n_run: int = 10) -> List[np.ndarray]:
+    """Same family structure as family_genomes, generated with byte-sized draws
+    (substitution and N-run positions drawn by count, not by a per-base test) so
+    that multi-Gbp references (BASELINE config 5: 2000 x 4 Mbp) take seconds per
+    Gbp.  A different random stream from family_genomes: C2-C4 keep theirs."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    conserved_len = int(min(conserved_len, length // 2))
+    conserved = ACGT[rng.integers(0, 4, size=conserved_len, dtype=np.uint8)] if conserved_len > 0 else None
+    out: List[np.ndarray] = []
+    base = None
+    for g in range(n_genomes):
+        if g % max(family_size, 1) == 0:
+            base = rng.integers(0, 4, size=length, dtype=np.uint8)
+        codes = base.copy()
+        if sub_rate > 0:
+            hit = rng.integers(0, length, size=int(rng.binomial(length, sub_rate)))
+            codes[hit] = (codes[hit] + rng.integers(1, 4, size=hit.size, dtype=np.uint8)) & 3
+        seq = ACGT[codes]
+        if conserved is not None:
+            at = int(rng.integers(0, length - conserved_len + 1))
+            seq[at:at + conserved_len] = conserved
+        if n_rate > 0 and n_run > 0:
+            for s in rng.integers(0, length, size=int(rng.binomial(length, n_rate))):
+                seq[s:s + n_run] = ord("N")
+        out.append(seq)
+    return out
+
+
 def sample_reads(genomes: Sequence[np.ndarray], n_reads: int, read_len: int, seed: int = 2,
                  err_rate: float = 0.005, qual_mean: float = 60.0, qual_sd: float = 8.0,
                  qual_min: int = 35, qual_max: int = 74) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

@@ -429,3 +429,28 @@ def test_full_size_shards_equal_one_pass():
     for x, y in zip(a, again.fetch()):
         assert x.tolist() == y.tolist()
     assert int(a[0][0]) + int(a[0][1]) + int(a[0][2]) == n
+
+
+@pytest.mark.gpu
+def test_table_sized_on_distinct_estimate(monkeypatch):
+    """The large-reference capacity path (HyperLogLog estimate, 1.43 slots per
+    distinct k-mer: load ~0.7, long probe chains) gives the same index and the
+    same results as the default table."""
+    gens, s, q, off = _synthetic_case(20, 30000, 5, 0.01, 31, 8000, 150, 0.01, seed=4242)
+    oix = O.OracleIndex(gens, 31)
+    monkeypatch.setenv("PA_CAP_HLL", "1")
+    index = N.Index(gens, 31)
+    monkeypatch.delenv("PA_CAP_HLL")
+    info = index.info()
+    assert index.n_kmers == oix.n_kmers
+    assert info.table_slots < 2 * index.n_kmers  # sized on the estimate (default: 4 x windows)
+    reads = N.Reads.upload(s, q, off)
+    for ps in (dict(), dict(m=0, p=0, mrq=58, mkq=59, mg=3)):
+        full = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+        result = N.Result(index)
+        N.align(index, reads, N.Params.make(full["m"], full["p"], full["mrq"], full["mkq"], full["mg"]), 0, result)
+        stats, uq, am, fk = result.fetch()
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"], mkq=full["mkq"],
+                      mg=full["mg"], detail=False)
+        assert stats.tolist() == o.stats.tolist(), ps
+        assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
