@@ -70,6 +70,7 @@ struct AlignArgs {
     const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
     const uint64_t *tile_nb;        // one-substitution neighbour bits, any | specific << 32 (null: none)
     int walk_rounds;
+    int tpos_local;                 // slot.tpos genome-local (first_pos), else concatenated
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
     int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
     const uint8_t *seq;
@@ -591,6 +592,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
+    a.tpos_local = idx->tpos_local;
     a.lane_maxpend = 96;
     if (const char *e = std::getenv("PA_LANE_MAXPEND")) a.lane_maxpend = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("PA_WALK_ROUNDS")) a.walk_rounds = std::atoi(e);

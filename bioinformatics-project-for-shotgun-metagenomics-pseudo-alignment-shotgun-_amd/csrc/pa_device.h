@@ -45,6 +45,16 @@ __device__ __forceinline__ uint32_t class_size_of(uint32_t cls, uint32_t G, cons
     return cls < G ? 1u : class_genomes[cls - G];
 }
 
+// Concatenated-genome position of a key's first occurrence: slot.tpos is
+// genome-local, in the key's first genome (its specific genome, or the first of
+// its genome set: records are [size, ascending genomes...]).
+__device__ __forceinline__ uint64_t first_pos(uint32_t cls, uint32_t tpos, uint32_t G, const uint32_t *class_genomes,
+                                              const uint64_t *goff, bool local) {
+    if (!local) return tpos;  // references below 2^32 bases: tpos is concatenated already
+    const uint32_t g = cls < G ? cls : class_genomes[cls - G + 1];
+    return goff[g] + tpos;
+}
+
 __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
     x ^= x >> 33;
     x *= 0xff51afd7ed558ccdull;

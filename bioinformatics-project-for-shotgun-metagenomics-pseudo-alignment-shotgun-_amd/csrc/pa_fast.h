@@ -630,7 +630,9 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
             if (!b2) continue;
             const int l = (int)__builtin_ctzll(b1 ? b1 : b2);
             const uint32_t ga = b1 ? __builtin_amdgcn_readlane(scls, l) : NONE;
-            const int64_t A = (int64_t)__builtin_amdgcn_readlane(stp, l) - (int64_t)__builtin_amdgcn_readlane(sw, l);
+            const uint32_t lcls = __builtin_amdgcn_readlane(scls, l), ltp = __builtin_amdgcn_readlane(stp, l);
+            const int64_t A = (int64_t)first_pos(lcls, ltp, a.G, a.class_genomes, a.goff, a.tpos_local) -
+                              (int64_t)__builtin_amdgcn_readlane(sw, l);
             const int64_t g0 = A - (int64_t)shift;  // genome position of staged base 0
             if (g0 < 0) continue;
             // walk bits (and the anchor genome) only in round 0 and only inside the

@@ -150,10 +150,6 @@ __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstar
         if (run < k) continue;  // window contains a non-ACGT base (src/kmer.py:145)
         uint64_t slot = table_insert<NW>(table, cap, key, home_of(key, key_hash(key), hc), n_kmers, err);
         if (slot == ~0ull) return;
-        if (tile) {  // first occurrence; a stale plain load can only be larger
-            const uint32_t t = (uint32_t)(gstart + w);
-            if (table[slot].tpos > t) atomicMin(&table[slot].tpos, t);
-        }
         uint32_t old = atomicMax(&last_g[slot], g + 1);
         if (old < g + 1) {
             uint32_t d = atomicAdd(&deg[slot], 1u);
@@ -409,10 +405,16 @@ __global__ void k_tile_pack(const uint8_t *__restrict__ codes, uint64_t n, uint6
 }
 
 // Class of the k-mer starting at every window of one genome (tile_cls is
-// pre-filled with NONE, which stays at windows with non-ACGT bases).
+// pre-filled with NONE, which stays at windows with non-ACGT bases), and the
+// key's first occurrence: slot.tpos = the smallest position of the key inside
+// its first genome (FASTA order: the specific genome, or the first of its set),
+// concatenated while the reference is < 2^32 bases, else genome-local so that
+// references of any total length tile (the concatenated position is then
+// goff[first genome] + tpos; pad::first_pos).
 template <int NW>
 __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k, uint64_t mask0,
-                           const Slot<NW> *table, HomeCfg hc, uint32_t *tile_cls) {
+                           Slot<NW> *table, HomeCfg hc, uint32_t *tile_cls, uint32_t g, uint32_t G,
+                           const uint32_t *__restrict__ class_genomes, int local) {
     uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
     if (w0 >= nwin) return;
     uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
@@ -433,8 +435,15 @@ __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, u
         if (run < k) continue;
         uint64_t slot;
         uint32_t cls, tpos;
-        if (table_find<NW>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos))
+        if (table_find<NW>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) {
             tile_cls[gstart + w] = cls;
+            if (local) {
+                const uint32_t fg = cls < G ? cls : class_genomes[cls - G + 1];
+                if (fg == g && tpos > (uint32_t)w) atomicMin(&table[slot].tpos, (uint32_t)w);  // (stale: an extra atomic)
+            } else if (tpos > (uint32_t)(gstart + w)) {
+                atomicMin(&table[slot].tpos, (uint32_t)(gstart + w));
+            }
+        }
     }
 }
 
@@ -729,19 +738,41 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
                                off, lists);
         }
         B_HIP(hipGetLastError());
-        uint64_t cs_cap = 2 * n_multi + 64;
-        B_HIP(hipMalloc(&cs_key, cs_cap * 8));
-        B_HIP(hipMalloc(&cs_rep, cs_cap * 8));
-        B_HIP(hipMalloc(&cs_id, cs_cap * 4));
-        hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0, st,
-                           cs_key, cs_cap, EMPTY);
+        // distinct genome sets: a hash over the multi slots' genome lists.  A
+        // reference has few distinct sets (C2: 342, 2000 genomes in families:
+        // ~10^4) however many multi-genome k-mers (10^9 at 8 Gbp), so the hash
+        // starts at 16 M entries and grows on overflow, up to 2 per k-mer
+        const uint64_t cs_max = 2 * n_multi + 64;
+        uint64_t cs_cap = std::min<uint64_t>(cs_max, (1ull << 24) + 64);
         unsigned sgrid = grid_for(cap) > 65536 ? 65536 : grid_for(cap);
-        hipLaunchKernelGGL(k_class_insert<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists, cs_key,
-                           cs_rep, cs_cap, err);
-        // class ids: at most n_multi classes
-        B_HIP(hipMalloc(&idx->class_size, n_multi * 4));
-        B_HIP(hipMalloc(&idx->class_off, n_multi * 8));
-        B_HIP(hipMalloc(&rep_of, n_multi * 8));
+        for (;;) {
+            B_HIP(hipMalloc(&cs_key, cs_cap * 8));
+            B_HIP(hipMalloc(&cs_rep, cs_cap * 8));
+            hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0,
+                               st, cs_key, cs_cap, EMPTY);
+            hipLaunchKernelGGL(k_class_insert<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists,
+                               cs_key, cs_rep, cs_cap, err);
+            B_HIP(hipGetLastError());
+            B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
+            B_HIP(hipStreamSynchronize(st));
+            if (!(h_err & 4u) || cs_cap >= cs_max) break;
+            hipFree(cs_key);
+            hipFree(cs_rep);
+            cs_key = cs_rep = nullptr;
+            B_HIP(hipMemsetAsync(err, 0, 4, st));
+            cs_cap = std::min<uint64_t>(cs_max, 4 * cs_cap);
+        }
+        if (h_err & 4u) {
+            pa::set_error("index build: genome-set table overflow (internal error)");
+            cleanup();
+            return PA_EINTERNAL;
+        }
+        B_HIP(hipMalloc(&cs_id, cs_cap * 4));
+        // class ids: at most min(n_multi, cs_cap) classes
+        const uint64_t max_cls = std::min<uint64_t>(n_multi, cs_cap);
+        B_HIP(hipMalloc(&idx->class_size, max_cls * 4));
+        B_HIP(hipMalloc(&idx->class_off, max_cls * 8));
+        B_HIP(hipMalloc(&rep_of, max_cls * 8));
         hipLaunchKernelGGL(k_class_number, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0,
                            st, cs_key, cs_rep, cs_id, cs_cap, deg, idx->class_size, idx->class_off, rep_of, cnt + 3,
                            cnt + 4);
@@ -775,13 +806,17 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         }
         idx->n_multi = n_cls;
         idx->class_entries = entries;
-        idx->device_bytes += n_multi * 12 + std::max<uint64_t>(entries, 1) * 4;
+        idx->device_bytes += n_cls * 12 + std::max<uint64_t>(entries, 1) * 4;
     }
     if (idx->tile_n > 0 && (uint64_t)G + idx->class_entries >= PA_TILE_REP) idx->tile_n = 0;  // ids need bit 31
     cleanup();  // the build scratch (20 B per slot) is not needed by the tiles
     deg = last_g = aux = lists = cs_id = err = nullptr;
     off = cs_key = cs_rep = rep_of = nullptr;
     cnt = nullptr;
+    if (idx->tile_n > 0) {  // tiles: 6.5 B per base (class, flags, set sizes, 2-bit string), + margin
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || idx->tile_n * 7 + (2ull << 30) > free_b) idx->tile_n = 0;
+    }
     if (idx->tile_n > 0) {  // step 6: genome tiling
         const uint64_t n = idx->tile_n, nwords = n / 32 + 32;  // padded: the walk reads up to 18 words past a position
         B_HIP(hipMalloc(&idx->tile_cls, n * 4));
@@ -794,7 +829,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             if ((uint64_t)k > len) continue;
             uint64_t nwin = len - k + 1;
             hipLaunchKernelGGL(k_tile_cls<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
-                               idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls);
+                               idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls, g, G,
+                               idx->class_genomes, idx->tpos_local);
         }
         if (k <= 31)
             hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
@@ -906,8 +942,12 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     // genome tiling for single-word keys while positions fit 32 bits (tpos);
     // PA_NO_TILE=1 turns it off (A/B measurements)
     const char *no_tile = std::getenv("PA_NO_TILE");
-    idx->tile_n = (idx->nw == 1 && k > 0 && total > 0 && total < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
+    uint64_t max_glen = 0;
+    for (uint32_t g = 0; g < n; g++) max_glen = std::max<uint64_t>(max_glen, goff[g + 1] - goff[g]);
+    idx->tile_n = (idx->nw == 1 && k > 0 && total > 0 && max_glen < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
                       ? total : 0;
+    idx->tpos_local = total >= 0xFFFFFFFFull ? 1 : 0;
+    if (const char *e = std::getenv("PA_TPOS_LOCAL")) idx->tpos_local |= e[0] == '1';  // tests: the >= 4 Gbp layout
     PA_HIP(hipMalloc(&idx->codes, std::max<uint64_t>(total, 1)));
     PA_HIP(hipMalloc(&idx->goff, (n + 1) * 8));
     PA_HIP(hipMalloc(&idx->counters, 32 * 8));

@@ -76,6 +76,7 @@ struct pa_index {
     uint64_t *goff = nullptr;          // device [n_genomes+1]
     std::vector<uint64_t> h_goff;
     uint64_t total_windows = 0;
+    int tpos_local = 0;                // slot.tpos genome-local (references of >= 2^32 bases), else concatenated
     uint64_t distinct_estimate = 0;    // HyperLogLog estimate (+3 %) when the table was sized on it, else 0
     // genome tiling (single-word keys, < 2^32 genome bases): the genomes as one
     // concatenated 2-bit string plus the class of the k-mer starting at every

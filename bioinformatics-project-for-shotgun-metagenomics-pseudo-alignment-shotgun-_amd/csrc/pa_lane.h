@@ -51,7 +51,7 @@ constexpr int kPassEntries = 64 * PA_LANE_PROBES;
 // Per-wave LDS of the lane kernel.
 struct __align__(16) LaneWave {
     uint64_t R[64][kLaneWords + 1];  // every lane's packed read (+ a zero word), for keys of listed windows
-    unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 32) | tpos
+    unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 40) | position
     uint32_t flags[64];              // bit 0: specific k-mer found off the walk, bit 1: unspecific one
     uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
     uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
@@ -148,7 +148,8 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
 struct LaneRead {
     int kind;                          // LANE_* (LANE_WALK: still resolving)
     uint32_t len, W;
-    uint32_t atp, acls, aw;            // anchor: first occurrence, class, window
+    uint64_t atp;                      // anchor: first occurrence (concatenated position)
+    uint32_t acls, aw;                 //   its class and window
     uint32_t g, nspec, nincl, hr;      // walk results (anchor genome, counts)
     uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
     uint64_t F0, F1;                   // windows failing --min-kmer-quality (never looked up)
@@ -336,14 +337,19 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
         sw[i] = (uint32_t)(((uint64_t)(W - 1) * i) / (NSEED - 1));
         skey[i] = row_bits(row, 2 * sw[i]) >> sh;
     }
-    uint32_t sfound, scls[NSEED], stp[NSEED];
-    lane_probe<NSEED>(a, skey, (1u << NSEED) - 1, sfound, scls, stp);
+    uint32_t sfound, scls[NSEED], stp32[NSEED];
+    lane_probe<NSEED>(a, skey, (1u << NSEED) - 1, sfound, scls, stp32);
+    uint64_t stp[NSEED];  // first occurrences, concatenated positions (NONE64: none)
+#pragma unroll
+    for (int i = 0; i < NSEED; i++)
+        stp[i] = bit(sfound, i) && stp32[i] != NONE ? first_pos(scls[i], stp32[i], a.G, a.class_genomes, a.goff, a.tpos_local)
+                                                     : ~0ull;
     int at = -1;
 #pragma unroll
     for (int pass = 0; pass < 2; pass++)
 #pragma unroll
         for (int i = 0; i < NSEED; i++)
-            if (at < 0 && bit(sfound, i) && stp[i] != NONE && (pass == 1 || scls[i] < a.G)) at = i;
+            if (at < 0 && stp[i] != ~0ull && (pass == 1 || scls[i] < a.G)) at = i;
     if (at < 0) return (void)LANE_HARD_WHY(3);  // no anchor
     S.atp = stp[0];
     S.acls = scls[0];
@@ -363,11 +369,12 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
         // distinct candidate stretches (selects only: no runtime register indexing)
         const int64_t e0 = (int64_t)S.atp - S.aw;
         int64_t e1 = INT64_MIN, e2 = INT64_MIN;
-        uint32_t t1 = 0, w1 = 0, c1 = 0, t2 = 0, w2 = 0, c2 = 0;
+        uint64_t t1 = 0, t2 = 0;
+        uint32_t w1 = 0, c1 = 0, w2 = 0, c2 = 0;
 #pragma unroll
         for (int i = 0; i < NSEED; i++) {
             const int64_t Ai = (int64_t)stp[i] - sw[i];
-            if (!bit(sfound, i) || stp[i] == NONE || Ai == e0 || Ai == e1 || e2 != INT64_MIN) continue;
+            if (stp[i] == ~0ull || Ai == e0 || Ai == e1 || e2 != INT64_MIN) continue;
             if (e1 == INT64_MIN) {
                 e1 = Ai;
                 t1 = stp[i], w1 = sw[i], c1 = scls[i];
@@ -635,7 +642,8 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
                 atomicOr(&LW.flags[o], 2u);
             } else {
                 atomicOr(&LW.flags[o], 1u);
-                atomicMin(&LW.cand[o], ((unsigned long long)w << 32) | t4[i]);
+                atomicMin(&LW.cand[o], ((unsigned long long)w << 40) | first_pos(cl, t4[i], a.G, a.class_genomes, a.goff,
+                                                                               a.tpos_local));
             }
         }
         wave_sync();  // the list is rewritten by the next pass
@@ -723,8 +731,8 @@ void k_align_lane(AlignArgs a) {
                         atomicAdd(&a.dbg[15], 1ull);
 #endif
                         const unsigned long long cd = LW.cand[lane];
-                        S.atp = (uint32_t)cd;
-                        S.aw = (uint32_t)(cd >> 32);
+                        S.atp = cd & ((1ull << 40) - 1);
+                        S.aw = (uint32_t)(cd >> 40);
                         S.acls = NONE;  // genome from the position
                     } else {
                         S.kind = LANE_HARD;
