@@ -65,10 +65,10 @@ struct AlignArgs {
     const uint64_t *tile_pk;
     uint64_t tile_n;
     const uint64_t *goff;           // genome start positions [G + 1] (concatenated coordinates)
-    const uint16_t *tile16;         // lane kernel tile (null: no lane kernel); set sizes for --max-genomes
     const uint64_t *tile_fl;        // lane kernel flag planes (pairs per 64 positions)
     const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
-    const uint64_t *tile_nb;        // one-substitution neighbour bits, any | specific << 32 (null: none)
+    const void *tile_nb;            // one-substitution neighbour bits (null: none)
+    int nb_spec;                    //   1: 64-bit present | specific << 32, 0: 32-bit present
     int walk_rounds;
     int tpos_local;                 // slot.tpos genome-local (first_pos), else concatenated
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
@@ -126,17 +126,19 @@ __device__ __forceinline__ void count_genome(const AlignArgs &a, const WgCounter
 #include "pa_lane.h"
 
 // Plane of the windows whose genome set is larger than mg (--max-genomes,
-// src/kmer.py:425-427), bit i of word j <-> position 64 j + i, from tile16's
-// set sizes: the lane walk then tests a walked window with one bit instead of
-// a 2-byte tile entry.  Made once per (index, mg) and cached in the index.
-__global__ __launch_bounds__(256) void k_tile_big(const uint16_t *__restrict__ t16, uint64_t n, int32_t mg,
+// src/kmer.py:425-427), bit i of word j <-> position 64 j + i, from tile_cls
+// and the set records: the lane walk then tests a walked window with one bit.
+// Made once per (index, mg) and cached in the index.
+__global__ __launch_bounds__(256) void k_tile_big(const uint32_t *__restrict__ tile_cls, uint64_t n, uint32_t G,
+                                                  const uint32_t *__restrict__ class_genomes, int32_t mg,
                                                   uint64_t *__restrict__ big, uint64_t n_words) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n_words; j += nw) {
         const uint64_t t = 64 * j + lane;
-        const uint32_t v = t < n ? t16[t] : 0u;
-        const uint64_t b = __ballot((v & PA_T16_VALID) && (int32_t)(v & PA_T16_SIZE) > mg);
+        const uint32_t v = t < n ? tile_cls[t] : NONE;
+        const bool ok = v != NONE && (int64_t)class_size_of(v & ~PA_TILE_REP, G, class_genomes) > (int64_t)mg;
+        const uint64_t b = __ballot(ok);
         if (lane == 0) big[j] = b;
     }
 }
@@ -587,9 +589,9 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_cls = idx->tile_cls;
     a.tile_pk = idx->tile_pk;
     a.goff = idx->goff;
-    a.tile16 = idx->tile_cls ? idx->tile16 : nullptr;
     a.tile_fl = idx->tile_cls ? idx->tile_fl : nullptr;
     a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
+    a.nb_spec = idx->nb_spec;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
     a.tpos_local = idx->tpos_local;
@@ -689,7 +691,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     const bool fast_ok = idx->k > 0 && idx->nw <= 2 && idx->n_kmers > 0;
     // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
     const char *no_lane = std::getenv("PA_NO_LANE");
-    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile16 && a.tile_fl && !(no_lane && no_lane[0] == '1');
+    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile_fl && !(no_lane && no_lane[0] == '1');
     if (fast_ok) {
         const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
         const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4
@@ -705,7 +707,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
                 if (!idx->tile_big) PA_HIP(hipMalloc(&idx->tile_big, n_words * 8));
                 if (idx->tile_big_mg != a.prm.mg) {
                     hipLaunchKernelGGL(k_tile_big, dim3((unsigned)std::min<uint64_t>((n_words + 3) / 4, 1u << 20)),
-                                       dim3(256), 0, st, idx->tile16, a.tile_n, (int32_t)a.prm.mg, idx->tile_big, n_words);
+                                       dim3(256), 0, st, idx->tile_cls, a.tile_n, a.G, idx->class_genomes,
+                                       (int32_t)a.prm.mg, idx->tile_big, n_words);
                     PA_HIP(hipGetLastError());
                     idx->tile_big_mg = a.prm.mg;
                 }

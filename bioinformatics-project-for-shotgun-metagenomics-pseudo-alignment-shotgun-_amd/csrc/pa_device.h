@@ -21,7 +21,6 @@ constexpr uint64_t BUSY = ~0ull - 1;     // slot being written (multi-word inser
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t PA_TILE_REP = 0x80000000u;  // tile_cls flag: the k-mer repeats within the next 127 positions
 // compact tile (uint16 per position) of the lane kernel
-constexpr uint32_t PA_T16_VALID = 0x8000u, PA_T16_REP = 0x4000u, PA_T16_SPEC = 0x2000u, PA_T16_SIZE = 0x1FFFu;
 
 template <int NW>
 struct Key {

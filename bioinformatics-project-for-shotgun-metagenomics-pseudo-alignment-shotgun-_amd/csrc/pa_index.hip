@@ -490,7 +490,9 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 // Defined on the 2-bit genome string (N packed as A), for windows that are
 // indexed themselves (tile_cls != NONE).
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
-                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, unsigned long long *nb) {
+                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full) {
+    unsigned long long *nb = (unsigned long long *)nb_out;  // full: 64-bit words, present | specific << 32
+    uint32_t *nb32 = (uint32_t *)nb_out;                    // else 32-bit words, present
     const int sh = 64 - 2 * k;
     uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -507,28 +509,14 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
                 uint64_t slot;
                 uint32_t cls, tpos;
                 if (table_find<1>(table, hc.cap, key, home_of<1>(key, key_hash(key), hc), slot, cls, tpos))
-                    atomicOr(&nb[3 * (t + j) + b], (cls < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                {
+                    if (full)
+                        atomicOr(&nb[3 * (t + j) + b], (cls < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                    else
+                        atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
+                }
             }
         }
-    }
-}
-
-// Compact tile for the lane kernel (pa_lane.h): per position 0 (no indexed
-// window) or PA_T16_VALID | [PA_T16_REP] | [PA_T16_SPEC] | min(set size, 8191).
-__global__ void k_tile16(const uint32_t *__restrict__ tile_cls, uint64_t n, uint32_t G,
-                         const uint32_t *__restrict__ class_genomes, uint16_t *__restrict__ t16) {
-    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (; t < n; t += stride) {
-        const uint32_t v = tile_cls[t];
-        uint16_t o = 0;
-        if (v != NONE) {
-            const uint32_t c = v & ~PA_TILE_REP;
-            const uint32_t sz = class_size_of(c, G, class_genomes);
-            o = (uint16_t)(PA_T16_VALID | ((v & PA_TILE_REP) ? PA_T16_REP : 0u) | (c < G ? PA_T16_SPEC : 0u) |
-                           (sz < PA_T16_SIZE ? sz : PA_T16_SIZE));
-        }
-        t16[t] = o;
     }
 }
 
@@ -536,7 +524,7 @@ __global__ void k_tile16(const uint32_t *__restrict__ tile_cls, uint64_t n, uint
 // (A, B), bit i <-> position 64 j + i: (0,0) no indexed window, (1,0) a
 // multi-genome k-mer, (1,1) a specific one, (0,1) a k-mer that repeats within
 // 127 positions (PA_TILE_REP).  0.25 B per base: the 120 windows of a read
-// are one or two 64-B lines, where the 2-byte tile16 is four or five.
+// are one or two 64-B lines, where a 2-byte entry per position would be four or five.
 // One wave per word pair, the planes by ballot.
 __global__ __launch_bounds__(256) void k_tile_planes(const uint32_t *__restrict__ tile_cls, uint64_t n, uint32_t G,
                                                      uint64_t *__restrict__ fl, uint64_t n_pairs) {
@@ -835,28 +823,30 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         if (k <= 31)
             hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
                                st, idx->tile_pk, idx->tile_cls, n, k);
-        if (k <= 31 && G < PA_T16_SIZE) {  // set sizes fit 13 bits exactly
-            B_HIP(hipMalloc(&idx->tile16, n * 2 + 512));  // padded: the lane walk loads 2 x 33 dwords
-            B_HIP(hipMemsetAsync(idx->tile16, 0, n * 2 + 512, st));
-            hipLaunchKernelGGL(k_tile16, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
-                               idx->tile_cls, n, G, idx->class_genomes, idx->tile16);
-            idx->device_bytes += n * 2;
+        if (k <= 31) {
             const uint64_t n_pairs = n / 64 + 4;  // padded: the walk reads three pairs from any position
             B_HIP(hipMalloc(&idx->tile_fl, n_pairs * 16));
             hipLaunchKernelGGL(k_tile_planes, dim3((unsigned)std::min<uint64_t>((n_pairs + 3) / 4, 1u << 20)), dim3(256),
                                0, st, idx->tile_cls, n, G, idx->tile_fl, n_pairs);
             idx->device_bytes += n_pairs * 16;
-            // one-substitution neighbours (12 B per base) when they fit a quarter of the free memory;
-            // PA_NO_NB=1 skips them (A/B measurements)
+            // one-substitution neighbours: 24 B per base (present | specific) when
+            // that leaves a quarter of the free memory, else 12 B (present only:
+            // a present neighbour is then probed), else none; PA_NO_NB=1 skips
+            // them, PA_NB_HALF=1 forces the 12-B form (A/B measurements, tests)
             size_t free_b = 0, total_b = 0;
-            const char *no_nb = std::getenv("PA_NO_NB");
-            if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess && n * 24 <= free_b / 4) {
-                B_HIP(hipMalloc(&idx->tile_nb, n * 24 + 64));
-                B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 24 + 64, st));
-                hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
-                                   idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                   (unsigned long long *)idx->tile_nb);
-                idx->device_bytes += n * 24;
+            const char *no_nb = std::getenv("PA_NO_NB"), *nb_half = std::getenv("PA_NB_HALF");
+            if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+                const bool full = n * 24 <= free_b / 4 * 3 && !(nb_half && nb_half[0] == '1');
+                const uint64_t wb = full ? 8 : 4;
+                if (n * 3 * wb <= free_b / 4 * 3) {
+                    B_HIP(hipMalloc(&idx->tile_nb, n * 3 * wb + 64));
+                    B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 3 * wb + 64, st));
+                    hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
+                                       st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                       idx->tile_nb, full ? 1 : 0);
+                    idx->nb_spec = full ? 1 : 0;
+                    idx->device_bytes += n * 3 * wb;
+                }
             }
         }
         B_HIP(hipGetLastError());
@@ -903,7 +893,6 @@ void index_release(pa_index *idx) {
     hipFree(idx->goff);
     hipFree(idx->tile_cls);
     hipFree(idx->tile_pk);
-    hipFree(idx->tile16);
     hipFree(idx->tile_fl);
     idx->tile_fl = nullptr;
     hipFree(idx->tile_big);
@@ -913,7 +902,6 @@ void index_release(pa_index *idx) {
     idx->tile_nb = nullptr;
     idx->tile_cls = nullptr;
     idx->tile_pk = nullptr;
-    idx->tile16 = nullptr;
     hipFree(idx->ws.ptr);
     hipFree(idx->queue);
     hipFree(idx->queue_hard);

@@ -84,11 +84,11 @@ struct pa_index {
     uint64_t tile_n = 0;               // concatenated bases (0: no tiling)
     uint32_t *tile_cls = nullptr;      // [tile_n]
     uint64_t *tile_pk = nullptr;       // [tile_n / 32 + 32] MSB-first 2-bit words (padded)
-    uint16_t *tile16 = nullptr;        // [tile_n] lane-kernel tile: valid | rep | specific | set size (G < 8191)
     uint64_t *tile_fl = nullptr;       // [2 (tile_n / 64 + 4)] lane-kernel flag planes (k_tile_planes)
     uint64_t *tile_big = nullptr;      // [tile_n / 64 + 4] plane "set size > tile_big_mg" (pa_align, cached)
     int64_t tile_big_mg = -1;          // the --max-genomes value tile_big was made for (-1: none)
-    uint64_t *tile_nb = nullptr;       // [3 tile_n] one-substitution neighbour bits, any | specific << 32 (k_nb_build), optional
+    void *tile_nb = nullptr;           // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional:
+    int nb_spec = 0;                   //   1: 64-bit words, present | specific << 32; 0: 32-bit words, present
     uint64_t device_bytes = 0;
     // align scratch
     pa::Workspace ws;

@@ -47,6 +47,13 @@ constexpr int kLaneWords = 6;     // 64-bit words of the packed read (32 bases e
 #define PA_LANE_SLOTS 1   // table slots per probe step in the cooperative passes
 #endif
 constexpr int kPassEntries = 64 * PA_LANE_PROBES;
+// Per-workgroup LDS unique counters up to this many genomes (12 B each); above
+// it the lane kernel counts in global memory (one atomic per unique read), so
+// that the counters do not cost occupancy.
+#ifndef PA_LANE_LDS_GENOMES
+#define PA_LANE_LDS_GENOMES 512
+#endif
+constexpr uint32_t kLaneLdsGenomeCap = PA_LANE_LDS_GENOMES;
 
 // Per-wave LDS of the lane kernel.
 struct __align__(16) LaneWave {
@@ -486,8 +493,15 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             if (has_nb) {
                 // neighbour word of the genome base at A + e and the read's base there
                 const uint32_t cg = (uint32_t)(gwi >> (62 - 2 * j)) & 3u, cr = (uint32_t)(row[i] >> (62 - 2 * j)) & 3u;
-                const uint64_t nbq = a.tile_nb[3 * ((uint64_t)A + e) + ((cr - cg - 1) & 3u)];
-                const uint64_t nbw = nbq & 0xFFFFFFFFull, nbs = nbq >> 32;  // present, present and specific
+                const uint64_t ni = 3 * ((uint64_t)A + e) + ((cr - cg - 1) & 3u);
+                uint64_t nbw, nbs;  // present, present and specific (unknown: present)
+                if (a.nb_spec) {
+                    const uint64_t nbq = ((const uint64_t *)a.tile_nb)[ni];
+                    nbw = nbq & 0xFFFFFFFFull;
+                    nbs = nbq >> 32;
+                } else {
+                    nbw = nbs = ((const uint32_t *)a.tile_nb)[ni];
+                }
 #ifdef PA_STATS
                 atomicAdd(&a.dbg[16], 1ull);
 #endif
@@ -666,7 +680,7 @@ void k_align_lane(AlignArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const uint32_t G = a.G;
     const int lane = lane_id();
-    const bool lds = G <= kLdsGenomeCap;
+    const bool lds = G <= kLaneLdsGenomeCap;
     const size_t cnt_bytes = lds ? ((size_t)G * 12 + 15) / 16 * 16 : 0;
     unsigned long long *first = (unsigned long long *)smem;
     uint32_t *uniq = (uint32_t *)(first + (lds ? G : 0));
@@ -806,5 +820,5 @@ void k_align_lane(AlignArgs a) {
 }
 
 constexpr size_t lane_lds_bytes(uint32_t G) {
-    return (G <= kLdsGenomeCap ? ((size_t)G * 12 + 15) / 16 * 16 : 0) + (size_t)kWaves * sizeof(LaneWave);
+    return (G <= kLaneLdsGenomeCap ? ((size_t)G * 12 + 15) / 16 * 16 : 0) + (size_t)kWaves * sizeof(LaneWave);
 }
