@@ -243,13 +243,15 @@ __device__ __forceinline__ uint32_t lane_mismatches(const AlignArgs &a, const ui
 #pragma unroll
     for (int i = 0; i <= kLaneWords; i++) gw[i] = gp[i];
     uint32_t n = 0;
+    // the read's last word holds len - 32 * qlast bases: one mask (not one per word)
+    const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;
+    const uint64_t tail = rl >= 32 ? ~0ull : ~0ull << (64 - 2 * rl);
 #pragma unroll
     for (int i = 0; i < kLaneWords; i++) {
         if (32 * i >= (int)len) break;
         const uint64_t gwi = gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i];
         uint64_t d = row[i] ^ gwi;
-        const uint32_t rest = len - 32 * i;
-        if (rest < 32) d &= ~0ull << (64 - 2 * rest);
+        if ((uint32_t)i == qlast) d &= tail;
         n += __popcll((d | (d >> 1)) & 0x5555555555555555ull);
     }
     return n;
@@ -344,8 +346,26 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
         sw[i] = (uint32_t)(((uint64_t)(W - 1) * i) / (NSEED - 1));
         skey[i] = row_bits(row, 2 * sw[i]) >> sh;
     }
-    uint32_t sfound, scls[NSEED], stp32[NSEED];
-    lane_probe<NSEED>(a, skey, (1u << NSEED) - 1, sfound, scls, stp32);
+#ifndef PA_LANE_SEED_ROUNDS
+#define PA_LANE_SEED_ROUNDS 2
+#endif
+    // two rounds: the first and the last seed, then -- only if neither is a
+    // specific k-mer -- the middle ones (a random 64-B line per probe is what
+    // bounds this kernel)
+    uint32_t sfound = 0, scls[NSEED], stp32[NSEED];
+    {
+        constexpr uint32_t all = (1u << NSEED) - 1, outer = 1u | (1u << (NSEED - 1));
+        uint32_t act = PA_LANE_SEED_ROUNDS > 1 ? outer : all;
+#pragma unroll 1
+        for (int round = 0; round < 2 && act; round++) {
+            uint32_t f;
+            lane_probe<NSEED>(a, skey, act, f, scls, stp32);
+            sfound |= f;
+            const bool spec = (bit(f, 0) && scls[0] < a.G && stp32[0] != NONE) ||
+                              (bit(f, NSEED - 1) && scls[NSEED - 1] < a.G && stp32[NSEED - 1] != NONE);
+            act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
+        }
+    }
     uint64_t stp[NSEED];  // first occurrences, concatenated positions (NONE64: none)
 #pragma unroll
     for (int i = 0; i < NSEED; i++)
@@ -463,13 +483,14 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0, NS0 = 0, NS1 = 0;
     uint32_t nmis = 0;
     const bool has_nb = a.tile_nb != nullptr;
+    const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;  // the last word holds rl bases
+    const uint64_t tail = rl >= 32 ? ~0ull : ~0ull << (64 - 2 * rl);
 #pragma unroll
     for (int i = 0; i < kLaneWords; i++) {
         if (32 * i >= (int)len) break;
         const uint64_t gwi = gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i];
         uint64_t d = row[i] ^ gwi;
-        const uint32_t rest = len - 32 * i;  // bases of the read in this word
-        if (rest < 32) d &= ~0ull << (64 - 2 * rest);
+        if ((uint32_t)i == qlast) d &= tail;
         uint64_t m = (d | (d >> 1)) & 0x5555555555555555ull;  // one bit per mismatching base
         while (m) {
             const uint32_t j = __builtin_clzll(m) >> 1, e = 32 * i + j;
