@@ -460,3 +460,53 @@ def test_large_reference_layout(monkeypatch):
                       mg=full["mg"], detail=False)
         assert stats.tolist() == o.stats.tolist(), ps
         assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_pseudo_align_random_big_kmers_property(seed):
+    """The reference's randomized property test (src/test_kmer.py:227-247, 364-421),
+    seeded: the 31-mers of the 63-bp BigRead spread at random over 4 genomes
+    joined by NN; the read is unique iff the specific-count margin is >= m and
+    the total-count gap is <= p, recomputed from the index view -- and the GPU
+    result equals the oracle's."""
+    import random
+    from kmer import KmerReference, Read, ReadMappingType, extract_kmers_from_genome
+    from records import FASTAQRecordContainer, FASTARecordContainer
+    fq = FASTAQRecordContainer()
+    fq.parse_records("@BigRead\nAGCTAGCTAGAGGTCCTAATCCTAGCTAGCTAGCTAGCTAGCTAGCTGGTCATCAAAACCTTT\n+\n" + "I" * 63 + "\n")
+    rec = list(fq)[0]
+    rnd = random.Random(seed)
+    k = 31
+    genomes = {f">Genome{i + 1}": [] for i in range(4)}
+    for _, km in extract_kmers_from_genome(k, rec["sequence"]):
+        for g in rnd.sample(list(genomes), k=rnd.randint(1, 4)):
+            genomes[g].append(km)
+    if any(not s for s in genomes.values()):
+        pytest.skip("a genome drew no k-mer")
+    fa = FASTARecordContainer()
+    fa.parse_records("".join(f"{name}\n{'NN'.join(seq)}\n" for name, seq in genomes.items()))
+    ref = KmerReference(k, fa)
+    m, p = 1, 1
+    spec, total = {}, {}
+    for km, gmap in ref.kmers.items():
+        if len(gmap) == 1:
+            g0 = next(iter(gmap))
+            spec[g0] = spec.get(g0, 0) + len(gmap[g0])
+        for g, pos in gmap.items():
+            total[g] = total.get(g, 0) + len(pos)
+    result = Read(rec).pseudo_align(ref, m=m, p=p)
+    order = sorted(spec, key=spec.get, reverse=True)
+    if not order:
+        assert result == ReadMappingType.AMBIGUOUSLY_MAPPED
+    else:
+        top = spec[order[0]]
+        second = spec[order[1]] if len(order) > 1 else 0
+        if top - second >= m and not max(total.values()) - total[order[0]] > p:
+            assert result == ReadMappingType.UNIQUELY_MAPPED
+        else:
+            assert result == ReadMappingType.AMBIGUOUSLY_MAPPED
+    oix = O.OracleIndex([g["genome"] for g in fa], k)
+    seq, off = O.concat([rec["sequence"]])
+    qual, _ = O.concat([rec["quality_sequence"]])
+    o = oix.align(seq, qual, off, m=m, p=p)
+    assert int(o.types[0]) == result.value
