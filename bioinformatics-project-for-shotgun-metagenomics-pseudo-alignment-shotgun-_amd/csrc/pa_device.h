@@ -157,6 +157,53 @@ __device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint6
     }
 }
 
+// NP single-word probes in flight together, a whole 64-B line (4 slots) per
+// step: tables are whole lines (cap % 4 == 0), so a search costs ~1-2 round
+// trips even at a high load factor, where slot-by-slot probing (table_find)
+// pays one dependent load per slot.  Bit i of `found` / cls[i]: key i's result.
+template <int NP>
+__device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, const HomeCfg &hc,
+                                                const uint64_t (&key)[NP], uint32_t (&cls)[NP]) {
+    uint64_t pos[NP];
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+        Key<1> kk;
+        kk.w[0] = key[i];
+        pos[i] = home_of<1>(kk, key_hash(kk), hc);
+    }
+    uint32_t act = (1u << NP) - 1, found = 0;
+    while (act) {
+        Slot<1> s[NP][4];
+#pragma unroll
+        for (int i = 0; i < NP; i++)
+            if ((act >> i) & 1u) {
+                const uint64_t b = pos[i] & ~3ull;
+#pragma unroll
+                for (int h = 0; h < 4; h++) s[i][h] = t[b + h];
+            }
+#pragma unroll
+        for (int i = 0; i < NP; i++) {
+            if (!((act >> i) & 1u)) continue;
+            const uint64_t b = pos[i] & ~3ull;
+            bool done = false;
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                if (done || b + h < pos[i]) continue;
+                if (s[i][h].key[0] == EMPTY) {
+                    done = true;
+                } else if (s[i][h].key[0] == key[i]) {
+                    done = true;
+                    found |= 1u << i;
+                    cls[i] = s[i][h].cls;
+                }
+            }
+            if (done) act &= ~(1u << i);
+            pos[i] = (b + 4 == hc.cap) ? 0 : b + 4;
+        }
+    }
+    return found;
+}
+
 // ---- wavefront (64-lane) helpers ------------------------------------------
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }

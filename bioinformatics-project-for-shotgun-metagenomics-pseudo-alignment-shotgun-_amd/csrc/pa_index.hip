@@ -502,19 +502,18 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
         for (int j = 0; j < k; j++) {
             const int bs = 2 * (k - 1 - j);
             const uint64_t cj = (K >> bs) & 3;
+            uint64_t keys[3];
+            uint32_t cls[3];
+#pragma unroll
+            for (int b = 0; b < 3; b++) keys[b] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
+            const uint32_t f = probe_lines<3>(table, hc, keys, cls);  // the three substitutions together
 #pragma unroll
             for (int b = 0; b < 3; b++) {
-                Key<1> key;
-                key.w[0] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
-                uint64_t slot;
-                uint32_t cls, tpos;
-                if (table_find<1>(table, hc.cap, key, home_of<1>(key, key_hash(key), hc), slot, cls, tpos))
-                {
-                    if (full)
-                        atomicOr(&nb[3 * (t + j) + b], (cls < G ? 0x100000001ull : 1ull) << (k - 1 - j));
-                    else
-                        atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
-                }
+                if (!((f >> b) & 1u)) continue;
+                if (full)
+                    atomicOr(&nb[3 * (t + j) + b], (cls[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                else
+                    atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
             }
         }
     }
