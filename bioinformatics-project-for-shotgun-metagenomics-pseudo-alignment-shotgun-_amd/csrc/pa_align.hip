@@ -69,10 +69,12 @@ struct AlignArgs {
     const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
     const void *tile_nb;            // one-substitution neighbour bits (null: none)
     int nb_spec;                    //   1: 64-bit present | specific << 32, 0: 32-bit present
+    const uint64_t *bloom;          // Bloom filter of the keys (null: none), 2^bloom_lg words
+    uint32_t bloom_lg;
     int walk_rounds;
     int tpos_local;                 // slot.tpos genome-local (first_pos), else concatenated
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
-    int dbg_mode;  // PA_STATS builds: stop each read after phase N (timing dissection; results invalid)
+    int dbg_mode;  // PA_STATS / PA_DISSECT builds: stop each read after phase N (timing dissection; results invalid)
     const uint8_t *seq;
     const uint8_t *qual;
     const uint64_t *off;
@@ -592,6 +594,8 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_fl = idx->tile_cls ? idx->tile_fl : nullptr;
     a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
     a.nb_spec = idx->nb_spec;
+    a.bloom = idx->tile_cls ? idx->bloom : nullptr;
+    a.bloom_lg = idx->bloom_lg;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
     a.tpos_local = idx->tpos_local;
@@ -745,7 +749,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     fprintf(stderr, "[pa_stats] lane: cooperative probes %llu re-anchors %llu neighbour words %llu | pending: invalid %llu "
             "2+ mismatches %llu neighbour present %llu\n", d[18], d[19], d[20], d[21], d[22], d[23]);
     fprintf(stderr, "[pa_stats] lane found: shared-neighbour+specific %llu second-walk specific %llu probed-shared+specific %llu"
-            " | unique by bound %llu\n", d[24], d[25], d[26], d[27]);
+            " | unique by bound %llu, by off-walk count %llu | probes past the Bloom filter %llu\n", d[24], d[25], d[26], d[27], d[28],
+            d[29]);
 #endif
     return PA_OK;
 }

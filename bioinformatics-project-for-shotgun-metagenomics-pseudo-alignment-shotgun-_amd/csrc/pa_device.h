@@ -204,6 +204,27 @@ __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, c
     return found;
 }
 
+// Word-blocked Bloom filter of the table's single-word keys (the lane
+// kernel's prefilter for the windows it must probe): 2^lg 64-bit words, one
+// word per key (the top lg bits of a 64-bit mix, lg <= 28) and six bits in it
+// (six 6-bit fields of the low 36).  No false negatives: a key whose bits are
+// not all set is not in the table.
+__device__ __forceinline__ uint64_t bloom_mix(uint64_t x) {
+    x ^= 0x9E3779B97F4A7C15ull;
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+__device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) m |= 1ull << ((h >> (6 * i)) & 63);
+    return m;
+}
+
 // ---- wavefront (64-lane) helpers ------------------------------------------
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }

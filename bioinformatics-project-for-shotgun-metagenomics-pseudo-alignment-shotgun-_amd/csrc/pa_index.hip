@@ -519,6 +519,18 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
     }
 }
 
+// The Bloom filter of the table's keys (pa_device.h bloom_mix): one pass over
+// the slots, an atomic OR per key.
+__global__ void k_bloom_build(const Slot<1> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+        const uint64_t key = table[i].key[0];
+        if (key == EMPTY) continue;
+        const uint64_t h = bloom_mix(key);
+        atomicOr((unsigned long long *)&bloom[h >> (64 - lg)], (unsigned long long)bloom_bits(h));
+    }
+}
+
 // Flag planes of the lane walk (pa_lane.h): per 64 positions a word pair
 // (A, B), bit i <-> position 64 j + i: (0,0) no indexed window, (1,0) a
 // multi-genome k-mer, (1,1) a specific one, (0,1) a k-mer that repeats within
@@ -847,6 +859,25 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
                     idx->device_bytes += n * 3 * wb;
                 }
             }
+            // the Bloom filter of the keys, for the lane kernel's probes of windows
+            // off the walk (almost all absent): worth it while it stays in the
+            // memory-side cache, so 16 bits per key up to PA_BLOOM_MB (default
+            // 64; 0: none), fewer down to 8 bits per key, else none
+            {
+                const char *bm = std::getenv("PA_BLOOM_MB");
+                const uint64_t cap_b = (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 64ull) << 20;
+                uint32_t lg = 6;
+                while (lg < 28 && (1ull << lg) * 64 < idx->n_kmers * 16) lg++;
+                while (lg > 6 && (1ull << lg) * 8 > cap_b) lg--;
+                if (cap_b > 0 && idx->n_kmers > 0 && (1ull << lg) * 64 >= idx->n_kmers * 8 && (1ull << lg) * 8 <= cap_b) {
+                    B_HIP(hipMalloc(&idx->bloom, (1ull << lg) * 8));
+                    B_HIP(hipMemsetAsync(idx->bloom, 0, (1ull << lg) * 8, st));
+                    hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                       dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg);
+                    idx->bloom_lg = lg;
+                    idx->device_bytes += (1ull << lg) * 8;
+                }
+            }
         }
         B_HIP(hipGetLastError());
         B_HIP(hipStreamSynchronize(st));
@@ -899,6 +930,9 @@ void index_release(pa_index *idx) {
     idx->tile_big_mg = -1;
     hipFree(idx->tile_nb);
     idx->tile_nb = nullptr;
+    hipFree(idx->bloom);
+    idx->bloom = nullptr;
+    idx->bloom_lg = 0;
     idx->tile_cls = nullptr;
     idx->tile_pk = nullptr;
     hipFree(idx->ws.ptr);

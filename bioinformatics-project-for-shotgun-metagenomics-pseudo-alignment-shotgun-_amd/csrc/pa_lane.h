@@ -59,7 +59,7 @@ constexpr uint32_t kLaneLdsGenomeCap = PA_LANE_LDS_GENOMES;
 struct __align__(16) LaneWave {
     uint64_t R[64][kLaneWords + 1];  // every lane's packed read (+ a zero word), for keys of listed windows
     unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 40) | position
-    uint32_t flags[64];              // bit 0: specific k-mer found off the walk, bit 1: unspecific one
+    uint32_t flags[64];              // bit 0: specific k-mer found off the walk; bits 2..: unspecific ones found
     uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
     uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
 };
@@ -664,6 +664,21 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
                 act |= 1u << i;
             }
         }
+        if (a.bloom) {  // windows whose key is surely absent are not probed
+            uint64_t bw[NPR], bm[NPR];
+#pragma unroll
+            for (int i = 0; i < NPR; i++) {
+                const uint64_t h = bloom_mix(key4[i]);
+                bm[i] = bloom_bits(h);
+                bw[i] = bit(act, i) ? a.bloom[h >> (64 - a.bloom_lg)] : ~0ull;
+            }
+#pragma unroll
+            for (int i = 0; i < NPR; i++)
+                if ((bw[i] & bm[i]) != bm[i]) act &= ~(1u << i);
+#ifdef PA_STATS
+            atomicAdd(&a.dbg[25], (unsigned long long)__popc(act));
+#endif
+        }
         uint32_t f, c4[NPR], t4[NPR];
         lane_probe<NPR, PA_LANE_SLOTS>(a, key4, act, f, c4, t4);
 #pragma unroll
@@ -674,7 +689,7 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
             if ((a.prm.flags & F_MG) && (int64_t)class_size_of(cl, a.G, a.class_genomes) > (int64_t)a.prm.mg) {
                 atomicAdd(&LW.hr[o], 1u);  // highly redundant: counted, never included
             } else if (cl >= a.G) {
-                atomicOr(&LW.flags[o], 2u);
+                atomicAdd(&LW.flags[o], 4u);  // unspecific: counted in bits 2..
             } else {
                 atomicOr(&LW.flags[o], 1u);
                 atomicMin(&LW.cand[o], ((unsigned long long)w << 40) | first_pos(cl, t4[i], a.G, a.class_genomes, a.goff,
@@ -722,13 +737,13 @@ void k_align_lane(AlignArgs a) {
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows are done with
         if (r < a.n) lane_prep<NEED_Q, WIN_Q>(a, r, LW.R[lane], S);
-#ifdef PA_STATS
+#if defined(PA_STATS) || defined(PA_DISSECT)
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
 #pragma unroll 1
         for (int attempt = 0; attempt < 2; attempt++) {
             if (S.kind == LANE_WALK) lane_walk<WIN_Q>(a, LW.R[lane], S);
-#ifdef PA_STATS
+#if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif
             if (!__ballot(S.kind == LANE_WALK)) break;
@@ -750,9 +765,9 @@ void k_align_lane(AlignArgs a) {
 #endif
                 }
             }
-            // a multi-genome k-mer off the walk next to walked specific ones: the
-            // wave kernel, without probing
-            if (S.kind == LANE_WALK && S.uoff && S.nspec > 0) {
+            // a multi-genome k-mer off the walk next to walked specific ones
+            // under --max-genomes (its set size decides): the wave kernel, without probing
+            if (S.kind == LANE_WALK && S.uoff && S.nspec > 0 && (a.prm.flags & F_MG)) {
                 S.kind = LANE_HARD;
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
@@ -776,8 +791,22 @@ void k_align_lane(AlignArgs a) {
                     }
                 } else {
                     S.hr += LW.hr[lane];
-                    if ((fl & 2u) || S.uoff) {  // unspecific k-mers off the walk: fine only without specific ones
-                        if (S.nspec > 0) {
+                    const uint32_t noff = (fl >> 2) + S.uoff;  // unspecific k-mers off the walk
+                    if (noff) {
+                        // Only g has specific k-mers (the walked ones; none off the
+                        // walk), so the specific map is {g} and the read is UNIQUE g
+                        // (src/kmer.py:452-454) unless the total counts demote it:
+                        // any h has at most (nincl - nspec) + noff distinct included
+                        // k-mers, g at least nincl, so with noff - nspec <= p no total
+                        // exceeds g's by more than p (src/kmer.py:471-474).  Set sizes
+                        // (--max-genomes) are not known for the uoff windows: not then.
+                        if (S.nspec > 0 && !(a.prm.flags & F_MG) &&
+                            (a.prm.p < 0 || (int64_t)noff - (int64_t)S.nspec <= (int64_t)a.prm.p)) {
+                            S.kind = LANE_UNIQUE;
+#ifdef PA_STATS
+                            atomicAdd(&a.dbg[24], 1ull);
+#endif
+                        } else if (S.nspec > 0) {
                             S.kind = LANE_HARD;
                             LANE_HARD_WHY(7);
                             LANE_HARD_WHY(18);
