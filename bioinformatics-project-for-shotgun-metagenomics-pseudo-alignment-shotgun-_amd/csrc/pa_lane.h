@@ -483,6 +483,9 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0, NS0 = 0, NS1 = 0;
     uint32_t nmis = 0;
     const bool has_nb = a.tile_nb != nullptr;
+    uint64_t epk = 0;  // positions e of the mismatches to look up in the neighbour bits (8 bits each, <= 8)
+    uint32_t cpk = 0;  //   their substitution index (cr - cg - 1) & 3 (2 bits each)
+    uint32_t nnb = 0;
     const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;  // the last word holds rl bases
     const uint64_t tail = rl >= 32 ? ~0ull : ~0ull << (64 - 2 * rl);
 #pragma unroll
@@ -511,32 +514,45 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             V1 |= U1 & r1;
             U0 |= r0;
             U1 |= r1;
-            if (has_nb) {
-                // neighbour word of the genome base at A + e and the read's base there
+            if (has_nb) {  // the neighbour word of the genome base at A + e and the read's base there
                 const uint32_t cg = (uint32_t)(gwi >> (62 - 2 * j)) & 3u, cr = (uint32_t)(row[i] >> (62 - 2 * j)) & 3u;
-                const uint64_t ni = 3 * ((uint64_t)A + e) + ((cr - cg - 1) & 3u);
-                uint64_t nbw, nbs;  // present, present and specific (unknown: present)
-                if (a.nb_spec) {
-                    const uint64_t nbq = ((const uint64_t *)a.tile_nb)[ni];
-                    nbw = nbq & 0xFFFFFFFFull;
-                    nbs = nbq >> 32;
-                } else {
-                    nbw = nbs = ((const uint32_t *)a.tile_nb)[ni];
-                }
+                epk |= (uint64_t)e << (8 * nnb);
+                cpk |= ((cr - cg - 1) & 3u) << (2 * nnb);
+                nnb++;
+            }
+        }
+    }
+    // the neighbour words, four loads in flight at a time (one round trip for
+    // up to four mismatches, not one per mismatch)
+#pragma unroll 1
+    for (uint32_t b0 = 0; b0 < nnb; b0 += 4) {
+        uint64_t nv[4];
+        int32_t sf[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t q = b0 + u < nnb ? b0 + u : b0;  // (a repeated load past the last)
+            const uint32_t e = (uint32_t)(epk >> (8 * q)) & 255u, c = (cpk >> (2 * q)) & 3u;
+            const uint64_t ni = 3 * ((uint64_t)A + e) + c;
+            nv[u] = a.nb_spec ? ((const uint64_t *)a.tile_nb)[ni] : (uint64_t)((const uint32_t *)a.tile_nb)[ni];
+            sf[u] = b0 + u < nnb ? (int32_t)e - k + 1 : 1000;  // bit q of the word <-> window e - k + 1 + q
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (sf[u] == 1000) continue;
+            // present, present and specific (the 32-bit form: present only)
+            const uint64_t nbw = nv[u] & 0xFFFFFFFFull, nbs = a.nb_spec ? nv[u] >> 32 : nbw;
 #ifdef PA_STATS
-                atomicAdd(&a.dbg[16], 1ull);
+            atomicAdd(&a.dbg[16], 1ull);
 #endif
-                // bit q <-> window e - k + 1 + q
-                const int32_t sft = (int32_t)e - k + 1;
-                if (sft >= 0) {
-                    NP0 |= sft < 64 ? nbw << sft : 0ull;
-                    NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 32 ? nbw >> (64 - sft) : 0ull);
-                    NS0 |= sft < 64 ? nbs << sft : 0ull;
-                    NS1 |= sft >= 64 ? nbs << (sft - 64) : (sft > 32 ? nbs >> (64 - sft) : 0ull);
-                } else {
-                    NP0 |= nbw >> (-sft);
-                    NS0 |= nbs >> (-sft);
-                }
+            const int32_t sft = sf[u];
+            if (sft >= 0) {
+                NP0 |= sft < 64 ? nbw << sft : 0ull;
+                NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 32 ? nbw >> (64 - sft) : 0ull);
+                NS0 |= sft < 64 ? nbs << sft : 0ull;
+                NS1 |= sft >= 64 ? nbs << (sft - 64) : (sft > 32 ? nbs >> (64 - sft) : 0ull);
+            } else {
+                NP0 |= nbw >> (-sft);
+                NS0 |= nbs >> (-sft);
             }
         }
     }
@@ -776,7 +792,11 @@ void k_align_lane(AlignArgs a) {
             if (S.kind == LANE_WALK) {
                 const uint32_t fl = LW.flags[lane];
                 if (fl & 1u) {  // a specific k-mer off the walk: walk again from it (once)
-                    if (attempt == 0) {
+#if defined(PA_STATS) || defined(PA_DISSECT)
+                    if (a.dbg_mode == 12) S.kind = LANE_AMB;  // timing dissection: no second walk
+#endif
+                    if (S.kind != LANE_WALK) {
+                    } else if (attempt == 0) {
 #ifdef PA_STATS
                         atomicAdd(&a.dbg[15], 1ull);
 #endif
