@@ -62,9 +62,11 @@ struct __align__(16) LaneWave {
     uint32_t flags[64];              // bit 0: specific k-mer found off the walk; bits 2..: unspecific ones found
     uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
     uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
+    uint32_t again_r[128];           // reads to walk again from a specific k-mer found off their walk,
+    unsigned long long again_a[128]; //   and that anchor: (window << 40) | position
 };
 
-enum : int { LANE_UNIQUE = 0, LANE_AMB = 1, LANE_UNMAPPED = 2, LANE_DROP = 3, LANE_HARD = 4, LANE_WALK = 5 };
+enum : int { LANE_UNIQUE = 0, LANE_AMB = 1, LANE_UNMAPPED = 2, LANE_DROP = 3, LANE_HARD = 4, LANE_WALK = 5, LANE_AGAIN = 6 };
 
 // Word q of a register array by a runtime index (selects; no scratch).
 template <int N>
@@ -257,9 +259,11 @@ __device__ __forceinline__ uint32_t lane_mismatches(const AlignArgs &a, const ui
     return n;
 }
 
-// Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor.
+// Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor (a
+// read walked again: the given anchor, cd != ~0).
 template <bool NEED_Q, bool WIN_Q>
-__device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64_t *row, LaneRead &S) {
+__device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsigned long long cd, uint64_t *row,
+                                          LaneRead &S) {
     S.kind = LANE_HARD;
     S.hr = S.nspec = S.nincl = 0;
     S.F0 = S.F1 = 0;
@@ -335,6 +339,13 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, uint64
     }
     row[kLaneWords] = 0;
     if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
+    if (cd != ~0ull) {  // walked again: from the specific k-mer found off the first walk
+        S.atp = cd & ((1ull << 40) - 1);
+        S.aw = (uint32_t)(cd >> 40);
+        S.acls = NONE;  // genome from the position
+        S.kind = LANE_WALK;
+        return;
+    }
     const int sh = 64 - 2 * k;
     // ---- seeds: NSEED windows spread evenly from the first to the last; a
     // specific one (its genome is the read's) is preferred as the anchor
@@ -745,19 +756,41 @@ void k_align_lane(AlignArgs a) {
         __syncthreads();
     }
     uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0, n_hr = 0, n_qf = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    const uint64_t n_iter = (a.n + stride - 1) / stride;  // uniform trip count (wave-wide phases)
-    for (uint64_t it = 0; it < n_iter; it++) {
-        const uint64_t r = it * stride + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    // Each wave takes chunks of 64 consecutive reads; a read whose walk finds a
+    // specific k-mer off it is walked again from that k-mer, but later, with 63
+    // others (a list per wave), so that the 3 % of such reads do not hold whole
+    // waves for a second walk.  Every decision below is wave-uniform.
+    const uint64_t n_chunks = (a.n + 63) / 64, wave_stride = (uint64_t)gridDim.x * kWaves;
+    uint64_t chunk = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    uint32_t n_again = 0;  // entries in LW.again_r / again_a
+    while (true) {
+        uint64_t r = ~0ull;
+        unsigned long long cd = ~0ull;
+        bool again_batch = false;
+        if (n_again >= 64 || (chunk >= n_chunks && n_again > 0)) {
+            const uint32_t take = n_again < 64 ? n_again : 64;
+            if ((uint32_t)lane < take) {
+                r = LW.again_r[n_again - take + lane];
+                cd = LW.again_a[n_again - take + lane];
+            }
+            n_again -= take;
+            again_batch = true;
+        } else if (chunk < n_chunks) {
+            r = chunk * 64 + lane;
+            if (r >= a.n) r = ~0ull;
+            chunk += wave_stride;
+        } else {
+            break;
+        }
         LaneRead S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
-        wave_sync();  // the previous read's rows are done with
-        if (r < a.n) lane_prep<NEED_Q, WIN_Q>(a, r, LW.R[lane], S);
+        wave_sync();  // the previous read's rows (and the taken list entries) are done with
+        if (r != ~0ull) lane_prep<NEED_Q, WIN_Q>(a, r, cd, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
 #pragma unroll 1
-        for (int attempt = 0; attempt < 2; attempt++) {
+        for (int attempt = again_batch ? 1 : 0; attempt < 2; attempt++) {
             if (S.kind == LANE_WALK) lane_walk<WIN_Q>(a, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
@@ -796,14 +829,11 @@ void k_align_lane(AlignArgs a) {
                     if (a.dbg_mode == 12) S.kind = LANE_AMB;  // timing dissection: no second walk
 #endif
                     if (S.kind != LANE_WALK) {
-                    } else if (attempt == 0) {
+                    } else if (attempt == 0) {  // later, in a batch of such reads
 #ifdef PA_STATS
                         atomicAdd(&a.dbg[15], 1ull);
 #endif
-                        const unsigned long long cd = LW.cand[lane];
-                        S.atp = cd & ((1ull << 40) - 1);
-                        S.aw = (uint32_t)(cd >> 40);
-                        S.acls = NONE;  // genome from the position
+                        S.kind = LANE_AGAIN;
                     } else {
                         S.kind = LANE_HARD;
                         LANE_HARD_WHY(7);
@@ -847,6 +877,15 @@ void k_align_lane(AlignArgs a) {
             if (lane == __builtin_ctzll(hb)) qbase = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
             qbase = shfl64(qbase, __builtin_ctzll(hb));
             if (hard) a.queue_hard[qbase + lanes_below(hb)] = (uint32_t)r;
+        }
+        const bool again = S.kind == LANE_AGAIN;
+        const uint64_t ab = __ballot(again);
+        if (ab) {  // (at most 63 + 64 entries: a batch is taken once 64 wait)
+            if (again) {
+                LW.again_r[n_again + lanes_below(ab)] = (uint32_t)r;
+                LW.again_a[n_again + lanes_below(ab)] = LW.cand[lane];
+            }
+            n_again += (uint32_t)__popcll(ab);
         }
         if (S.kind == LANE_UNIQUE) {
             const uint64_t key = first_key(a.base + r, 0);
