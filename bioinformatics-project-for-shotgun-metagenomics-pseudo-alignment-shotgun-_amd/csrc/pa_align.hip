@@ -751,6 +751,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     fprintf(stderr, "[pa_stats] lane found: shared-neighbour+specific %llu second-walk specific %llu probed-shared+specific %llu"
             " | unique by bound %llu, by off-walk count %llu | probes past the Bloom filter %llu\n", d[24], d[25], d[26], d[27], d[28],
             d[29]);
+    fprintf(stderr, "[pa_stats] lane seeds: anchor ranked among stretches %llu, second seed round %llu\n", d[30], d[31]);
 #endif
     return PA_OK;
 }

@@ -37,6 +37,10 @@ constexpr int kLaneMaxW = 128;    // windows per read on the lane path
 constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
 constexpr int kLaneChunks = 12;   // 16-B chunks covering shift + kLaneMaxLen bases
 constexpr int kLaneWords = 6;     // 64-bit words of the packed read (32 bases each)
+#ifndef PA_LANE_MAXMIS
+#define PA_LANE_MAXMIS 40
+#endif
+constexpr uint32_t kLaneMaxMis = PA_LANE_MAXMIS;  // mismatching bases against the anchor stretch (else the wave kernel)
 #ifndef PA_LANE_PROBES
 #define PA_LANE_PROBES 4  // unwalked windows probed per lane and cooperative pass
 #endif
@@ -375,6 +379,9 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             const bool spec = (bit(f, 0) && scls[0] < a.G && stp32[0] != NONE) ||
                               (bit(f, NSEED - 1) && scls[NSEED - 1] < a.G && stp32[NSEED - 1] != NONE);
             act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
+#ifdef PA_STATS
+            if (act) atomicAdd(&a.dbg[27], 1ull);
+#endif
         }
     }
     uint64_t stp[NSEED];  // first occurrences, concatenated positions (NONE64: none)
@@ -422,6 +429,9 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             }
         }
         if (e1 != INT64_MIN) {
+#ifdef PA_STATS
+            atomicAdd(&a.dbg[26], 1ull);
+#endif
             uint32_t best = ~0u, bj = 0;
 #pragma unroll 1
             for (uint32_t j = 0; j < 3; j++) {
@@ -517,9 +527,19 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
                 hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) & (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
                          : 0ull;
             if (!((r0 & IX0) | (r1 & IX1))) continue;
-            if (++nmis > 8) {  // a wrong stretch, not a few sequencing errors
-                S.kind = LANE_HARD;
-                return (void)LANE_HARD_WHY(5);
+            if (++nmis > 8) {
+                // past the neighbour-bit budget (a sibling's stretch, not a few
+                // sequencing errors): its windows are probed; the walked ones
+                // still hold (a found specific k-mer re-anchors the read)
+                if (nmis > kLaneMaxMis) {
+                    S.kind = LANE_HARD;
+                    return (void)LANE_HARD_WHY(5);
+                }
+                V0 |= r0;
+                V1 |= r1;
+                U0 |= r0;
+                U1 |= r1;
+                continue;
             }
             V0 |= U0 & r0;
             V1 |= U1 & r1;
