@@ -286,9 +286,13 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     if (NEED_Q) {
         const uint4 *qp = (const uint4 *)(a.qual + o0);
         uint32_t sum = 0, qmin = 255;
-#pragma unroll 1
-        for (uint32_t c = 0; c < nch; c += 2) {
-            const uint4 v0 = qp[c], v1 = qp[c + 1];  // (buffers are padded past the last read)
+        uint4 qc[2 * kLaneWords];  // every chunk load issued before any is used (one round trip)
+#pragma unroll
+        for (uint32_t c = 0; c < 2 * kLaneWords; c++) qc[c] = c < nch ? qp[c] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t c = 0; c < 2 * kLaneWords; c += 2) {
+            if (c >= nch) break;
+            const uint4 v0 = qc[c], v1 = qc[c + 1];
             const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
             for (int e = 0; e < 8; e++) {
@@ -325,11 +329,15 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     const uint32_t s2 = 2 * shift;
     uint32_t bad = 0;
     uint64_t prev = 0;
-#pragma unroll 1
+    // every chunk load of the read issued before any is used (one round trip)
+    uint4 ch[2 * kLaneWords];
+#pragma unroll
+    for (int c = 0; c < 2 * kLaneWords; c++) ch[c] = 16u * c < shift + len ? sp[c] : make_uint4(0, 0, 0, 0);
+#pragma unroll
     for (int q = 0; q <= kLaneWords; q++) {
         uint64_t P = 0;
         if (q < kLaneWords && 32u * q < shift + len) {
-            const uint4 v0 = sp[2 * q], v1 = sp[2 * q + 1];
+            const uint4 v0 = ch[2 * q], v1 = ch[2 * q + 1];
             const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
             for (int e = 0; e < 8; e++) {
