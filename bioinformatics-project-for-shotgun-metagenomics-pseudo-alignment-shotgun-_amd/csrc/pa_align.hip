@@ -69,6 +69,7 @@ struct AlignArgs {
     const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
     const void *tile_nb;            // one-substitution neighbour bits (null: none)
     int nb_spec;                    //   1: 64-bit present | specific << 32, 0: 32-bit present
+    const uint32_t *gblk;           // the genome holding position j << 16 (tiled indexes)
     const uint64_t *bloom;          // Bloom filter of the keys (null: none), 2^bloom_lg words
     uint32_t bloom_lg;
     int walk_rounds;
@@ -594,6 +595,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_fl = idx->tile_cls ? idx->tile_fl : nullptr;
     a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
     a.nb_spec = idx->nb_spec;
+    a.gblk = idx->tile_gblk;
     a.bloom = idx->tile_cls ? idx->bloom : nullptr;
     a.bloom_lg = idx->bloom_lg;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;

@@ -831,6 +831,21 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
                                idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls, g, G,
                                idx->class_genomes, idx->tpos_local);
         }
+        {  // genome of every 2^16-th position: genome_of is then one or two goff steps
+            const uint64_t nb_ = (n >> 16) + 2;
+            std::vector<uint32_t> gb(nb_);
+            for (uint64_t j = 0; j < nb_; j++) {
+                const uint64_t pos = j << 16;
+                uint32_t g = (uint32_t)(std::upper_bound(idx->h_goff.begin(), idx->h_goff.begin() + G + 1, pos) -
+                                        idx->h_goff.begin());
+                g = g == 0 ? 0 : g - 1;
+                gb[j] = g >= G ? G - 1 : g;
+            }
+            B_HIP(hipMalloc(&idx->tile_gblk, nb_ * 4));
+            B_HIP(hipMemcpyAsync(idx->tile_gblk, gb.data(), nb_ * 4, hipMemcpyHostToDevice, st));
+            B_HIP(hipStreamSynchronize(st));
+            idx->device_bytes += nb_ * 4;
+        }
         if (k <= 31)
             hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
                                st, idx->tile_pk, idx->tile_cls, n, k);
@@ -932,6 +947,8 @@ void index_release(pa_index *idx) {
     idx->tile_nb = nullptr;
     hipFree(idx->bloom);
     idx->bloom = nullptr;
+    hipFree(idx->tile_gblk);
+    idx->tile_gblk = nullptr;
     idx->bloom_lg = 0;
     idx->tile_cls = nullptr;
     idx->tile_pk = nullptr;

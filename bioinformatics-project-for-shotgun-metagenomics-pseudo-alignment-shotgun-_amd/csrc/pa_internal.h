@@ -89,6 +89,7 @@ struct pa_index {
     int64_t tile_big_mg = -1;          // the --max-genomes value tile_big was made for (-1: none)
     void *tile_nb = nullptr;           // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional:
     int nb_spec = 0;                   //   1: 64-bit words, present | specific << 32; 0: 32-bit words, present
+    uint32_t *tile_gblk = nullptr;     // [(tile_n >> 16) + 2] the genome holding position j << 16
     uint64_t *bloom = nullptr;         // [2^bloom_lg] Bloom filter of the table's keys (k_bloom_build), optional
     uint32_t bloom_lg = 0;
     uint64_t device_bytes = 0;

@@ -89,9 +89,11 @@ __device__ __forceinline__ uint64_t bits_at(const uint64_t (&v)[N], uint32_t o) 
     return r ? (hi | (word_at(v, q + 1) >> (64 - r))) : hi;
 }
 
-// Genome containing concatenated position t (binary search over goff).
-__device__ __forceinline__ uint32_t genome_of(const uint64_t *goff, uint32_t G, uint64_t t) {
-    uint32_t lo = 0, hi = G;  // goff[lo] <= t < goff[hi]
+// Genome containing concatenated position t (t < tile_n): a binary search over
+// goff between the genomes holding positions (t >> 16) << 16 and the next
+// 2^16-th (gblk) -- one genome, or two, for genomes longer than 64 kb.
+__device__ __forceinline__ uint32_t genome_of(const uint64_t *goff, const uint32_t *gblk, uint64_t t) {
+    uint32_t lo = gblk[t >> 16], hi = gblk[(t >> 16) + 1] + 1;  // goff[lo] <= t < goff[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (goff[mid] <= t)
@@ -489,7 +491,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         pa3[i] = fp[2 * i];
         pb3[i] = fp[2 * i + 1];
     }
-    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.G, S.atp);
+    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.gblk, S.atp);
     S.g = g;
     const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
     // every window of the read must lie inside the anchor genome
