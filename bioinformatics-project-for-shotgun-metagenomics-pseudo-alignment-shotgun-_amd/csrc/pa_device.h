@@ -225,6 +225,26 @@ __device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
     return m;
 }
 
+// The Bloom word of a k-mer (k <= 31) and its bits: the 64-B line is chosen by
+// the k-mer's minimizer (15-mers, hashed) -- windows of one read that share it,
+// most neighbours, read the same line (+1 % on C2, C3) -- the word within the
+// line and the bits by the k-mer's own mix.
+__device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uint64_t &w, uint64_t &m) {
+    const uint64_t h = bloom_mix(key);
+    m = bloom_bits(h);
+    const int mm = k < 15 ? k : 15;
+    const uint64_t mmask = (1ull << (2 * mm)) - 1;
+    uint32_t best = ~0u;
+    for (int i = 0; i + mm <= k; i++) {
+        const uint32_t x = (uint32_t)((key >> (2 * i)) & mmask);
+        uint32_t y = x * 0x9E3779B1u;  // (odd multiplier: a bijection on 32 bits)
+        y ^= y >> 15;
+        best = y < best ? y : best;
+    }
+    const uint64_t line = bloom_mix(best) >> (64 - (lg - 3));
+    w = (line << 3) | (h >> 61);
+}
+
 // ---- wavefront (64-lane) helpers ------------------------------------------
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }

@@ -521,13 +521,14 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
 
 // The Bloom filter of the table's keys (pa_device.h bloom_mix): one pass over
 // the slots, an atomic OR per key.
-__global__ void k_bloom_build(const Slot<1> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg) {
+__global__ void k_bloom_build(const Slot<1> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg, int k) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
         const uint64_t key = table[i].key[0];
         if (key == EMPTY) continue;
-        const uint64_t h = bloom_mix(key);
-        atomicOr((unsigned long long *)&bloom[h >> (64 - lg)], (unsigned long long)bloom_bits(h));
+        uint64_t w, m;
+        bloom_word(key, k, lg, w, m);
+        atomicOr((unsigned long long *)&bloom[w], (unsigned long long)m);
     }
 }
 
@@ -888,7 +889,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
                     B_HIP(hipMalloc(&idx->bloom, (1ull << lg) * 8));
                     B_HIP(hipMemsetAsync(idx->bloom, 0, (1ull << lg) * 8, st));
                     hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
-                                       dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg);
+                                       dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg, k);
                     idx->bloom_lg = lg;
                     idx->device_bytes += (1ull << lg) * 8;
                 }

@@ -353,6 +353,12 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     }
     row[kLaneWords] = 0;
     if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
+#if defined(PA_STATS) || defined(PA_DISSECT)
+    if (a.dbg_mode == 13) {  // timing dissection: stop after the packing
+        S.kind = LANE_AMB;
+        return;
+    }
+#endif
     if (cd != ~0ull) {  // walked again: from the specific k-mer found off the first walk
         S.atp = cd & ((1ull << 40) - 1);
         S.aw = (uint32_t)(cd >> 40);
@@ -389,6 +395,9 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             const bool spec = (bit(f, 0) && scls[0] < a.G && stp32[0] != NONE) ||
                               (bit(f, NSEED - 1) && scls[NSEED - 1] < a.G && stp32[NSEED - 1] != NONE);
             act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
+#if defined(PA_STATS) || defined(PA_DISSECT)
+            if (a.dbg_mode == 14) act = 0;  // timing dissection: one seed round
+#endif
 #ifdef PA_STATS
             if (act) atomicAdd(&a.dbg[27], 1ull);
 #endif
@@ -725,9 +734,9 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
             uint64_t bw[NPR], bm[NPR];
 #pragma unroll
             for (int i = 0; i < NPR; i++) {
-                const uint64_t h = bloom_mix(key4[i]);
-                bm[i] = bloom_bits(h);
-                bw[i] = bit(act, i) ? a.bloom[h >> (64 - a.bloom_lg)] : ~0ull;
+                uint64_t wi;
+                bloom_word(key4[i], a.k, a.bloom_lg, wi, bm[i]);
+                bw[i] = bit(act, i) ? a.bloom[wi] : ~0ull;
             }
 #pragma unroll
             for (int i = 0; i < NPR; i++)
