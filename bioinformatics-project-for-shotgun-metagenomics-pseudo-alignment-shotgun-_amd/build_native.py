@@ -23,7 +23,7 @@ BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libpa.so")
 ARCH = os.environ.get("PA_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["pa_index.hip", "pa_align.hip", "pa_api.cpp", "pa_ingest.cpp"]
+SOURCES = ["pa_index.hip", "pa_align.hip", "pa_api.cpp", "pa_ingest.cpp", "pa_comm.cpp"]
 HEADERS = ["pa_device.h", "pa_internal.h", "pa_fast.h", "pa_lane.h", "pa_home.h"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-value", "-Wno-unused-result", f"-I{INCLUDE}"]
 
@@ -77,7 +77,7 @@ def build(force: bool = False, verbose: bool = False, stats: bool = False, varia
     with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), 4))) as ex:
         list(ex.map(run, jobs))
     if force or jobs or _stale(lib, objs):
-        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-lz", "-lpthread"])
+        run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-lz", "-lpthread", "-ldl"])
     return lib
 
 

@@ -79,6 +79,8 @@ pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *ge
     *out = nullptr;
     PA_CHECK(genome_off != nullptr, PA_EINVAL, "genome_off must not be NULL");
     PA_CHECK(k <= PA_MAX_K, PA_EUNSUPPORTED, "k-mer length above PA_MAX_K (159) is not supported");
+    PA_CHECK(n_genomes <= PA_MAX_GENOMES, PA_EUNSUPPORTED,
+             "more than PA_MAX_GENOMES (2^20 - 1) genomes: the Summary order keys hold a list position in 20 bits");
     for (uint32_t g = 0; g < n_genomes; g++)
         PA_CHECK(genome_off[g + 1] >= genome_off[g], PA_EINVAL, "genome_off must be non-decreasing");
     const uint64_t total = genome_off[n_genomes] - genome_off[0];

@@ -863,7 +863,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             size_t free_b = 0, total_b = 0;
             const char *no_nb = std::getenv("PA_NO_NB"), *nb_half = std::getenv("PA_NB_HALF");
             if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-                const bool full = n * 24 <= free_b / 4 * 3 && !(nb_half && nb_half[0] == '1');
+                const bool full = n * 24 <= free_b / 4 * 3 && !(nb_half && nb_half[0] == '1') && !idx->force_large;
                 const uint64_t wb = full ? 8 : 4;
                 if (n * 3 * wb <= free_b / 4 * 3) {
                     B_HIP(hipMalloc(&idx->tile_nb, n * 3 * wb + 64));
@@ -881,7 +881,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             // 64; 0: none), fewer down to 8 bits per key, else none
             {
                 const char *bm = std::getenv("PA_BLOOM_MB");
-                const uint64_t cap_b = (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 64ull) << 20;
+                const uint64_t cap_b = idx->force_large ? 0ull : (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 64ull) << 20;
                 uint32_t lg = 6;
                 while (lg < 28 && (1ull << lg) * 64 < idx->n_kmers * 16) lg++;
                 while (lg > 6 && (1ull << lg) * 8 > cap_b) lg--;
@@ -986,7 +986,13 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     idx->tile_n = (idx->nw == 1 && k > 0 && total > 0 && max_glen < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
                       ? total : 0;
     idx->tpos_local = total >= 0xFFFFFFFFull ? 1 : 0;
+    // PA_LAYOUT=large (tests): every choice the build makes for a reference too
+    // large for the default layout (C5: 8 Gbp) -- table sized on the distinct
+    // estimate at 1.43 slots per k-mer, genome-local first occurrences, the 12-B
+    // present-only neighbour bits, no Bloom filter -- on a small reference
+    if (const char *e = std::getenv("PA_LAYOUT")) idx->force_large = std::strcmp(e, "large") == 0;
     if (const char *e = std::getenv("PA_TPOS_LOCAL")) idx->tpos_local |= e[0] == '1';  // tests: the >= 4 Gbp layout
+    idx->tpos_local |= idx->force_large;
     PA_HIP(hipMalloc(&idx->codes, std::max<uint64_t>(total, 1)));
     PA_HIP(hipMalloc(&idx->goff, (n + 1) * 8));
     PA_HIP(hipMalloc(&idx->counters, 32 * 8));
@@ -1027,6 +1033,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     if (const char *e = std::getenv("PA_CAP_HLL")) {  // tests / A-B: size on the distinct estimate, at 1.43 per k-mer
         if (e[0] == '1') cap = 0, free_b = (size_t)0;
     }
+    if (idx->force_large) cap = 0, free_b = (size_t)0;
     if (cap == 0 && k > 0 && windows > 0) {
         uint32_t *reg = nullptr;
         PA_HIP(hipMalloc(&reg, (4ull << kHllBits)));

@@ -162,6 +162,7 @@ class KmerReference:
         if not isinstance(k, int):
             raise TypeError(f"k must be an int, got {type(k)}")
         self.genomes: List[Record] = list(fasta_record_container)
+        self._all_genomes: Optional[List[Record]] = None  # before EXTSIM dropped any (k-mer view order)
         self.kmer_len: int = k
         self._device = N.default_device() if device is None else int(device)
         self._build()
@@ -190,6 +191,7 @@ class KmerReference:
                                    [len(g["genome"]) for g in self.genomes], similarity_threshold)
         if len(keep) != len({g.identifier for g in self.genomes}):
             self._index.close()
+            self._all_genomes = self.genomes
             self.genomes = [g for g in self.genomes if g.identifier in keep]
             self._build()  # pruning dropped genomes == building from the kept ones
         self.similarity_info = info
@@ -220,12 +222,20 @@ class KmerReference:
         """Introspection view ``{kmer: {Record: positions}}`` in the reference's
         insertion order (built on the host on first access; not used to align)."""
         if self._view is None:
+            # After EXTSIM the reference deletes the dropped genomes' entries from
+            # the full dict (src/kmer.py:232-245): the remaining k-mers keep the
+            # order of the full build, so walk every original genome and keep
+            # the kept ones' positions only.
+            kept = None if self._all_genomes is None else {id(g) for g in self.genomes}
             view: Dict[str, Dict[Record, Set[int]]] = {}
-            for rec in self.genomes:
+            for rec in (self.genomes if kept is None else self._all_genomes):
+                keep = kept is None or id(rec) in kept
                 for pos, km in extract_kmers_from_genome(self.kmer_len, rec["genome"]):
                     if constants.NULL_NUCLEOTIDES_CHAR not in km:
-                        view.setdefault(km, {}).setdefault(rec, set()).add(pos)
-            self._view = view
+                        entry = view.setdefault(km, {})
+                        if keep:
+                            entry.setdefault(rec, set()).add(pos)
+            self._view = view if kept is None else {km: gs for km, gs in view.items() if gs}
         return self._view
 
     def _genome_set(self, kmer: str) -> List[int]:
@@ -345,13 +355,42 @@ class Read:
 
 
 class _Batch:
-    """A container batch aligned on the GPU, kept for lazy per-read results."""
+    """A container batch aligned on the GPU, kept for lazy per-read results.
+    ``all_dropped``: every read failed --min-read-quality on the host (no GPU
+    pass was needed, see _align_columns)."""
 
-    __slots__ = ("base", "ids", "seq", "qual", "off", "params", "entries")
+    __slots__ = ("base", "ids", "seq", "qual", "off", "params", "mrq", "entries", "all_dropped", "_dropped")
 
-    def __init__(self, base, ids, seq, qual, off, params):
+    def __init__(self, base, ids, seq, qual, off, params, mrq, all_dropped=False):
         self.base, self.ids, self.seq, self.qual, self.off, self.params = base, ids, seq, qual, off, params
-        self.entries = None
+        self.mrq, self.all_dropped, self.entries, self._dropped = mrq, all_dropped, None, None
+
+    def dropped(self) -> Optional[np.ndarray]:
+        """Reads dropped by --min-read-quality (not in PseudoAlignment.reads), or None if none can be."""
+        if self.all_dropped:
+            return np.ones(len(self.ids), dtype=bool)
+        if self.mrq is None:
+            return None
+        if self._dropped is None:
+            self._dropped = _dropped_mask(self.qual, self.off, self.mrq)
+        return self._dropped
+
+
+def _dropped_mask(qual: np.ndarray, off: np.ndarray, mrq) -> np.ndarray:
+    """Read.mean_quality() < min_read_quality per read (src/kmer.py:394-399, 587),
+    raw ASCII: an exact integer test for an int threshold, the reference's own
+    float division (IEEE double, as numpy's) otherwise."""
+    off = np.asarray(off, dtype=np.int64)
+    lens = np.diff(off)
+    n = lens.size
+    sums = np.zeros(n, dtype=np.int64)
+    if qual.size and n:
+        nz = lens > 0
+        sums[nz] = np.add.reduceat(qual.astype(np.int64), off[:-1][nz])
+    if isinstance(mrq, int):
+        return sums < int(mrq) * lens
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return (sums / lens) < float(mrq)
 
 
 def _columnar(container) -> Tuple[List[str], np.ndarray, np.ndarray, np.ndarray]:
@@ -388,24 +427,35 @@ class PseudoAlignment:
     # -- bookkeeping ------------------------------------------------------------
 
     def _known_ids(self) -> Set[str]:
+        """Identifiers already in ``reads`` (src/kmer.py:557): reads dropped by
+        --min-read-quality never entered it."""
         if self._ids is None:
             ids: Set[str] = set()
             for b in self._batches:
-                ids.update(b.ids)
+                d = b.dropped()
+                ids.update(b.ids if d is None else (i for i, x in zip(b.ids, d) if not x))
             ids.update(i for _, i, _ in self._host)
             self._ids = ids
         return self._ids
 
-    def _add_ids(self, ids: Sequence[str]) -> None:
-        if not self._batches and not self._host:
-            return  # the first batch comes from one container, whose ids the parser made unique
+    def _add_ids(self, ids: Sequence[str], dropped: Optional[np.ndarray], unique_batch: bool) -> None:
+        """AddingExistingRead for an identifier already aligned -- before or
+        earlier in this batch (src/kmer.py:557-558).  ``unique_batch``: the ids
+        come from one parsed FASTQ container, which the grammar made unique."""
+        if not self._batches and not self._host and unique_batch:
+            return
         known = self._known_ids()
-        for rid in ids:
-            if rid in known:
+        seen: Set[str] = set()
+        for i, rid in enumerate(ids):
+            if dropped is not None and dropped[i]:
+                continue
+            if rid in known or (not unique_batch and rid in seen):
                 raise AddingExistingRead(f"There already exists a read with identifier: {rid}")
+            if not unique_batch:
+                seen.add(rid)
 
     def add_read(self, read: Read) -> None:
-        self._add_ids([read.identifier])
+        self._add_ids([read.identifier], None, False)
         if self._ids is not None:
             self._ids.add(read.identifier)
         entry = {"mapping_type": read.mapping.type,
@@ -425,9 +475,10 @@ class PseudoAlignment:
                                    min_read_quality: Optional[int] = None, min_kmer_quality: Optional[int] = None,
                                    max_genomes: Optional[int] = None) -> None:
         ids, seq, qual, off = _columnar(reads_container)
-        self._align_columns(ids, seq, qual, off, m, p, min_read_quality, min_kmer_quality, max_genomes)
+        self._align_columns(ids, seq, qual, off, m, p, min_read_quality, min_kmer_quality, max_genomes,
+                            unique_batch=isinstance(reads_container, FASTAQRecordContainer))
 
-    def _align_columns(self, ids, seq, qual, off, m, p, mrq, mkq, mg) -> None:
+    def _align_columns(self, ids, seq, qual, off, m, p, mrq, mkq, mg, unique_batch=False) -> None:
         n = len(ids)
         if n == 0:
             return
@@ -438,31 +489,42 @@ class PseudoAlignment:
         if mg is not None:
             self.filter_max_genomes_flag = True
         err = _check_align_args(self.kmer_reference, m, p, mrq, mkq, mg)
+        all_dropped = False
         if err is not None:
-            # the reference checks arguments only for reads that pass --min-read-quality
-            if mrq is None or not isinstance(mrq, (int, float)):
+            # the reference checks the arguments (Read.pseudo_align) only for
+            # reads that pass --min-read-quality (src/kmer.py:587-592): a batch
+            # whose every read is dropped by it is only counted
+            if mrq is None or isinstance(mrq, bool) or not isinstance(mrq, (int, float)):
                 raise err
-            sums = np.add.reduceat(qual.astype(np.int64), off[:-1].astype(np.int64)) if qual.size else None
-            lens = np.diff(off).astype(np.int64)
-            if sums is None or np.any(sums >= mrq * lens):
+            if not _dropped_mask(qual, off, mrq).all():
                 raise err
-        self._add_ids(ids)
+            all_dropped = True
+        dropped = _dropped_mask(qual, off, mrq) if (mrq is not None and (self._batches or self._host
+                                                                          or not unique_batch)) else None
+        self._add_ids(ids, np.ones(n, dtype=bool) if all_dropped else dropped, unique_batch)
         ref = self.kmer_reference
-        if self._result is None:
-            self._result = N.Result(ref.index)
-        prm = N.Params.make(m if err is None else 0, p if err is None else 0, mrq, mkq, mg)
-        reads = N.Reads.upload(seq, qual, off, device=ref.index.device)
-        N.align(ref.index, reads, prm, self._next_index, self._result)
-        stats, _, _, _ = self._result.fetch()
-        reads.close()
-        delta = stats - self._gpu_stats
-        self._gpu_stats = stats
-        self.filtered_quality_reads += int(delta[3])
-        self.filtered_quality_kmers += int(delta[4])
-        self.filtered_hr_kmers += int(delta[5])
-        self._batches.append(_Batch(self._next_index, ids, seq, qual, off, prm))
+        prm = None
+        if all_dropped:
+            self.filtered_quality_reads += n
+        else:
+            if self._result is None:
+                self._result = N.Result(ref.index)
+            prm = N.Params.make(m, p, mrq, mkq, mg)
+            reads = N.Reads.upload(seq, qual, off, device=ref.index.device)
+            N.align(ref.index, reads, prm, self._next_index, self._result)
+            stats, _, _, _ = self._result.fetch()
+            reads.close()
+            delta = stats - self._gpu_stats
+            self._gpu_stats = stats
+            self.filtered_quality_reads += int(delta[3])
+            self.filtered_quality_kmers += int(delta[4])
+            self.filtered_hr_kmers += int(delta[5])
+        b = _Batch(self._next_index, ids, seq, qual, off, prm, mrq, all_dropped)
+        b._dropped = dropped
+        self._batches.append(b)
         if self._ids is not None:
-            self._ids.update(ids)
+            d = b.dropped()
+            self._ids.update(ids if d is None else (i for i, x in zip(ids, d) if not x))
         self._next_index += n
 
     # -- results ----------------------------------------------------------------
@@ -474,6 +536,8 @@ class PseudoAlignment:
         ref = self.kmer_reference
         items: List[Tuple[int, str, Dict[str, Any]]] = list(self._host)
         for b in self._batches:
+            if b.all_dropped:
+                continue
             if b.entries is None:
                 reads = N.Reads.upload(b.seq, b.qual, b.off, device=ref.index.device)
                 types, _, _, loff, lists = N.align_detail(ref.index, reads, b.params)

@@ -58,17 +58,54 @@ def reduce_blocks(sum_block, min_block, group=None) -> None:
         dist.all_reduce(min_block, op=dist.ReduceOp.MIN, group=group)
 
 
-def reduce_result(result, device, stream=None, group=None):
-    """Copy a pa_result's blocks into torch tensors on `device`, all-reduce them
-    over RCCL and return (sum_block, min_block) as tensors."""
+def reduce_result(result, device, stream=None, group=None, write_back: bool = True):
+    """All-reduce a pa_result's counter blocks over torch.distributed and return
+    them as (sum_block, min_block) int64 tensors on `device`.
+
+    The blocks are copied out of the result (pa_result_copy_out, stream-ordered
+    on `stream`), reduced -- in place on the device over RCCL for the "nccl"
+    backend, through host tensors for "gloo" (CPU rehearsals, several ranks on
+    one device) -- and, with `write_back`, copied back into the result
+    (pa_result_copy_in), which then holds the job's counters."""
     import torch
+    import torch.distributed as dist
     sum_t = torch.empty(result.n_sum, dtype=torch.int64, device=device)
     min_t = torch.empty(max(result.n_genomes, 1), dtype=torch.int64, device=device)
     if result.n_genomes == 0:
         min_t.fill_(NO_FIRST_KEY)
     result.copy_out(sum_t.data_ptr(), min_t.data_ptr() if result.n_genomes else 0, stream)
-    reduce_blocks(sum_t, min_t, group)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.get_backend(group) == "gloo":
+            torch.cuda.synchronize(device)
+            sum_c, min_c = sum_t.cpu(), min_t.cpu()
+            reduce_blocks(sum_c, min_c, group)
+            sum_t.copy_(sum_c)
+            min_t.copy_(min_c)
+            torch.cuda.synchronize(device)
+        else:
+            reduce_blocks(sum_t, min_t, group)
+    if write_back:
+        result.copy_in(sum_t.data_ptr(), min_t.data_ptr() if result.n_genomes else 0, stream)
     return sum_t, min_t
+
+
+def make_comm(device: int, group=None):
+    """An RCCL communicator of the torch.distributed ranks for the C ABI's
+    pa_counters_reduce: rank 0 makes the id, a broadcast shares it."""
+    import torch.distributed as dist
+    import pa_native as N
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    box = [N.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0, group=group)
+    return N.Comm(device, world, rank, box[0])
+
+
+def reduce_result_capi(result, comm, stream=None) -> None:
+    """The same reduction through libpa.so only (pa_counters_reduce: ncclSum /
+    ncclMin in place on the result's device blocks) -- what an integrator
+    without torch would call."""
+    import pa_native as N
+    N.counters_reduce(result, comm, stream)
 
 
 def summary_from_blocks(sum_block: np.ndarray, min_block: np.ndarray, identifiers: Sequence[str],

@@ -19,6 +19,8 @@ LIB_PATH = os.environ.get("PA_LIBRARY", os.path.join(HERE, "libpa.so"))
 PA_OK, PA_EINVAL, PA_ETYPE, PA_ENOMEM, PA_EDEVICE, PA_EUNSUPPORTED, PA_EINTERNAL, PA_ENOTCANON, PA_EIO = range(9)
 PA_FASTA, PA_FASTQ = 0, 1
 PA_MAX_K = 159
+PA_MAX_GENOMES = (1 << 20) - 1
+PA_COMM_ID_BYTES = 128
 HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4
 NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
 
@@ -31,6 +33,7 @@ EXPORTS = (
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
     "pa_result_copy_in", "pa_result_free",
     "pa_align", "pa_align_detail", "pa_align_batch",
+    "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_counters_reduce",
     "pa_profile_enable", "pa_profile_read",
     "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free",
 )
@@ -119,6 +122,10 @@ def lib():
         "pa_align": (I32, [P, P, ctypes.POINTER(Params), U64, P, P]),
         "pa_align_detail": (I32, [P, P, ctypes.POINTER(Params), P, P, P, P, P, U64, ctypes.POINTER(U64), P]),
         "pa_align_batch": (I32, [P, P, P, P, U64, U64, ctypes.POINTER(Params), ctypes.POINTER(Stats), P, P, P, P]),
+        "pa_comm_unique_id": (I32, [P]),
+        "pa_comm_init": (I32, [I32, I32, I32, P, PP]),
+        "pa_comm_free": (I32, [P]),
+        "pa_counters_reduce": (I32, [P, P, P]),
         "pa_profile_enable": (I32, [P, I32]),
         "pa_profile_read": (I32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "pa_parse_text": (I32, [I32, P, U64, I32, I32, PP]),
@@ -479,6 +486,44 @@ class Result:
             self._h = None
 
     __del__ = close
+
+
+class Comm:
+    """An RCCL communicator of the job's ranks (pa_comm_init), for
+    pa_counters_reduce.  Rank 0 makes the id (``unique_id()``); every rank
+    passes the same bytes."""
+
+    def __init__(self, device: int, nranks: int, rank: int, uid: bytes):
+        if len(uid) != PA_COMM_ID_BYTES:
+            raise ValueError("communicator id must be PA_COMM_ID_BYTES bytes")
+        h = P()
+        buf = ctypes.create_string_buffer(bytes(uid), PA_COMM_ID_BYTES)
+        _check(lib().pa_comm_init(int(device), int(nranks), int(rank), ctypes.cast(buf, P), ctypes.byref(h)))
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(PA_COMM_ID_BYTES)
+        _check(lib().pa_comm_unique_id(ctypes.cast(buf, P)))
+        return buf.raw
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pa_comm_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+
+def counters_reduce(result: "Result", comm, stream=None) -> None:
+    """In-place SUM / MIN all-reduce of a pa_result over RCCL (pa_counters_reduce);
+    ``comm`` is a Comm or a raw ncclComm_t pointer."""
+    h = comm.handle if isinstance(comm, Comm) else P(int(comm))
+    _check(lib().pa_counters_reduce(result.handle, h, _stream(stream)))
 
 
 def align(index: Index, reads: Reads, params: Params, read_index_base: int, result: Result, stream=None) -> None:

@@ -60,22 +60,34 @@ def family_genomes(n_genomes: int, length: int, seed: int = 1, family_size: int 
 
 def family_genomes_fast(n_genomes: int, length: int, seed: int = 1, family_size: int = 5,
                         sub_rate: float = 0.01, conserved_len: int = 5000,
-                        n_rate: float = 1e-4, n_run: int = 10) -> List[np.ndarray]:
+                        n_rate: float = 1e-4, n_run: int = 10, near_dup_every: int = 0,
+                        near_dup_sub: float = 0.0005) -> List[np.ndarray]:
     """Same family structure as family_genomes, generated with byte-sized draws
     (substitution and N-run positions drawn by count, not by a per-base test) so
     that multi-Gbp references (BASELINE config 5: 2000 x 4 Mbp) take seconds per
-    Gbp.  A different random stream from family_genomes: C2-C4 keep theirs."""
+    Gbp.  A different random stream from family_genomes: C2-C4 keep theirs.
+
+    ``near_dup_every`` = f > 0 makes every f-th family (families f-1, 2f-1, ...)
+    a family of near-duplicates: its members carry ``near_dup_sub`` substitutions
+    per base against the family base instead of ``sub_rate``.  Two members then
+    share ~(1 - 2 near_dup_sub)^k of their k-mers (0.97 at k = 31 and 0.05 %),
+    above the EXTSIM threshold 0.95, so the similarity filter
+    (src/kmer.py:188-263) keeps one member of such a family and drops the rest;
+    members of the other families (1 % apart: ~0.54 shared) are all kept."""
     rng = np.random.Generator(np.random.PCG64(seed))
     conserved_len = int(min(conserved_len, length // 2))
     conserved = ACGT[rng.integers(0, 4, size=conserved_len, dtype=np.uint8)] if conserved_len > 0 else None
     out: List[np.ndarray] = []
     base = None
+    fam = max(family_size, 1)
     for g in range(n_genomes):
-        if g % max(family_size, 1) == 0:
+        if g % fam == 0:
             base = rng.integers(0, 4, size=length, dtype=np.uint8)
+        f = g // fam
+        rate = near_dup_sub if (near_dup_every > 0 and f % near_dup_every == near_dup_every - 1) else sub_rate
         codes = base.copy()
-        if sub_rate > 0:
-            hit = rng.integers(0, length, size=int(rng.binomial(length, sub_rate)))
+        if rate > 0:
+            hit = rng.integers(0, length, size=int(rng.binomial(length, rate)))
             codes[hit] = (codes[hit] + rng.integers(1, 4, size=hit.size, dtype=np.uint8)) & 3
         seq = ACGT[codes]
         if conserved is not None:

@@ -17,6 +17,12 @@
  *                            genomes_mapped_to (PseudoAlignment.reads)      src/kmer.py:542, 551-561
  *   pa_result_fetch          PseudoAlignment.get_summary inputs             src/kmer.py:622-657
  *   pa_align_batch           one-shot host-buffer form of pa_align
+ *   pa_counters_reduce       the multi-GPU sum/min of PseudoAlignment counters
+ *                            (read shards of one job); the
+ *                            reference is single-process, so this has no
+ *                            reference counterpart: it makes N per-rank
+ *                            get_summary inputs equal to the one-process ones
+ *                            src/kmer.py:622-657
  *   pa_parse_file/_text      FASTAFile / FASTAQFile -> FASTARecordContainer /
  *                            FASTAQRecordContainer.parse_records (host
  *                            threads, canonical subset of the grammar)     src/data_file.py:117-158,
@@ -73,6 +79,11 @@ typedef int32_t pa_status;
 #define PA_HAS_MAX_GENOMES 4u
 
 #define PA_NO_FIRST_KEY INT64_MAX  /* first_key of a genome never counted; all keys are < 2^63 */
+/* first_key = (global read index << 20) | position in that read's
+ * genomes_mapped_to list (<= G: a p-demoted list holds G* twice), so an index
+ * holds at most PA_MAX_GENOMES genomes (pa_index_build: PA_EUNSUPPORTED above)
+ * and read indices stay below 2^43. */
+#define PA_MAX_GENOMES ((1u << 20) - 1)
 
 typedef struct pa_index pa_index;
 typedef struct pa_reads pa_reads;
@@ -185,6 +196,24 @@ pa_status pa_align_detail(const pa_index *idx, const pa_reads *reads, const pa_p
 pa_status pa_align_batch(const pa_index *idx, const uint8_t *seq, const uint8_t *qual, const uint64_t *read_off,
                          uint64_t n_reads, uint64_t read_index_base, const pa_params *params, pa_stats *stats,
                          uint64_t *unique_reads, uint64_t *ambiguous_reads, uint64_t *first_key, void *stream);
+
+/* ---- multi-GPU reduce (RCCL over xGMI) ------------------------------------------- */
+
+/* One process per GPU, each aligning its own read shard with GLOBAL read
+ * indices (read_index_base), then ONE in-place all-reduce of every rank's
+ * pa_result: the sum block with ncclSum, the first-key block with ncclMin
+ * (uint64).  Afterwards every rank's pa_result holds the job's counters, and
+ * pa_result_fetch gives exactly what one process aligning all reads would
+ * (Summary key order included).  RCCL is opened at the first call
+ * (PA_RCCL_LIBRARY or librccl.so.1); PA_EUNSUPPORTED if it cannot be.
+ * `comm` is an ncclComm_t -- from pa_comm_init, or any RCCL communicator of
+ * the job's ranks (e.g. the one a framework already made).  Stream-ordered on
+ * `stream`; collective: every rank must call it. */
+#define PA_COMM_ID_BYTES 128
+pa_status pa_comm_unique_id(uint8_t *id /* [PA_COMM_ID_BYTES], rank 0; share it with the others */);
+pa_status pa_comm_init(int32_t device, int32_t nranks, int32_t rank, const uint8_t *id, void **comm);
+pa_status pa_comm_free(void *comm);
+pa_status pa_counters_reduce(pa_result *res, void *comm, void *stream);
 
 /* ---- profiling ------------------------------------------------------------------ */
 

@@ -38,7 +38,7 @@ def build(force: bool = False) -> str:
     """Compile the restatement with gcc into oracle/_build/ (gitignored)."""
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        subprocess.check_call(["gcc", "-O2", "-std=c11", "-shared", "-fPIC", "-o", LIB, SRC])
+        subprocess.check_call(["gcc", "-O2", "-std=c11", "-shared", "-fPIC", "-pthread", "-o", LIB, SRC])
     return LIB
 
 
@@ -53,6 +53,8 @@ def lib():
         L = ctypes.CDLL(LIB)
         L.ora_index_build.restype = P
         L.ora_index_build.argtypes = [ctypes.c_char_p, P, ctypes.c_uint32, ctypes.c_int64]
+        L.ora_index_build_mt.restype = P
+        L.ora_index_build_mt.argtypes = [ctypes.c_char_p, P, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int]
         L.ora_index_free.argtypes = [P]
         L.ora_index_n_kmers.restype = U64
         L.ora_index_n_kmers.argtypes = [P]
@@ -97,6 +99,16 @@ class AlignResult:
         return [int(x) for x in self.lists[self.list_off[r]:self.list_off[r + 1]]]
 
 
+def host_threads() -> int:
+    """Host threads this job may use: OMP_NUM_THREADS (the GPU box's CPU share)
+    capped by the affinity mask, at most 16."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, min(n, 16))
+
+
 def pack_params(m=1, p=1, mrq=None, mkq=None, mg=None):
     flags = (HAS_MRQ if mrq is not None else 0) | (HAS_MKQ if mkq is not None else 0) | (HAS_MG if mg is not None else 0)
     return int(m), int(p), int(mrq or 0), int(mkq or 0), int(mg or 0), flags
@@ -105,12 +117,16 @@ def pack_params(m=1, p=1, mrq=None, mkq=None, mg=None):
 class OracleIndex:
     """CPU k-mer index: genomes in FASTA order, k-mers with 'N' skipped."""
 
-    def __init__(self, genomes: Sequence, k: int):
+    def __init__(self, genomes: Sequence, k: int, threads: Optional[int] = None):
+        """``threads`` host threads build it (default: this job's CPU share, at
+        most 16); the index -- every k-mer's genome list included -- does not
+        depend on the thread count."""
         self.k = int(k)
         text, off = concat(genomes)
         self.n_genomes = len(off) - 1
         self._off = off
-        self._h = lib().ora_index_build(text, _ptr(off), self.n_genomes, self.k)
+        self._h = lib().ora_index_build_mt(text, _ptr(off), self.n_genomes, self.k,
+                                           int(threads if threads else host_threads()))
         if not self._h:
             raise MemoryError("oracle index build failed")
 

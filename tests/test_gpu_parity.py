@@ -440,15 +440,9 @@ def test_large_reference_layout(monkeypatch):
     as the oracle, the lane kernel on."""
     gens, s, q, off = _synthetic_case(20, 30000, 5, 0.01, 31, 8000, 150, 0.01, seed=4242)
     oix = O.OracleIndex(gens, 31)
-    monkeypatch.setenv("PA_CAP_HLL", "1")
-    monkeypatch.setenv("PA_TPOS_LOCAL", "1")
-    monkeypatch.setenv("PA_NB_HALF", "1")  # the 12-B neighbour bits (present only)
-    monkeypatch.setenv("PA_BLOOM_MB", "0")  # no Bloom filter (too many keys for the cache)
+    monkeypatch.setenv("PA_LAYOUT", "large")  # every choice the build makes for an 8 Gbp reference
     index = N.Index(gens, 31)
-    monkeypatch.delenv("PA_CAP_HLL")
-    monkeypatch.delenv("PA_TPOS_LOCAL")
-    monkeypatch.delenv("PA_NB_HALF")
-    monkeypatch.delenv("PA_BLOOM_MB")
+    monkeypatch.delenv("PA_LAYOUT")
     info = index.info()
     assert index.n_kmers == oix.n_kmers
     assert info.table_slots < 2 * index.n_kmers  # sized on the estimate (default: 4 x windows)

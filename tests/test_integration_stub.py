@@ -1,0 +1,89 @@
+"""The reference-side ctypes stub of INTEGRATION.md section 2, as written.
+
+A maintainer keeping the reference's own classes would paste that stub into
+the reference (src/pa_gpu.py) and call pa_index_build + pa_align_batch.  This
+test extracts the stub's code block from INTEGRATION.md verbatim (only the
+library path is filled in), runs it with nothing from this package's Python
+layer (no pa_native, no kmer), and rebuilds get_summary (src/kmer.py:622-657)
+from its outputs the way INTEGRATION.md describes: it must print exactly the
+reference CLI's stdout for BASELINE config 1 (tests/golden/config1_cli.json).
+The ABI checks (CPU) make sure the stub's symbols and struct sizes match
+include/pa.h; the run itself needs the GPU.
+"""
+
+import ctypes
+import json
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "bioinformatics-project-for-shotgun-metagenomics-pseudo-alignment-shotgun-_amd", "libpa.so")
+GOLD = os.path.join(REPO, "tests", "golden")
+
+
+def _stub_namespace():
+    with open(os.path.join(REPO, "INTEGRATION.md")) as f:
+        text = f.read()
+    m = re.search(r"```python\n(# src/pa_gpu\.py.*?)```", text, re.S)
+    assert m, "INTEGRATION.md section 2 stub not found"
+    code = m.group(1).replace('"/path/to/libpa.so"', repr(LIB))
+    ns = {}
+    exec(compile(code, "INTEGRATION.md:pa_gpu.py", "exec"), ns)
+    return ns
+
+
+def _fasta(path):
+    names, seqs = [], []
+    for line in open(path).read().splitlines():
+        if line.startswith(">"):
+            names.append(line[1:].strip())
+            seqs.append([])
+        elif line.strip():
+            seqs[-1].append(line.strip())
+    return names, ["".join(s) for s in seqs]
+
+
+def _fastq(path):
+    lines = open(path).read().splitlines()
+    return [lines[i + 1] for i in range(0, len(lines), 4)], [lines[i + 3] for i in range(0, len(lines), 4)]
+
+
+def test_stub_matches_the_abi():
+    """The stub's declarations agree with include/pa.h (no device needed)."""
+    ns = _stub_namespace()
+    assert ctypes.sizeof(ns["_Params"]) == 48 and ctypes.sizeof(ns["_Stats"]) == 48
+    with open(os.path.join(REPO, "include", "pa.h")) as f:
+        header = f.read()
+    for sym in ("pa_index_build", "pa_align_batch", "pa_last_error"):
+        assert re.search(r"\b" + sym + r"\(", header), sym
+        assert getattr(ns["_L"], sym) is not None
+
+
+@pytest.mark.gpu
+def test_stub_reproduces_config1_cli():
+    ns = _stub_namespace()
+    names, genomes = _fasta(os.path.join(GOLD, "config1.fa"))
+    seqs, quals = _fastq(os.path.join(GOLD, "config1.fq"))
+    index = ns["build_index"](genomes, 21)
+    with open(os.path.join(GOLD, "config1_cli.json")) as f:
+        cases = json.load(f)
+    for case in cases[:4]:  # [], -m 0 -p 0 (CLI-coerced to 1), -m 2 -p 3, -p -1
+        flags = case["flags"]
+        m = int(flags[flags.index("-m") + 1]) if "-m" in flags else 1
+        p = int(flags[flags.index("-p") + 1]) if "-p" in flags else 1
+        m, p = (m or 1), (p or 1)  # src/main.py:337-342
+        st, uniq, amb, first = ns["align"](index, len(genomes), seqs, quals, m=m, p=p)
+        stats = {"unique_mapped_reads": st.unique, "ambiguous_mapped_reads": st.ambiguous,
+                 "unmapped_reads": st.unmapped}
+        summary, order = {}, {}
+        for g in range(len(genomes)):
+            if int(first[g]) == 2 ** 63 - 1:
+                continue
+            e = summary.setdefault(names[g], {"unique_reads": 0, "ambiguous_reads": 0})
+            e["unique_reads"] += int(uniq[g])
+            e["ambiguous_reads"] += int(amb[g])
+            order[names[g]] = min(order.get(names[g], 2 ** 63), int(first[g]))
+        out = {"Statistics": stats, "Summary": {n: summary[n] for n in sorted(order, key=order.get)}}
+        assert json.dumps(out, indent=4) + "\n" == case["stdout"], flags
