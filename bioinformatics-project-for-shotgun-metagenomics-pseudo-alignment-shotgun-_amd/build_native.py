@@ -81,6 +81,19 @@ def build(force: bool = False, verbose: bool = False, stats: bool = False, varia
     return lib
 
 
+def build_tools(force: bool = False) -> str:
+    """Measurement tools (not part of libpa.so): profiles/fetch_calib, the
+    FETCH_SIZE calibration of the align kernels' access shapes."""
+    src = os.path.join(os.path.dirname(HERE), "profiles", "fetch_calib.hip")
+    exe = os.path.splitext(src)[0]
+    if force or _stale(exe, [src]):
+        r = subprocess.run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-o", exe, src],
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{r.stdout}")
+    return exe
+
+
 if __name__ == "__main__":
     var = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--variant=")]
     defs = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--define=")]

@@ -239,15 +239,19 @@ pa_status pa_reads_upload(int32_t device, const uint8_t *seq, const uint8_t *qua
     return PA_OK;
 }
 
-pa_status pa_reads_synthesize(const pa_index *idx, uint64_t n_reads, uint32_t read_len, uint64_t first_read,
-                              uint64_t seed, double sub_rate, void *stream, pa_reads **out) {
+pa_status pa_reads_synthesize_mix(const pa_index *idx, uint64_t n_reads, uint32_t read_len, uint64_t first_read,
+                                  uint64_t seed, double sub_rate, double rc_rate, double foreign_rate, void *stream,
+                                  pa_reads **out) {
     PA_CHECK(idx && out, PA_EINVAL, "NULL argument");
     *out = nullptr;
     PA_CHECK(read_len > 0, PA_EINVAL, "read_len must be positive");
+    PA_CHECK(rc_rate >= 0 && foreign_rate >= 0 && rc_rate + foreign_rate <= 1, PA_EINVAL,
+             "rc_rate and foreign_rate must be >= 0 with a sum <= 1");
     PA_HIP(hipSetDevice(idx->device));
     pa_reads *r = new (std::nothrow) pa_reads();
     PA_CHECK(r != nullptr, PA_ENOMEM, "out of host memory");
-    pa_status rc = pa::reads_synthesize(idx, r, n_reads, read_len, first_read, seed, sub_rate, as_stream(stream));
+    pa_status rc = pa::reads_synthesize(idx, r, n_reads, read_len, first_read, seed, sub_rate, rc_rate, foreign_rate,
+                                        as_stream(stream));
     if (rc != PA_OK) {
         hipFree(r->seq); hipFree(r->qual); hipFree(r->off);
         delete r;
@@ -255,6 +259,11 @@ pa_status pa_reads_synthesize(const pa_index *idx, uint64_t n_reads, uint32_t re
     }
     *out = r;
     return PA_OK;
+}
+
+pa_status pa_reads_synthesize(const pa_index *idx, uint64_t n_reads, uint32_t read_len, uint64_t first_read,
+                              uint64_t seed, double sub_rate, void *stream, pa_reads **out) {
+    return pa_reads_synthesize_mix(idx, n_reads, read_len, first_read, seed, sub_rate, 0.0, 0.0, stream, out);
 }
 
 pa_status pa_reads_info(const pa_reads *reads, uint64_t *n_reads, uint64_t *n_bases, uint32_t *max_len) {

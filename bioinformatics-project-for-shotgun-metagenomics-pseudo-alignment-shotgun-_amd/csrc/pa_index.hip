@@ -633,10 +633,16 @@ __device__ __forceinline__ uint64_t rng(uint64_t seed, uint64_t a, uint64_t b) {
     return fmix64(seed * 0xD1B54A32D192ED03ull ^ fmix64(a * 0x9E3779B97F4A7C15ull + b));
 }
 
+// Read r = global read first + r: a genome (uniform over those >= len), a start
+// (uniform), forward strand -- or, with rc_thresh / foreign_thresh > 0 (the
+// robustness workload), the reverse complement of that stretch (the reference
+// looks up forward k-mers only, src/kmer.py:423: such reads mostly go
+// unmapped) or uniform random bases (an organism absent from the index);
+// substitutions at sub_thresh / 2^24 per base; raw-ASCII qualities.
 __global__ void k_synth_reads(const uint8_t *__restrict__ codes, const uint64_t *__restrict__ goff,
                               const uint32_t *__restrict__ eligible, uint32_t n_eligible, uint64_t n_reads,
-                              uint32_t len, uint64_t first, uint64_t seed, uint32_t sub_thresh, uint8_t *seq,
-                              uint8_t *qual, uint64_t *off) {
+                              uint32_t len, uint64_t first, uint64_t seed, uint32_t sub_thresh, uint32_t rc_thresh,
+                              uint32_t foreign_thresh, uint8_t *seq, uint8_t *qual, uint64_t *off) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t total = n_reads * len;
@@ -649,9 +655,16 @@ __global__ void k_synth_reads(const uint8_t *__restrict__ codes, const uint64_t 
         uint32_t g = eligible[(uint32_t)((h0 >> 32) * n_eligible >> 32)];
         uint64_t glen = goff[g + 1] - goff[g];
         uint64_t start = __umul64hi(rng(seed, gr, 0xFFFFFFFEull), glen - len + 1);
-        uint32_t c = codes[goff[g] + start + j];
+        uint32_t kind = 0;  // 0 forward, 1 reverse complement, 2 foreign
+        if (rc_thresh | foreign_thresh) {
+            const uint32_t u = (uint32_t)(rng(seed, gr, 0xFFFFFFFDull) >> 40);
+            kind = u < foreign_thresh ? 2u : (u < foreign_thresh + rc_thresh ? 1u : 0u);
+        }
         uint64_t h = rng(seed, gr, j);
+        uint32_t c = kind == 0 ? codes[goff[g] + start + j] : kind == 1 ? codes[goff[g] + start + (len - 1 - j)] : 0u;
         if (c > 3) c = (uint32_t)(h & 3);                       // N in the genome -> random base
+        if (kind == 1) c = 3u - c;                              // complement (A-T, C-G)
+        if (kind == 2) c = (uint32_t)(rng(seed, gr, j + 0x200000000ull) & 3);
         if ((uint32_t)(h >> 40) < sub_thresh) c = (c + 1 + (uint32_t)((h >> 8) % 3)) & 3;  // substitution
         // raw-ASCII quality: clipped normal(60, 8) via an Irwin-Hall sum of four uniforms
         float u = (float)((h >> 2) & 0xFFF) + (float)((h >> 14) & 0xFFF) + (float)((h >> 26) & 0xFFF) +
@@ -1183,7 +1196,7 @@ pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint
 }
 
 pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_t len, uint64_t first,
-                           uint64_t seed, double sub_rate, hipStream_t st) {
+                           uint64_t seed, double sub_rate, double rc_rate, double foreign_rate, hipStream_t st) {
     std::vector<uint32_t> elig;
     for (uint32_t g = 0; g < idx->n_genomes; g++)
         if (idx->h_goff[g + 1] - idx->h_goff[g] >= len) elig.push_back(g);
@@ -1204,11 +1217,13 @@ pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_
     if (n == 0 || len == 0) {
         PA_HIP(hipMemsetAsync(r->off, 0, (n + 1) * 8, st));
     } else {
-        double t = sub_rate < 0 ? 0 : (sub_rate > 1 ? 1 : sub_rate);
-        uint32_t thresh = (uint32_t)std::min(16777215.0, t * 16777216.0);
+        auto th = [](double x) {
+            const double t = x < 0 ? 0 : (x > 1 ? 1 : x);
+            return (uint32_t)std::min(16777215.0, t * 16777216.0);
+        };
         hipLaunchKernelGGL(k_synth_reads, dim3(grid_for(r->n_bases) > 65536 ? 65536 : grid_for(r->n_bases)),
                            dim3(kBlock), 0, st, idx->codes, idx->goff, d_elig, (uint32_t)elig.size(), n, len, first,
-                           seed, thresh, r->seq, r->qual, r->off);
+                           seed, th(sub_rate), th(rc_rate), th(foreign_rate), r->seq, r->qual, r->off);
     }
     PA_HIP(hipGetLastError());
     PA_HIP(hipStreamSynchronize(st));

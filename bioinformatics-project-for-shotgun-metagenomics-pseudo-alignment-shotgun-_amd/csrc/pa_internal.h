@@ -133,7 +133,7 @@ pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint3
 pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint32_t n_groups, uint64_t *total,
                              uint64_t *uniq, uint64_t *inter, hipStream_t st);
 pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_t len, uint64_t first,
-                           uint64_t seed, double sub_rate, hipStream_t st);
+                           uint64_t seed, double sub_rate, double rc_rate, double foreign_rate, hipStream_t st);
 pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t base, pa_result *acc,
                 hipStream_t st);
 pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uint8_t *type, uint32_t *qf,

@@ -29,7 +29,7 @@ EXPORTS = (
     "pa_last_error", "pa_version", "pa_device_count",
     "pa_index_build", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
     "pa_index_extsim_stats",
-    "pa_reads_upload", "pa_reads_synthesize", "pa_reads_info", "pa_reads_download", "pa_reads_free",
+    "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_reads_download", "pa_reads_free",
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
     "pa_result_copy_in", "pa_result_free",
     "pa_align", "pa_align_detail", "pa_align_batch",
@@ -109,6 +109,8 @@ def lib():
         "pa_index_extsim_stats": (I32, [P, P, U32, P, P, P, P]),
         "pa_reads_upload": (I32, [I32, P, P, P, U64, P, PP]),
         "pa_reads_synthesize": (I32, [P, U64, U32, U64, U64, ctypes.c_double, P, PP]),
+        "pa_reads_synthesize_mix": (I32, [P, U64, U32, U64, U64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                          P, PP]),
         "pa_reads_info": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U32)]),
         "pa_reads_download": (I32, [P, U64, U64, P, P, P, P]),
         "pa_reads_free": (None, [P]),
@@ -404,10 +406,14 @@ class Reads:
 
     @classmethod
     def synthesize(cls, index: Index, n_reads: int, read_len: int, first_read: int = 0, seed: int = 2,
-                   sub_rate: float = 0.005, stream=None) -> "Reads":
+                   sub_rate: float = 0.005, stream=None, rc_rate: float = 0.0, foreign_rate: float = 0.0) -> "Reads":
         h = P()
-        _check(lib().pa_reads_synthesize(index.handle, n_reads, read_len, first_read, seed, sub_rate, _stream(stream),
-                                         ctypes.byref(h)))
+        if rc_rate or foreign_rate:
+            _check(lib().pa_reads_synthesize_mix(index.handle, n_reads, read_len, first_read, seed, sub_rate, rc_rate,
+                                                 foreign_rate, _stream(stream), ctypes.byref(h)))
+        else:
+            _check(lib().pa_reads_synthesize(index.handle, n_reads, read_len, first_read, seed, sub_rate,
+                                             _stream(stream), ctypes.byref(h)))
         return cls(h, index.device)
 
     def download(self, first: int = 0, count: Optional[int] = None):

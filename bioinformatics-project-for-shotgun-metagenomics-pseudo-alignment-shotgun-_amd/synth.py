@@ -61,7 +61,7 @@ def family_genomes(n_genomes: int, length: int, seed: int = 1, family_size: int 
 def family_genomes_fast(n_genomes: int, length: int, seed: int = 1, family_size: int = 5,
                         sub_rate: float = 0.01, conserved_len: int = 5000,
                         n_rate: float = 1e-4, n_run: int = 10, near_dup_every: int = 0,
-                        near_dup_sub: float = 0.0005) -> List[np.ndarray]:
+                        near_dup_sub: float = 0.0003) -> List[np.ndarray]:
     """Same family structure as family_genomes, generated with byte-sized draws
     (substitution and N-run positions drawn by count, not by a per-base test) so
     that multi-Gbp references (BASELINE config 5: 2000 x 4 Mbp) take seconds per
@@ -70,7 +70,7 @@ def family_genomes_fast(n_genomes: int, length: int, seed: int = 1, family_size:
     ``near_dup_every`` = f > 0 makes every f-th family (families f-1, 2f-1, ...)
     a family of near-duplicates: its members carry ``near_dup_sub`` substitutions
     per base against the family base instead of ``sub_rate``.  Two members then
-    share ~(1 - 2 near_dup_sub)^k of their k-mers (0.97 at k = 31 and 0.05 %),
+    share ~(1 - 2 near_dup_sub)^k of their k-mers (0.98 at k = 31 and 0.03 %),
     above the EXTSIM threshold 0.95, so the similarity filter
     (src/kmer.py:188-263) keeps one member of such a family and drops the rest;
     members of the other families (1 % apart: ~0.54 shared) are all kept."""

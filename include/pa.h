@@ -157,6 +157,13 @@ pa_status pa_reads_upload(int32_t device, const uint8_t *seq, const uint8_t *qua
  * index's genomes (read i = global read first_read + i; deterministic in seed). */
 pa_status pa_reads_synthesize(const pa_index *idx, uint64_t n_reads, uint32_t read_len, uint64_t first_read,
                               uint64_t seed, double sub_rate, void *stream, pa_reads **out);
+/* The same with a share of reverse-complemented reads (rc_rate: the reference
+ * looks up forward k-mers only, so these mostly go unmapped) and of reads of
+ * uniform random bases (foreign_rate: an organism absent from the index); the
+ * rest forward.  rc_rate + foreign_rate <= 1.  (The robustness workload.) */
+pa_status pa_reads_synthesize_mix(const pa_index *idx, uint64_t n_reads, uint32_t read_len, uint64_t first_read,
+                                  uint64_t seed, double sub_rate, double rc_rate, double foreign_rate, void *stream,
+                                  pa_reads **out);
 pa_status pa_reads_info(const pa_reads *reads, uint64_t *n_reads, uint64_t *n_bases, uint32_t *max_len);
 /* copy reads [first, first+count) back to the host (seq/qual: n_bases of that range) */
 pa_status pa_reads_download(const pa_reads *reads, uint64_t first, uint64_t count, uint8_t *seq, uint8_t *qual,
