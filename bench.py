@@ -353,20 +353,6 @@ def main():
     kern_s = kern_ms / max(launches, 1) / 1e3
     b_read = bytes_per_read(cfg)
     achieved = b_read * npg / kern_s / 1e9 if kern_s > 0 else 0.0
-    traffic = measured_frac = lines_per_read = line_frac = per = None
-    line_peak, line_src = random_line_roofline()
-    if rank == 0 and world == 1 and not args.no_traffic:
-        per, tnote = traffic_pass(args, cfg, kept_path)
-        if per is not None:
-            traffic = sum(per.values())
-            measured_frac = traffic / kern_s / 1e9 / HBM_PEAK_GBS if kern_s > 0 else None
-            line_frac = traffic / kern_s / 1e9 / line_peak if (kern_s > 0 and line_peak) else None
-            lines_per_read = traffic / 128.0 / npg
-            log(f"[rank 0] traffic: {traffic / 1e9:.2f} GB per pass ({lines_per_read:.1f} 128-B lines/read)")
-    else:
-        tnote = "not measured (--no-traffic, or a rank of a multi-GPU run)"
-    if kept_path:
-        os.unlink(kept_path)
     out = {
         "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -379,11 +365,8 @@ def main():
                    "read_mix": {"reverse_complement": cfg.get("rc_rate", 0.0), "foreign": cfg.get("foreign_rate", 0.0),
                                 "substitution_rate": cfg["read_err"]}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "achieved_basis": "algorithmic bytes (SURVEY.md 8d: L + q*L + 16*(L-k+1) per read)",
-                     "measured_frac": measured_frac, "lines_per_read": lines_per_read,
-                     "traffic_by_kernel": per, "traffic_basis": tnote,
-                     "random_line_frac": line_frac, "random_line_peak": line_peak, "random_line_peak_source": line_src,
                      "kernel": "align pass: k_align_lane + k_align_fast", "kernel_ms": kern_s * 1e3, "bytes_per_read": b_read},
         "deferred_read_fraction": deferred / max(npg * args.steps, 1),
         "index": {"build_s": build_s, "n_kmers": int(info.n_kmers), "multi_genome_sets": int(info.n_multi_classes),
@@ -401,6 +384,30 @@ def main():
         base, parity = cpu_baseline(cfg, genomes, index, reads, pk, args.cpu_seconds)
         out["cpu_baseline"] = base
         out["parity_sample"] = parity
+    # the traffic pass last, after this process's device memory is released:
+    # its child rebuilds the same index and reads (C5's would not fit twice)
+    traffic = measured_frac = lines_per_read = line_frac = per = None
+    line_peak, line_src = random_line_roofline()
+    if rank == 0 and world == 1 and not args.no_traffic:
+        result.close()
+        reads.close()
+        index.close()
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        per, tnote = traffic_pass(args, cfg, kept_path)
+        if per is not None:
+            traffic = sum(per.values())
+            measured_frac = traffic / kern_s / 1e9 / HBM_PEAK_GBS if kern_s > 0 else None
+            line_frac = traffic / kern_s / 1e9 / line_peak if (kern_s > 0 and line_peak) else None
+            lines_per_read = traffic / 128.0 / npg
+            log(f"[rank 0] traffic: {traffic / 1e9:.2f} GB per pass ({lines_per_read:.1f} 128-B lines/read)")
+    else:
+        tnote = "not measured (--no-traffic, or a rank of a multi-GPU run)"
+    if kept_path:
+        os.unlink(kept_path)
+    out["roofline"].update({"traffic": traffic, "measured_frac": measured_frac, "lines_per_read": lines_per_read,
+                            "traffic_by_kernel": per, "traffic_basis": tnote, "random_line_frac": line_frac,
+                            "random_line_peak": line_peak, "random_line_peak_source": line_src})
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -65,10 +65,12 @@ struct AlignArgs {
     const uint64_t *tile_pk;
     uint64_t tile_n;
     const uint64_t *goff;           // genome start positions [G + 1] (concatenated coordinates)
-    const uint64_t *tile_fl;        // lane kernel flag planes (pairs per 64 positions)
+    const uint64_t *tile_lw;        // lane kernel walk blocks (2-bit words + flag planes per 64 positions)
     const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
     const void *tile_nb;            // one-substitution neighbour bits (null: none)
     int nb_spec;                    //   1: 64-bit present | specific << 32, 0: 32-bit present
+    const uint32_t *tile_nbbig;     // --max-genomes >= 2: neighbour present with a set > mg (k_nb_big; null: none)
+    int mg_nb;                      // --max-genomes: the neighbour bits tell every present neighbour's set vs mg
     const uint32_t *gblk;           // the genome holding position j << 16 (tiled indexes)
     const uint64_t *bloom;          // Bloom filter of the keys (null: none), 2^bloom_lg words
     uint32_t bloom_lg;
@@ -146,6 +148,39 @@ __global__ __launch_bounds__(256) void k_tile_big(const uint32_t *__restrict__ t
     }
 }
 
+
+// The neighbour bits' "set size > mg" half for one --max-genomes value mg >= 2
+// (cached in the index like tile_big): bit i of nbbig[3 p + b] is set when the
+// one-substitution neighbour of tile_nb's word 3 p + b, bit i, is present with
+// more than mg genomes.  Only present, multi-genome neighbours are probed --
+// one thread per word, most words are zero.
+__global__ __launch_bounds__(256) void k_nb_big(const uint64_t *__restrict__ pk, const uint64_t *__restrict__ nb,
+                                                uint64_t n_words, int k, const Slot<1> *__restrict__ table, HomeCfg hc,
+                                                uint32_t G, const uint32_t *__restrict__ class_genomes, int32_t mg,
+                                                uint32_t *__restrict__ nbbig) {
+    const int sh = 64 - 2 * k;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_words; i += stride) {
+        const uint64_t v = nb[i];
+        uint32_t cand = (uint32_t)v & ~(uint32_t)(v >> 32);  // present, not specific (size 1 <= mg)
+        uint32_t big = 0;
+        const uint64_t p = i / 3;
+        const uint32_t b = (uint32_t)(i - 3 * p);
+        while (cand) {
+            const uint32_t q = __builtin_ctz(cand);
+            cand &= cand - 1;
+            const uint64_t w = p - (uint64_t)(k - 1) + q;  // the window (bit q of the word)
+            const uint64_t K = get64_at(pk, 2 * w) >> sh;
+            const int bs = 2 * (k - 1 - (int)(p - w));
+            const uint64_t cj = (K >> bs) & 3;
+            uint64_t key[1] = {K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs)};
+            uint32_t cls[1];
+            if (probe_lines<1>(table, hc, key, cls) && (int64_t)class_size_of(cls[0], G, class_genomes) > (int64_t)mg)
+                big |= 1u << q;
+        }
+        nbbig[i] = big;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // exact kernel (one workgroup per read, dense per-genome scratch)
@@ -592,7 +627,7 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_cls = idx->tile_cls;
     a.tile_pk = idx->tile_pk;
     a.goff = idx->goff;
-    a.tile_fl = idx->tile_cls ? idx->tile_fl : nullptr;
+    a.tile_lw = idx->tile_cls ? idx->tile_lw : nullptr;
     a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
     a.nb_spec = idx->nb_spec;
     a.gblk = idx->tile_gblk;
@@ -697,7 +732,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
     const bool fast_ok = idx->k > 0 && idx->nw <= 2 && idx->n_kmers > 0;
     // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
     const char *no_lane = std::getenv("PA_NO_LANE");
-    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile_fl && !(no_lane && no_lane[0] == '1');
+    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile_lw && !(no_lane && no_lane[0] == '1');
     if (fast_ok) {
         const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
         const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4
@@ -719,7 +754,33 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
                     idx->tile_big_mg = a.prm.mg;
                 }
                 a.tile_big = idx->tile_big;
+                // the neighbour bits' set-size half for this mg (12 B per base;
+                // only with the 24-B neighbour bits, and when it fits)
+                if (idx->tile_nb && idx->nb_spec && !std::getenv("PA_NO_NBBIG")) {
+                    const uint64_t nw = 3 * a.tile_n;
+                    if (!idx->tile_nbbig) {
+                        size_t free_b = 0, total_b = 0;
+                        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && nw * 4 + (8ull << 30) < free_b &&
+                            hipMalloc(&idx->tile_nbbig, nw * 4 + 64) == hipSuccess)
+                            idx->tile_nbbig_mg = -1;
+                        else
+                            idx->tile_nbbig = nullptr;
+                        (void)hipGetLastError();
+                    }
+                    if (idx->tile_nbbig && idx->tile_nbbig_mg != a.prm.mg) {
+                        hipLaunchKernelGGL(k_nb_big, dim3((unsigned)std::min<uint64_t>((nw + 255) / 256, 1u << 20)),
+                                           dim3(256), 0, st, idx->tile_pk, (const uint64_t *)idx->tile_nb, nw, (int)idx->k,
+                                           (const Slot<1> *)idx->table, idx->home, a.G, idx->class_genomes,
+                                           (int32_t)a.prm.mg, idx->tile_nbbig);
+                        PA_HIP(hipGetLastError());
+                        idx->tile_nbbig_mg = a.prm.mg;
+                    }
+                    a.tile_nbbig = idx->tile_nbbig;
+                }
             }
+            // every present neighbour's set size vs mg known from the bits
+            a.mg_nb = (a.prm.flags & F_MG) && a.tile_nb && a.nb_spec && (a.prm.mg < 2 || a.tile_nbbig) &&
+                      !std::getenv("PA_NO_MGNB");
             a.queue_hard = idx->queue_hard;
             a.queue_hard_count = (unsigned long long *)idx->counters + 3;
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));

@@ -532,25 +532,30 @@ __global__ void k_bloom_build(const Slot<1> *__restrict__ table, uint64_t cap, u
     }
 }
 
-// Flag planes of the lane walk (pa_lane.h): per 64 positions a word pair
-// (A, B), bit i <-> position 64 j + i: (0,0) no indexed window, (1,0) a
-// multi-genome k-mer, (1,1) a specific one, (0,1) a k-mer that repeats within
-// 127 positions (PA_TILE_REP).  0.25 B per base: the 120 windows of a read
-// are one or two 64-B lines, where a 2-byte entry per position would be four or five.
-// One wave per word pair, the planes by ballot.
-__global__ __launch_bounds__(256) void k_tile_planes(const uint32_t *__restrict__ tile_cls, uint64_t n, uint32_t G,
-                                                     uint64_t *__restrict__ fl, uint64_t n_pairs) {
+// The lane walk's view of the genomes (pa_lane.h), one 32-B block per 64
+// positions j: {2-bit words 2j and 2j+1 of tile_pk (positions 64 j .. 64 j +
+// 63), flag plane A, flag plane B}, bit i of a plane <-> position 64 j + i:
+// (A,B) = (0,0) no indexed window, (1,0) a multi-genome k-mer, (1,1) a
+// specific one, (0,1) a k-mer that repeats within 127 positions (PA_TILE_REP).
+// A read's walk needs the bases of [A, A + 150) and the flags of its 120
+// windows: 3 or 4 consecutive blocks, 96-128 B -- on gfx950, where every miss
+// is a 128-B request, 1.6 lines on average, against 2.6 for the separate
+// 2-bit string and plane arrays.  One wave per block, the planes by ballot.
+__global__ __launch_bounds__(256) void k_tile_walk(const uint32_t *__restrict__ tile_cls, const uint64_t *__restrict__ pk,
+                                                   uint64_t n, uint32_t G, uint64_t *__restrict__ lw, uint64_t n_blocks) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n_pairs; j += nw) {
+    for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n_blocks; j += nw) {
         const uint64_t t = 64 * j + lane;
         const uint32_t v = t < n ? tile_cls[t] : NONE;
         const bool ok = v != NONE, rep = ok && (v & PA_TILE_REP);
         const bool spec = ok && !rep && (v & ~PA_TILE_REP) < G;
         const uint64_t a = __ballot(ok && !rep), b = __ballot(rep || spec);
-        if (lane == 0) {
-            fl[2 * j] = a;
-            fl[2 * j + 1] = b;
+        if (lane < 4) {
+            const uint64_t w = lane == 0 ? (64 * j < n ? pk[2 * j] : 0ull)
+                             : lane == 1 ? (64 * j + 32 < n ? pk[2 * j + 1] : 0ull)
+                             : lane == 2 ? a : b;
+            lw[4 * j + lane] = w;
         }
     }
 }
@@ -864,11 +869,11 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
                                st, idx->tile_pk, idx->tile_cls, n, k);
         if (k <= 31) {
-            const uint64_t n_pairs = n / 64 + 4;  // padded: the walk reads three pairs from any position
-            B_HIP(hipMalloc(&idx->tile_fl, n_pairs * 16));
-            hipLaunchKernelGGL(k_tile_planes, dim3((unsigned)std::min<uint64_t>((n_pairs + 3) / 4, 1u << 20)), dim3(256),
-                               0, st, idx->tile_cls, n, G, idx->tile_fl, n_pairs);
-            idx->device_bytes += n_pairs * 16;
+            const uint64_t n_blocks = n / 64 + 5;  // padded: the walk reads four blocks from any position
+            B_HIP(hipMalloc(&idx->tile_lw, n_blocks * 32));
+            hipLaunchKernelGGL(k_tile_walk, dim3((unsigned)std::min<uint64_t>((n_blocks + 3) / 4, 1u << 20)), dim3(256),
+                               0, st, idx->tile_cls, idx->tile_pk, n, G, idx->tile_lw, n_blocks);
+            idx->device_bytes += n_blocks * 32;
             // one-substitution neighbours: 24 B per base (present | specific) when
             // that leaves a quarter of the free memory, else 12 B (present only:
             // a present neighbour is then probed), else none; PA_NO_NB=1 skips
@@ -952,13 +957,16 @@ void index_release(pa_index *idx) {
     hipFree(idx->goff);
     hipFree(idx->tile_cls);
     hipFree(idx->tile_pk);
-    hipFree(idx->tile_fl);
-    idx->tile_fl = nullptr;
+    hipFree(idx->tile_lw);
+    idx->tile_lw = nullptr;
     hipFree(idx->tile_big);
     idx->tile_big = nullptr;
     idx->tile_big_mg = -1;
     hipFree(idx->tile_nb);
     idx->tile_nb = nullptr;
+    hipFree(idx->tile_nbbig);
+    idx->tile_nbbig = nullptr;
+    idx->tile_nbbig_mg = -1;
     hipFree(idx->bloom);
     idx->bloom = nullptr;
     hipFree(idx->tile_gblk);

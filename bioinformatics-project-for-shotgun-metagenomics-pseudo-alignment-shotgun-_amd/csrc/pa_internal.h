@@ -85,11 +85,13 @@ struct pa_index {
     uint64_t tile_n = 0;               // concatenated bases (0: no tiling)
     uint32_t *tile_cls = nullptr;      // [tile_n]
     uint64_t *tile_pk = nullptr;       // [tile_n / 32 + 32] MSB-first 2-bit words (padded)
-    uint64_t *tile_fl = nullptr;       // [2 (tile_n / 64 + 4)] lane-kernel flag planes (k_tile_planes)
+    uint64_t *tile_lw = nullptr;       // [4 (tile_n / 64 + 5)] lane-walk blocks: 2-bit words + flag planes (k_tile_walk)
     uint64_t *tile_big = nullptr;      // [tile_n / 64 + 4] plane "set size > tile_big_mg" (pa_align, cached)
     int64_t tile_big_mg = -1;          // the --max-genomes value tile_big was made for (-1: none)
     void *tile_nb = nullptr;           // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional:
     int nb_spec = 0;                   //   1: 64-bit words, present | specific << 32; 0: 32-bit words, present
+    uint32_t *tile_nbbig = nullptr;    // [3 tile_n] neighbour present with a set > tile_nbbig_mg (pa_align, cached)
+    int64_t tile_nbbig_mg = -1;
     uint32_t *tile_gblk = nullptr;     // [(tile_n >> 16) + 2] the genome holding position j << 16
     uint64_t *bloom = nullptr;         // [2^bloom_lg] Bloom filter of the table's keys (k_bloom_build), optional
     uint32_t bloom_lg = 0;

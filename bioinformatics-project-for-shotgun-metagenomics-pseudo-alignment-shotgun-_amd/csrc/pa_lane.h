@@ -68,6 +68,7 @@ struct __align__(16) LaneWave {
     uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
     uint32_t again_r[128];           // reads to walk again from a specific k-mer found off their walk,
     unsigned long long again_a[128]; //   and that anchor: (window << 40) | position
+    uint32_t n_hr[64], n_qf[64];     // per-lane window counters of the settled reads (kept out of VGPRs)
 };
 
 enum : int { LANE_UNIQUE = 0, LANE_AMB = 1, LANE_UNMAPPED = 2, LANE_DROP = 3, LANE_HARD = 4, LANE_WALK = 5, LANE_AGAIN = 6 };
@@ -240,16 +241,38 @@ __device__ __forceinline__ void lane_window_quality(const AlignArgs &a, const ui
     S.qf = (uint32_t)(__popcll(F0) + __popcll(F1));
 }
 
+// The walk blocks (k_tile_walk) from position A on: the 2-bit words of the
+// read's span -- gw[i] = the genome's bases from A' = A & ~31 on, word i -- and,
+// with PLANES, the flag planes of blocks A >> 6 .. +2.  Three 32-B blocks, a
+// fourth only when the read reaches into it (every load issued before any is
+// used): 1.6 128-B lines per read on average.
+template <bool PLANES>
+__device__ __forceinline__ void lane_blocks(const AlignArgs &a, uint64_t A, uint32_t len, uint64_t (&gw)[kLaneWords + 1],
+                                            uint64_t (&pa3)[3], uint64_t (&pb3)[3]) {
+    const uint64_t *lb = a.tile_lw + 4 * (A >> 6);
+    const uint32_t r0 = (uint32_t)(A & 63), o = r0 >> 5, last = r0 + len - 1;
+#pragma unroll
+    for (int i = 0; i <= kLaneWords; i++) {  // only the words holding bases of the read
+        const uint32_t w = o + (uint32_t)i;
+        gw[i] = 32 * w <= last ? lb[4 * (w >> 1) + (w & 1)] : 0ull;
+    }
+    if (PLANES) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const ulonglong2 p = *(const ulonglong2 *)(lb + 4 * i + 2);
+            pa3[i] = p.x;
+            pb3[i] = p.y;
+        }
+    }
+}
+
 // Mismatching bases between the read (LDS row, len bases) and the genome
 // string from concatenated position A on; ~0u when the read does not fit.
 __device__ __forceinline__ uint32_t lane_mismatches(const AlignArgs &a, const uint64_t *row, uint32_t len, int64_t A) {
     if (A < 0 || (uint64_t)A + len > a.tile_n) return ~0u;
-    const uint64_t gb = 2 * (uint64_t)A;
-    const uint64_t *gp = a.tile_pk + (gb >> 6);
-    const uint32_t gr = (uint32_t)(gb & 63);
-    uint64_t gw[kLaneWords + 1];
-#pragma unroll
-    for (int i = 0; i <= kLaneWords; i++) gw[i] = gp[i];
+    const uint32_t gr = (uint32_t)(2 * (uint64_t)A & 63);
+    uint64_t gw[kLaneWords + 1], u3[3];
+    lane_blocks<false>(a, (uint64_t)A, len, gw, u3, u3);
     uint32_t n = 0;
     // the read's last word holds len - 32 * qlast bases: one mask (not one per word)
     const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;
@@ -482,24 +505,13 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     const int64_t A = (int64_t)S.atp - (int64_t)S.aw;  // genome position of window 0
     const bool in_tile = A >= 0 && (uint64_t)A + W <= a.tile_n;
     const uint64_t Ac = in_tile ? (uint64_t)A : 0;
-    // every load of the walk is issued before anything waits: the genome words
-    // of the read's span (tile_pk is padded), the first 64 tile entries (as
-    // dwords from an even position), and the anchor genome's range
-    const uint64_t gb = 2 * Ac;
-    const uint64_t *gp = a.tile_pk + (gb >> 6);
-    const uint32_t gr = (uint32_t)(gb & 63);
-    uint64_t gw[kLaneWords + 1];
-#pragma unroll
-    for (int i = 0; i <= kLaneWords; i++) gw[i] = gp[i];
-    // flag planes of windows 0..127 (bit w <-> genome position A + w): three
-    // word pairs from the pair holding A (tile_fl is padded)
-    const uint64_t *fp = a.tile_fl + 2 * (Ac >> 6);
-    uint64_t pa3[3], pb3[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        pa3[i] = fp[2 * i];
-        pb3[i] = fp[2 * i + 1];
-    }
+    // every load of the walk is issued before anything waits: the walk blocks
+    // of the read's span -- its genome words and the flag planes of windows
+    // 0..127 (bit w <-> genome position A + w; tile_lw is padded) -- and the
+    // anchor genome's range
+    const uint32_t gr = (uint32_t)(2 * Ac & 63);
+    uint64_t gw[kLaneWords + 1], pa3[3], pb3[3];
+    lane_blocks<true>(a, Ac, len, gw, pa3, pb3);
     const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.gblk, S.atp);
     S.g = g;
     const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
@@ -520,7 +532,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     // A mismatch inside no indexed window (an N run of the genome, where the
     // read has some base) changes nothing that is decided here -- unindexed
     // windows are probed anyway -- and does not count toward the cap
-    uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0, NS0 = 0, NS1 = 0;
+    uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0, NS0 = 0, NS1 = 0, NG0 = 0, NG1 = 0;
     uint32_t nmis = 0;
     const bool has_nb = a.tile_nb != nullptr;
     uint64_t epk = 0;  // positions e of the mismatches to look up in the neighbour bits (8 bits each, <= 8)
@@ -577,6 +589,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
 #pragma unroll 1
     for (uint32_t b0 = 0; b0 < nnb; b0 += 4) {
         uint64_t nv[4];
+        uint32_t ng[4];
         int32_t sf[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -584,13 +597,14 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             const uint32_t e = (uint32_t)(epk >> (8 * q)) & 255u, c = (cpk >> (2 * q)) & 3u;
             const uint64_t ni = 3 * ((uint64_t)A + e) + c;
             nv[u] = a.nb_spec ? ((const uint64_t *)a.tile_nb)[ni] : (uint64_t)((const uint32_t *)a.tile_nb)[ni];
+            ng[u] = a.tile_nbbig ? a.tile_nbbig[ni] : 0u;  // --max-genomes >= 2: present with a set > mg
             sf[u] = b0 + u < nnb ? (int32_t)e - k + 1 : 1000;  // bit q of the word <-> window e - k + 1 + q
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             if (sf[u] == 1000) continue;
             // present, present and specific (the 32-bit form: present only)
-            const uint64_t nbw = nv[u] & 0xFFFFFFFFull, nbs = a.nb_spec ? nv[u] >> 32 : nbw;
+            const uint64_t nbw = nv[u] & 0xFFFFFFFFull, nbs = a.nb_spec ? nv[u] >> 32 : nbw, nbg = ng[u];
 #ifdef PA_STATS
             atomicAdd(&a.dbg[16], 1ull);
 #endif
@@ -600,9 +614,12 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
                 NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 32 ? nbw >> (64 - sft) : 0ull);
                 NS0 |= sft < 64 ? nbs << sft : 0ull;
                 NS1 |= sft >= 64 ? nbs << (sft - 64) : (sft > 32 ? nbs >> (64 - sft) : 0ull);
+                NG0 |= sft < 64 ? nbg << sft : 0ull;
+                NG1 |= sft >= 64 ? nbg << (sft - 64) : (sft > 32 ? nbg >> (64 - sft) : 0ull);
             } else {
                 NP0 |= nbw >> (-sft);
                 NS0 |= nbs >> (-sft);
+                NG0 |= nbg >> (-sft);
             }
         }
     }
@@ -611,11 +628,19 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         NP1 = NS1 = ~0ull;
     }
     // a window with one mismatch whose k-mer is present but multi-genome needs
-    // no probe unless --max-genomes asks for its set size: it only makes the
-    // read ambiguous (if no specific k-mer is included) or sends it to the wave
-    // kernel (if one is)
+    // no probe: it only makes the read ambiguous (if no specific k-mer is
+    // included) or sends it to the wave kernel (if one is).  Under
+    // --max-genomes its set size decides whether it is included at all or
+    // counted as highly redundant (src/kmer.py:425-427): known from the bits
+    // when a.mg_nb (NB: present with a set larger than mg -- every present one
+    // for mg <= 0, every multi-genome one for mg == 1, the per-mg bits
+    // tile_nbbig above), else the present neighbours are probed
     const bool has_mg = a.prm.flags & F_MG;
-    const uint64_t NQ0 = has_mg ? NP0 : NS0, NQ1 = has_mg ? NP1 : NS1;
+    const int32_t mgv = a.prm.mg;
+    const bool mgk = has_mg && a.mg_nb;
+    const uint64_t NB0 = !mgk ? 0ull : (mgv <= 0 ? NP0 : (mgv == 1 ? NP0 & ~NS0 : NG0));
+    const uint64_t NB1 = !mgk ? 0ull : (mgv <= 0 ? NP1 : (mgv == 1 ? NP1 & ~NS1 : NG1));
+    const uint64_t NQ0 = !has_mg ? NS0 : (mgk ? NS0 & ~NB0 : NP0), NQ1 = !has_mg ? NS1 : (mgk ? NS1 & ~NB1 : NP1);
     // ---- walked windows: 128-bit masks from the planes.  valid: an indexed
     // genome window, spec: its k-mer is specific (to g, the genome it lies in),
     // rep: it may repeat inside the read
@@ -628,7 +653,8 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     // bits do not settle (two or more in the window, or the neighbour present)
     const uint64_t P0 = (live0 & ~valid0) | (valid0 & U0 & (V0 | NQ0));
     const uint64_t P1 = (live1 & ~valid1) | (valid1 & U1 & (V1 | NQ1));
-    S.uoff = (uint32_t)(__popcll(valid0 & U0 & ~V0 & NP0 & ~NQ0) + __popcll(valid1 & U1 & ~V1 & NP1 & ~NQ1));
+    S.uoff = (uint32_t)(__popcll(valid0 & U0 & ~V0 & NP0 & ~NQ0 & ~NB0) + __popcll(valid1 & U1 & ~V1 & NP1 & ~NQ1 & ~NB1));
+    const uint32_t hr_off = (uint32_t)(__popcll(valid0 & U0 & ~V0 & NB0) + __popcll(valid1 & U1 & ~V1 & NB1));
     const uint64_t walked0 = valid0 & ~U0, walked1 = valid1 & ~U1;
 #ifdef PA_STATS
     atomicAdd(&a.dbg[17], (unsigned long long)(__popcll(live0 & ~valid0) + __popcll(live1 & ~valid1)));
@@ -666,7 +692,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     const uint32_t nspec = (uint32_t)(__popcll(incl0 & spec0) + __popcll(incl1 & spec1));
     S.nspec = nspec;
     S.nincl = nincl;
-    S.hr = hr;
+    S.hr = hr + hr_off;  // windows, repeats included (quirk 4)
     S.P0 = P0;
     S.P1 = P1;
     // a read with very many unwalked windows is left to the wave kernel
@@ -766,15 +792,16 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
     }
 }
 
-// Waves per SIMD the register allocation must allow.  The kernel is bound by
-// the latency of random table / tile reads, so occupancy pays: 4 (128 VGPRs, a
-// few spilled dwords) measured +6 % on C2 over 3, and the k-mer quality
-// variant (168 VGPRs at 3) +2-4 % on C3 at 4 despite its spills.
+// Waves per SIMD the register allocation must allow.  The kernel needs ~155
+// VGPRs (and ~150 SGPRs, which spill into VGPR lanes): at 4 waves per SIMD
+// (128 VGPRs) it spilled 110-150 B per lane to scratch and measured 3-12 %
+// slower than at 3 (168 VGPRs, no scratch) on C2 / C3 / C3raw (round 2 A/B:
+// 3.15 vs 3.25, 2.31 vs 2.42, 1.57 vs 1.78 G reads/s).
 #ifndef PA_LANE_WAVES
-#define PA_LANE_WAVES 4
+#define PA_LANE_WAVES 3
 #endif
 #ifndef PA_LANE_WAVES_Q
-#define PA_LANE_WAVES_Q 4
+#define PA_LANE_WAVES_Q 3
 #endif
 template <bool NEED_Q, bool WIN_Q>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIN_Q ? PA_LANE_WAVES_Q : PA_LANE_WAVES)))
@@ -794,13 +821,18 @@ void k_align_lane(AlignArgs a) {
         }
         __syncthreads();
     }
-    uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0, n_hr = 0, n_qf = 0;
+    // Register budget: this kernel runs at 4 waves per SIMD (128 VGPRs), so the
+    // loop's bookkeeping lives in SGPRs (wave-uniform: chunk cursor, read
+    // counts by ballot) and LDS (per-lane window counters), not in VGPRs.
+    uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0;  // wave totals (scalar)
+    LW.n_hr[lane] = 0;
+    LW.n_qf[lane] = 0;
     // Each wave takes chunks of 64 consecutive reads; a read whose walk finds a
     // specific k-mer off it is walked again from that k-mer, but later, with 63
     // others (a list per wave), so that the 3 % of such reads do not hold whole
     // waves for a second walk.  Every decision below is wave-uniform.
     const uint64_t n_chunks = (a.n + 63) / 64, wave_stride = (uint64_t)gridDim.x * kWaves;
-    uint64_t chunk = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    uint64_t chunk = (uint64_t)blockIdx.x * kWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t n_again = 0;  // entries in LW.again_r / again_a
     while (true) {
         uint64_t r = ~0ull;
@@ -841,9 +873,11 @@ void k_align_lane(AlignArgs a) {
             // most X specific k-mers and at most (nincl - nspec) + X in total,
             // while g has at least nspec and nincl (src/kmer.py:444-480): with
             // nspec >= X + max(m, 1) g is the strict top and unique, and with
-            // X - nspec <= p no genome's total exceeds g's by more than p.  Set
-            // sizes (--max-genomes) are not known off the walk: not then.
-            if (S.kind == LANE_WALK && S.nspec > 0 && !(a.prm.flags & F_MG)) {
+            // X - nspec <= p no genome's total exceeds g's by more than p.
+            // Under --max-genomes the filtered_hr_kmers count needs the set size
+            // of every window found off the walk: only when every one is known
+            // from the bits (a.mg_nb, nothing left to probe).
+            if (S.kind == LANE_WALK && S.nspec > 0 && (!(a.prm.flags & F_MG) || (a.mg_nb && !(S.P0 | S.P1)))) {
                 const int64_t X = (int64_t)(__popcll(S.P0) + __popcll(S.P1) + S.uoff);
                 const int64_t ns = (int64_t)S.nspec;
                 if (ns >= X + (a.prm.m > 0 ? a.prm.m : 1) && (a.prm.p < 0 || X - ns <= a.prm.p)) {
@@ -855,7 +889,7 @@ void k_align_lane(AlignArgs a) {
             }
             // a multi-genome k-mer off the walk next to walked specific ones
             // under --max-genomes (its set size decides): the wave kernel, without probing
-            if (S.kind == LANE_WALK && S.uoff && S.nspec > 0 && (a.prm.flags & F_MG)) {
+            if (S.kind == LANE_WALK && S.uoff && S.nspec > 0 && (a.prm.flags & F_MG) && !a.mg_nb) {
                 S.kind = LANE_HARD;
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
@@ -887,9 +921,9 @@ void k_align_lane(AlignArgs a) {
                         // (src/kmer.py:452-454) unless the total counts demote it:
                         // any h has at most (nincl - nspec) + noff distinct included
                         // k-mers, g at least nincl, so with noff - nspec <= p no total
-                        // exceeds g's by more than p (src/kmer.py:471-474).  Set sizes
-                        // (--max-genomes) are not known for the uoff windows: not then.
-                        if (S.nspec > 0 && !(a.prm.flags & F_MG) &&
+                        // exceeds g's by more than p (src/kmer.py:471-474).  Under
+                        // --max-genomes only when the uoff windows' set sizes are known.
+                        if (S.nspec > 0 && (!(a.prm.flags & F_MG) || a.mg_nb) &&
                             (a.prm.p < 0 || (int64_t)noff - (int64_t)S.nspec <= (int64_t)a.prm.p)) {
                             S.kind = LANE_UNIQUE;
 #ifdef PA_STATS
@@ -936,20 +970,16 @@ void k_align_lane(AlignArgs a) {
                 atomicMin(&a.first[S.g], (unsigned long long)key);
             }
         }
-        n_uniq += S.kind == LANE_UNIQUE;
-        n_amb += S.kind == LANE_AMB;
-        n_unm += S.kind == LANE_UNMAPPED;
-        n_drop += S.kind == LANE_DROP;
+        n_uniq += (uint32_t)__popcll(__ballot(S.kind == LANE_UNIQUE));
+        n_amb += (uint32_t)__popcll(__ballot(S.kind == LANE_AMB));
+        n_unm += (uint32_t)__popcll(__ballot(S.kind == LANE_UNMAPPED));
+        n_drop += (uint32_t)__popcll(__ballot(S.kind == LANE_DROP));
         const bool settled = S.kind == LANE_UNIQUE || S.kind == LANE_AMB || S.kind == LANE_UNMAPPED;
-        n_hr += settled ? S.hr : 0u;
-        if (WIN_Q) n_qf += settled ? S.qf : 0u;
+        if (settled && S.hr) LW.n_hr[lane] += S.hr;
+        if (WIN_Q && settled && S.qf) LW.n_qf[lane] += S.qf;
     }
-    n_uniq = wave_sum(n_uniq);
-    n_amb = wave_sum(n_amb);
-    n_unm = wave_sum(n_unm);
-    n_drop = wave_sum(n_drop);
-    n_hr = wave_sum(n_hr);
-    if (WIN_Q) n_qf = wave_sum(n_qf);
+    const uint32_t n_hr = wave_sum(LW.n_hr[lane]);
+    const uint32_t n_qf = WIN_Q ? wave_sum(LW.n_qf[lane]) : 0u;
     if (lane == 0) {
         if (n_uniq) atomicAdd(&a.stats[0], (unsigned long long)n_uniq);
         if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
