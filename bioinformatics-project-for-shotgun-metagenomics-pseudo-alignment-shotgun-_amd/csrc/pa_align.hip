@@ -573,7 +573,10 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
     const size_t shm = lane_lds_bytes(a.G);
     const bool win_q = (a.prm.flags & F_MKQ) != 0;
-    auto kern = win_q ? k_align_lane<true, true> : need_q ? k_align_lane<true, false> : k_align_lane<false, false>;
+    const bool mg = (a.prm.flags & F_MG) != 0;
+    auto kern = win_q ? (mg ? k_align_lane<true, true, true> : k_align_lane<true, true, false>)
+              : need_q ? (mg ? k_align_lane<true, false, true> : k_align_lane<true, false, false>)
+                       : (mg ? k_align_lane<false, false, true> : k_align_lane<false, false, false>);
     if (shm > 64 * 1024) PA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     int per_cu = 0, dev = 0, cus = 256;
     PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, shm));

@@ -997,8 +997,6 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     }
     for (auto &o : idx->h_goff) o -= goff[0];
     idx->total_windows = windows;
-    const int m = 0;
-    const uint32_t R = 1;
     // genome tiling for single-word keys while positions fit 32 bits (tpos);
     // PA_NO_TILE=1 turns it off (A/B measurements)
     const char *no_tile = std::getenv("PA_NO_TILE");
@@ -1106,10 +1104,9 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         }
     }
     if (cap == 0) cap = 64;
-    const uint64_t align = std::max<uint64_t>(4, R);  // whole 64-B lines (the fast kernel probes a line per step)
-    cap = (cap + align - 1) / align * align;
+    cap = (cap + 3) / 4 * 4;  // whole 64-B lines (the fast kernel probes a line per step)
     idx->cap = cap;
-    idx->home = pad::HomeCfg{cap, m > 0 ? cap / R : 0, R, (int)std::max<int64_t>(k, 0), m};
+    idx->home = pad::HomeCfg{cap};
     PA_HIP(hipMalloc(&idx->table, idx->cap * sb));
     PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
     idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;

@@ -62,7 +62,7 @@ struct pa_index {
     // open-addressing table: slots of {uint64 key[nw]; uint32 cls; uint32 tpos}
     void *table = nullptr;
     uint64_t cap = 0;
-    pad::HomeCfg home{};               // home-slot function (minimizer regions for k <= 31)
+    pad::HomeCfg home{};               // home-slot function
     uint64_t n_kmers = 0;
     // classes: cls < n_genomes means {cls}; cls >= n_genomes is multi class (cls - n_genomes)
     uint64_t n_multi = 0;

@@ -8,30 +8,37 @@
 // Why a lane per read: the wave-per-read kernel (pa_fast.h) spends most of its
 // issue slots on wave-wide bookkeeping (ballots, reductions, LDS hashes) for a
 // read whose windows are, almost always, one stretch of one genome.  Here each
-// lane takes a whole read and proves that case cheaply:
-//   1. the read is 2-bit packed in registers (16-B loads, SWAR codes);
-//   2. three seed windows (first, middle, last) are probed in the hash table;
-//      a found seed gives the read's position on the concatenated genomes
-//      (the key's first occurrence, slot.tpos) -- the anchor;
-//   3. the read's packed bases XOR the genome's from the anchor on give the
-//      mismatching bases; every window without a mismatch whose genome window
-//      is indexed resolves to tile_cls[anchor + w], exactly the table's class;
-//   4. the other windows (sequencing errors, N in the genome) are probed by the
-//      whole wave together: each lane lists its unwalked windows, the lists are
-//      concatenated in LDS and every lane probes four entries per pass, so a
-//      lane with many unwalked windows does not hold its wave back.  A found
-//      specific k-mer names the read's genome: the read is walked again from
-//      it (once).
-// If so, every included k-mer occurs in the anchor genome g, the walked
-// windows hold no k-mer twice (no PA_TILE_REP flag, the windows of one read are
-// < 127 apart), every specific k-mer is specific to g, and the reference's
-// decision collapses: no specific k-mer -> AMBIGUOUS with an empty list
-// (src/kmer.py:458-461); else exactly one genome -> UNIQUE g (src/kmer.py:453),
-// and the p-check cannot demote (every included k-mer contains g, so no genome
-// exceeds g's total; src/kmer.py:464-480).  Any other read -- a found
-// non-walked window, a local repeat, no anchor, a non-ACGT base, a k-mer
-// quality filter that can bite, a read longer than the lane limits -- is
-// queued whole for the wave kernel, which handles every case exactly.
+// lane takes a whole read and proves that case cheaply (DESIGN.md section 4):
+//   1. lane_prep: the read is 2-bit packed (16-B loads, SWAR codes) into the
+//      lane's LDS row; with a quality filter, the read mean and -- when the
+//      read's minimum quality can fail it -- a 128-bit mask of the windows
+//      failing --min-kmer-quality (a running sum over the staged chunks);
+//   2. five seed windows (first ... last) are probed in two rounds: the first
+//      and the last, then the middle three only if neither is specific.  A
+//      found seed gives the read's position on the concatenated genomes (the
+//      key's first occurrence) -- the anchor; with only multi-genome seeds, up
+//      to three distinct stretches are compared with the read and the one with
+//      the fewest mismatching bases is walked;
+//   3. lane_walk: the read XOR the genome words of the walk block gives the
+//      mismatching bases; the flag planes give 128-bit masks of indexed /
+//      specific / local-repeat windows; a window with exactly one mismatch is
+//      settled by its neighbour bits (tile_nb, four words per round trip);
+//   4. enough walked specific k-mers decide the read by a bound, without any
+//      probe (k_align_lane's loop);
+//   5. lane_probe_wave: the other windows (two or more mismatches, unindexed
+//      genome windows, present specific neighbours) are probed by the whole
+//      wave together -- each lane lists its windows, the lists are concatenated
+//      in LDS, the Bloom filter drops surely absent keys and every lane probes
+//      four entries per pass.  A found specific k-mer off the walk re-anchors
+//      the read: it is walked again later, in a per-wave batch of 64 such reads.
+// If every included k-mer is a walked window of genome g (no local repeat among
+// them, the walk inside g), the reference's decision collapses: no specific
+// k-mer -> AMBIGUOUS with an empty list (src/kmer.py:458-461); else exactly one
+// genome -> UNIQUE g (src/kmer.py:453), and the p-check cannot demote (every
+// included k-mer contains g; src/kmer.py:464-480).  Any other read -- no
+// anchor, a local repeat, a non-ACGT base, a second re-anchoring, a read longer
+// than the lane limits -- is queued whole for the wave kernel, which handles
+// every case exactly.
 
 constexpr int kLaneMaxW = 128;    // windows per read on the lane path
 constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
@@ -498,7 +505,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 
 // Phase 2: walk from the anchor; walked windows resolve from the tile, the
 // others are left in P0 / P1 for the cooperative probes.
-template <bool WIN_Q>
+template <bool WIN_Q, bool MG>
 __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *row, LaneRead &S) {
     const int k = a.k;
     const uint32_t W = S.W, len = S.len;
@@ -597,7 +604,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             const uint32_t e = (uint32_t)(epk >> (8 * q)) & 255u, c = (cpk >> (2 * q)) & 3u;
             const uint64_t ni = 3 * ((uint64_t)A + e) + c;
             nv[u] = a.nb_spec ? ((const uint64_t *)a.tile_nb)[ni] : (uint64_t)((const uint32_t *)a.tile_nb)[ni];
-            ng[u] = a.tile_nbbig ? a.tile_nbbig[ni] : 0u;  // --max-genomes >= 2: present with a set > mg
+            ng[u] = MG && a.tile_nbbig ? a.tile_nbbig[ni] : 0u;  // --max-genomes >= 2: present with a set > mg
             sf[u] = b0 + u < nnb ? (int32_t)e - k + 1 : 1000;  // bit q of the word <-> window e - k + 1 + q
         }
 #pragma unroll
@@ -635,7 +642,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     // when a.mg_nb (NB: present with a set larger than mg -- every present one
     // for mg <= 0, every multi-genome one for mg == 1, the per-mg bits
     // tile_nbbig above), else the present neighbours are probed
-    const bool has_mg = a.prm.flags & F_MG;
+    const bool has_mg = MG;  // (a.prm.flags & F_MG)
     const int32_t mgv = a.prm.mg;
     const bool mgk = has_mg && a.mg_nb;
     const uint64_t NB0 = !mgk ? 0ull : (mgv <= 0 ? NP0 : (mgv == 1 ? NP0 & ~NS0 : NG0));
@@ -792,19 +799,21 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
     }
 }
 
-// Waves per SIMD the register allocation must allow.  The kernel needs ~155
-// VGPRs (and ~150 SGPRs, which spill into VGPR lanes): at 4 waves per SIMD
-// (128 VGPRs) it spilled 110-150 B per lane to scratch and measured 3-12 %
-// slower than at 3 (168 VGPRs, no scratch) on C2 / C3 / C3raw (round 2 A/B:
-// 3.15 vs 3.25, 2.31 vs 2.42, 1.57 vs 1.78 G reads/s).
+// Waves per SIMD the register allocation must allow.  The kernel is bound by
+// the latency of random table / tile reads, so occupancy pays as long as the
+// spills stay out of the walk: without --max-genomes and the window-quality
+// mask (MG, WIN_Q false: C2) it needs ~145 VGPRs and runs at 4 waves per SIMD
+// (128 VGPRs, 32 B/lane of scratch outside the walk loops; round-2 A/B on C2:
+// 3.48 vs 3.36 G reads/s at 3).  With them (C3) it needs ~170 and spills
+// 100-140 B/lane at 4, so it runs at 3 (no scratch).
 #ifndef PA_LANE_WAVES
-#define PA_LANE_WAVES 3
+#define PA_LANE_WAVES 4
 #endif
 #ifndef PA_LANE_WAVES_Q
 #define PA_LANE_WAVES_Q 3
 #endif
-template <bool NEED_Q, bool WIN_Q>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIN_Q ? PA_LANE_WAVES_Q : PA_LANE_WAVES)))
+template <bool NEED_Q, bool WIN_Q, bool MG>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((WIN_Q || MG) ? PA_LANE_WAVES_Q : PA_LANE_WAVES)))
 void k_align_lane(AlignArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const uint32_t G = a.G;
@@ -821,7 +830,7 @@ void k_align_lane(AlignArgs a) {
         }
         __syncthreads();
     }
-    // Register budget: this kernel runs at 4 waves per SIMD (128 VGPRs), so the
+    // Register budget: this kernel runs at 3-4 waves per SIMD (PA_LANE_WAVES), so the
     // loop's bookkeeping lives in SGPRs (wave-uniform: chunk cursor, read
     // counts by ballot) and LDS (per-lane window counters), not in VGPRs.
     uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0;  // wave totals (scalar)
@@ -862,7 +871,7 @@ void k_align_lane(AlignArgs a) {
 #endif
 #pragma unroll 1
         for (int attempt = again_batch ? 1 : 0; attempt < 2; attempt++) {
-            if (S.kind == LANE_WALK) lane_walk<WIN_Q>(a, LW.R[lane], S);
+            if (S.kind == LANE_WALK) lane_walk<WIN_Q, MG>(a, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif
@@ -877,7 +886,7 @@ void k_align_lane(AlignArgs a) {
             // Under --max-genomes the filtered_hr_kmers count needs the set size
             // of every window found off the walk: only when every one is known
             // from the bits (a.mg_nb, nothing left to probe).
-            if (S.kind == LANE_WALK && S.nspec > 0 && (!(a.prm.flags & F_MG) || (a.mg_nb && !(S.P0 | S.P1)))) {
+            if (S.kind == LANE_WALK && S.nspec > 0 && (!MG || (a.mg_nb && !(S.P0 | S.P1)))) {
                 const int64_t X = (int64_t)(__popcll(S.P0) + __popcll(S.P1) + S.uoff);
                 const int64_t ns = (int64_t)S.nspec;
                 if (ns >= X + (a.prm.m > 0 ? a.prm.m : 1) && (a.prm.p < 0 || X - ns <= a.prm.p)) {
@@ -889,7 +898,7 @@ void k_align_lane(AlignArgs a) {
             }
             // a multi-genome k-mer off the walk next to walked specific ones
             // under --max-genomes (its set size decides): the wave kernel, without probing
-            if (S.kind == LANE_WALK && S.uoff && S.nspec > 0 && (a.prm.flags & F_MG) && !a.mg_nb) {
+            if (S.kind == LANE_WALK && S.uoff && S.nspec > 0 && MG && !a.mg_nb) {
                 S.kind = LANE_HARD;
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
@@ -923,7 +932,7 @@ void k_align_lane(AlignArgs a) {
                         // k-mers, g at least nincl, so with noff - nspec <= p no total
                         // exceeds g's by more than p (src/kmer.py:471-474).  Under
                         // --max-genomes only when the uoff windows' set sizes are known.
-                        if (S.nspec > 0 && (!(a.prm.flags & F_MG) || a.mg_nb) &&
+                        if (S.nspec > 0 && (!MG || a.mg_nb) &&
                             (a.prm.p < 0 || (int64_t)noff - (int64_t)S.nspec <= (int64_t)a.prm.p)) {
                             S.kind = LANE_UNIQUE;
 #ifdef PA_STATS
@@ -985,7 +994,7 @@ void k_align_lane(AlignArgs a) {
         if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
         if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
         if (n_drop) atomicAdd(&a.stats[3], (unsigned long long)n_drop);
-        if (n_hr && (a.prm.flags & F_MG)) atomicAdd(&a.stats[5], (unsigned long long)n_hr);
+        if (n_hr && MG) atomicAdd(&a.stats[5], (unsigned long long)n_hr);
         if (WIN_Q && n_qf) atomicAdd(&a.stats[4], (unsigned long long)n_qf);
     }
     if (lds) {

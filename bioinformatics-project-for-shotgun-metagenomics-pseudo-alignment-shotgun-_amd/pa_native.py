@@ -136,7 +136,11 @@ def lib():
         "pa_seqset_export": (I32, [P, P, P, P, P]),
         "pa_seqset_free": (None, [P]),
     }
+    # PA_LIBRARY_PARTIAL=1: an older libpa (A/B experiments) may lack newer entry points
+    partial = os.environ.get("PA_LIBRARY_PARTIAL") == "1"
     for name, (res, args) in sig.items():
+        if partial and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
