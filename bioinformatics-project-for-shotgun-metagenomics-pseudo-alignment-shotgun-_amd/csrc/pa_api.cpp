@@ -75,6 +75,11 @@ pa_status pa_device_count(int32_t *n) {
 
 pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *genome_off, uint32_t n_genomes,
                          int64_t k, void *stream, pa_index **out) {
+    return pa_index_build_ex(device, genomes, genome_off, n_genomes, k, 0u, stream, out);
+}
+
+pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t *genome_off, uint32_t n_genomes,
+                            int64_t k, uint32_t flags, void *stream, pa_index **out) {
     PA_CHECK(out != nullptr, PA_EINVAL, "out must not be NULL");
     *out = nullptr;
     PA_CHECK(genome_off != nullptr, PA_EINVAL, "genome_off must not be NULL");
@@ -110,13 +115,22 @@ pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *ge
     pa_index *idx = new (std::nothrow) pa_index();
     PA_CHECK(idx != nullptr, PA_ENOMEM, "out of host memory");
     idx->device = device;
-    pa_status rc = pa::index_build(idx, genomes, genome_off, n_genomes, k, as_stream(stream));
+    pa_status rc = pa::index_build(idx, genomes, genome_off, n_genomes, k, as_stream(stream),
+                                   (flags & PA_BUILD_DEFER_TILES) != 0);
     if (rc != PA_OK) {
         pa::index_release(idx);
         delete idx;
         return rc;
     }
     *out = idx;
+    return PA_OK;
+}
+
+pa_status pa_index_prepare(pa_index *idx, void *stream) {
+    PA_CHECK(idx != nullptr, PA_EINVAL, "NULL argument");
+    PA_HIP(hipSetDevice(idx->device));
+    PA_TRY(pa::index_prepare(idx, as_stream(stream)));
+    PA_HIP(hipStreamSynchronize(as_stream(stream)));
     return PA_OK;
 }
 
@@ -396,6 +410,7 @@ pa_status pa_align(const pa_index *idx, const pa_reads *reads, const pa_params *
     pa::DevParams dp;
     PA_TRY(to_dev_params(params, idx->n_genomes, &dp));
     PA_HIP(hipSetDevice(idx->device));
+    PA_TRY(pa::index_prepare(const_cast<pa_index *>(idx), as_stream(stream)));
     return pa::align(const_cast<pa_index *>(idx), reads, dp, read_index_base, acc, as_stream(stream));
 }
 
@@ -407,6 +422,7 @@ pa_status pa_align_detail(const pa_index *idx, const pa_reads *reads, const pa_p
     pa::DevParams dp;
     PA_TRY(to_dev_params(params, idx->n_genomes, &dp));
     PA_HIP(hipSetDevice(idx->device));
+    PA_TRY(pa::index_prepare(const_cast<pa_index *>(idx), as_stream(stream)));
     return pa::align_detail(const_cast<pa_index *>(idx), reads, dp, read_type, filtered_kmers, redundant_kmers,
                             list_off, lists, list_cap, list_total, as_stream(stream));
 }

@@ -489,8 +489,17 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 // that the variant k-mer is shared, which is all an ambiguous read needs.
 // Defined on the 2-bit genome string (N packed as A), for windows that are
 // indexed themselves (tile_cls != NONE).
+// Two passes: pass 0 probes the 3k neighbours of every window that is its
+// k-mer's first occurrence (slot.tpos); pass 1 copies them to every other
+// occurrence t of the k-mer, which has the same neighbours: the bits of window
+// t sit at the same bit (k - 1 - j) of words 3 (t + j) + b as the first
+// occurrence's in words 3 (fo + j) + b, so the copy reads 3k consecutive words
+// (~6 128-B lines) instead of probing 3k keys (C5's families repeat about half
+// of their windows).
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
-                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full) {
+                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
+                           const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local,
+                           int pass) {
     unsigned long long *nb = (unsigned long long *)nb_out;  // full: 64-bit words, present | specific << 32
     uint32_t *nb32 = (uint32_t *)nb_out;                    // else 32-bit words, present
     const int sh = 64 - 2 * k;
@@ -499,19 +508,41 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
     for (; t < n; t += stride) {
         if (tile_cls[t] == NONE) continue;
         const uint64_t K = get64_at(pk, 2 * t) >> sh;
+        Key<1> kk;
+        kk.w[0] = K;
+        uint64_t slot;
+        uint32_t cls, tpos;
+        if (!table_find<1>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos)) continue;
+        const uint64_t fo = first_pos(cls, tpos, G, class_genomes, goff, local != 0);
+        if ((fo == t) != (pass == 0)) continue;
+        if (pass == 1) {  // copy the first occurrence's bits of this window
+            for (int j = 0; j < k; j++) {
+#pragma unroll
+                for (int b = 0; b < 3; b++) {
+                    if (full) {
+                        const unsigned long long m = nb[3 * (fo + j) + b] & (0x100000001ull << (k - 1 - j));
+                        if (m) atomicOr(&nb[3 * (t + j) + b], m);
+                    } else {
+                        const uint32_t m = nb32[3 * (fo + j) + b] & (1u << (k - 1 - j));
+                        if (m) atomicOr(&nb32[3 * (t + j) + b], m);
+                    }
+                }
+            }
+            continue;
+        }
         for (int j = 0; j < k; j++) {
             const int bs = 2 * (k - 1 - j);
             const uint64_t cj = (K >> bs) & 3;
             uint64_t keys[3];
-            uint32_t cls[3];
+            uint32_t cls3[3];
 #pragma unroll
             for (int b = 0; b < 3; b++) keys[b] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
-            const uint32_t f = probe_lines<3>(table, hc, keys, cls);  // the three substitutions together
+            const uint32_t f = probe_lines<3>(table, hc, keys, cls3);  // the three substitutions together
 #pragma unroll
             for (int b = 0; b < 3; b++) {
                 if (!((f >> b) & 1u)) continue;
                 if (full)
-                    atomicOr(&nb[3 * (t + j) + b], (cls[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                    atomicOr(&nb[3 * (t + j) + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
                 else
                     atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
             }
@@ -827,10 +858,25 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         idx->device_bytes += n_cls * 12 + std::max<uint64_t>(entries, 1) * 4;
     }
     if (idx->tile_n > 0 && (uint64_t)G + idx->class_entries >= PA_TILE_REP) idx->tile_n = 0;  // ids need bit 31
-    cleanup();  // the build scratch (20 B per slot) is not needed by the tiles
-    deg = last_g = aux = lists = cs_id = err = nullptr;
-    off = cs_key = cs_rep = rep_of = nullptr;
-    cnt = nullptr;
+    idx->tiles_pending = idx->tile_n > 0 ? 1 : 0;  // made by build_tiles_nw (index_prepare)
+#undef B_HIP
+    cleanup();
+    return rc;
+}
+
+// Step 6, the align-side view of the index (k <= 31, references whose
+// genomes are each < 2^32 bases): the genome tiling, flag planes and walk
+// blocks, neighbour bits and the Bloom filter.  Made after the build scratch
+// is freed -- at the end of pa_index_build, or deferred (PA_BUILD_DEFER_TILES)
+// to pa_index_prepare / the first align call, so that an index used only for
+// EXTSIM statistics (src/kmer.py:152-263) never pays for it.
+template <int NW>
+pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
+    const uint32_t G = idx->n_genomes;
+    const int k = (int)idx->k;
+    const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
+    Slot<NW> *table = (Slot<NW> *)idx->table;
+#define B_HIP(call) PA_HIP(call)
     if (idx->tile_n > 0) {  // tiles: 6.5 B per base (class, flags, set sizes, 2-bit string), + margin
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || idx->tile_n * 7 + (2ull << 30) > free_b) idx->tile_n = 0;
@@ -886,9 +932,11 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
                 if (n * 3 * wb <= free_b / 4 * 3) {
                     B_HIP(hipMalloc(&idx->tile_nb, n * 3 * wb + 64));
                     B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 3 * wb + 64, st));
-                    hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
-                                       st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                       idx->tile_nb, full ? 1 : 0);
+                    for (int pass = 0; pass < 2; pass++)
+                        hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
+                                           st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                           idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
+                                           pass);
                     idx->nb_spec = full ? 1 : 0;
                     idx->device_bytes += n * 3 * wb;
                 }
@@ -918,8 +966,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         idx->device_bytes += n * 4 + nwords * 8;
     }
 #undef B_HIP
-    cleanup();
-    return rc;
+    return PA_OK;
 }
 
 template <int NW>
@@ -983,8 +1030,21 @@ void index_release(pa_index *idx) {
     idx->table = nullptr;
 }
 
+pa_status index_prepare(pa_index *idx, hipStream_t st) {
+    if (!idx->tiles_pending) return PA_OK;
+    idx->tiles_pending = 0;
+    pa_status rc = build_tiles_nw<1>(idx, st);  // (tiles are made for single-word keys only)
+    if (rc != PA_OK) {  // the index stays usable without its align-side view
+        hipFree(idx->tile_cls); hipFree(idx->tile_pk); hipFree(idx->tile_lw); hipFree(idx->tile_nb);
+        hipFree(idx->tile_gblk); hipFree(idx->bloom);
+        idx->tile_cls = nullptr, idx->tile_pk = nullptr, idx->tile_lw = nullptr, idx->tile_nb = nullptr;
+        idx->tile_gblk = nullptr, idx->bloom = nullptr, idx->bloom_lg = 0, idx->tile_n = 0;
+    }
+    return rc;
+}
+
 pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
-                      hipStream_t st) {
+                      hipStream_t st, bool defer_tiles) {
     idx->k = k;
     idx->nw = k > 0 ? key_words(k) : 1;
     idx->n_genomes = n;
@@ -1111,15 +1171,17 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
     idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
     if (k <= 0 || windows == 0) return PA_OK;
+    pa_status rc = PA_EUNSUPPORTED;
     switch (idx->nw) {
-        case 1: return build_nw<1>(idx, st);
-        case 2: return build_nw<2>(idx, st);
-        case 3: return build_nw<3>(idx, st);
-        case 4: return build_nw<4>(idx, st);
-        case 5: return build_nw<5>(idx, st);
+        case 1: rc = build_nw<1>(idx, st); break;
+        case 2: rc = build_nw<2>(idx, st); break;
+        case 3: rc = build_nw<3>(idx, st); break;
+        case 4: rc = build_nw<4>(idx, st); break;
+        case 5: rc = build_nw<5>(idx, st); break;
+        default: set_error("unsupported k");
     }
-    set_error("unsupported k");
-    return PA_EUNSUPPORTED;
+    if (rc != PA_OK || defer_tiles) return rc;
+    return index_prepare(idx, st);
 }
 
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,

@@ -83,6 +83,7 @@ struct pa_index {
     // concatenated 2-bit string plus the class of the k-mer starting at every
     // position (NONE where no indexed window starts); slots point into it (tpos)
     uint64_t tile_n = 0;               // concatenated bases (0: no tiling)
+    int tiles_pending = 0;             // 1: the tiles below are still to be made (index_prepare)
     uint32_t *tile_cls = nullptr;      // [tile_n]
     uint64_t *tile_pk = nullptr;       // [tile_n / 32 + 32] MSB-first 2-bit words (padded)
     uint64_t *tile_lw = nullptr;       // [4 (tile_n / 64 + 5)] lane-walk blocks: 2-bit words + flag planes (k_tile_walk)
@@ -129,7 +130,8 @@ struct pa_result {
 
 namespace pa {
 pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
-                      hipStream_t st);
+                      hipStream_t st, bool defer_tiles);
+pa_status index_prepare(pa_index *idx, hipStream_t st);  // the tiles of a deferred build (no-op otherwise)
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
                        uint32_t *size_out, hipStream_t st);
 pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint32_t n_groups, uint64_t *total,

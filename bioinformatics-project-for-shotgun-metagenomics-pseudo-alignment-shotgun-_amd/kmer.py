@@ -172,7 +172,10 @@ class KmerReference:
     # -- device index -------------------------------------------------------
 
     def _build(self) -> None:
-        self._index = N.Index([g["genome"] for g in self.genomes], self.kmer_len, device=self._device)
+        # the align-side view (tiles, neighbour bits) is made at the first align:
+        # an index that EXTSIM then rebuilds from the kept genomes never needs it
+        self._index = N.Index([g["genome"] for g in self.genomes], self.kmer_len, device=self._device,
+                              defer_tiles=True)
         self._view: Optional[Dict[str, Dict[Record, Set[int]]]] = None
 
     @property

@@ -23,11 +23,12 @@ PA_MAX_GENOMES = (1 << 20) - 1
 PA_COMM_ID_BYTES = 128
 HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4
 NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
+PA_BUILD_DEFER_TILES = 1
 
 # every symbol declared in include/pa.h
 EXPORTS = (
     "pa_last_error", "pa_version", "pa_device_count",
-    "pa_index_build", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
+    "pa_index_build", "pa_index_build_ex", "pa_index_prepare", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
     "pa_index_extsim_stats",
     "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_reads_download", "pa_reads_free",
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
@@ -102,6 +103,8 @@ def lib():
         "pa_version": (ctypes.c_char_p, []),
         "pa_device_count": (I32, [ctypes.POINTER(I32)]),
         "pa_index_build": (I32, [I32, ctypes.c_char_p, P, U32, I64, P, PP]),
+        "pa_index_build_ex": (I32, [I32, ctypes.c_char_p, P, U32, I64, U32, P, PP]),
+        "pa_index_prepare": (I32, [P, P]),
         "pa_index_free": (None, [P]),
         "pa_index_get_info": (I32, [P, ctypes.POINTER(IndexInfo)]),
         "pa_index_lookup": (I32, [P, ctypes.c_char_p, U64, U32, P, P, P]),
@@ -308,20 +311,28 @@ def concat(chunks: Sequence) -> Tuple[np.ndarray, np.ndarray]:
 class Index:
     """A device-resident k-mer index (pa_index)."""
 
-    def __init__(self, genomes: Sequence, k: int, device: Optional[int] = None, stream=None):
+    def __init__(self, genomes: Sequence, k: int, device: Optional[int] = None, stream=None,
+                 defer_tiles: bool = False):
+        """defer_tiles: build the table and genome sets only (PA_BUILD_DEFER_TILES);
+        the align-side view is made by prepare() or the first align."""
         buf, off = concat(genomes)
         self.device = default_device() if device is None else int(device)
         self.k = int(k)
         h = P()
         kk = max(min(self.k, 2 ** 62), -2 ** 62)
-        _check(lib().pa_index_build(self.device, buf.ctypes.data_as(ctypes.c_char_p) if buf.size else None,
-                                    _ptr(off), len(off) - 1, kk, _stream(stream), ctypes.byref(h)))
+        _check(lib().pa_index_build_ex(self.device, buf.ctypes.data_as(ctypes.c_char_p) if buf.size else None,
+                                       _ptr(off), len(off) - 1, kk, PA_BUILD_DEFER_TILES if defer_tiles else 0,
+                                       _stream(stream), ctypes.byref(h)))
         self._h = h
         self.n_genomes = len(off) - 1
 
     @property
     def handle(self):
         return self._h
+
+    def prepare(self, stream=None) -> None:
+        """Make a deferred build's align-side view now (pa_index_prepare)."""
+        _check(lib().pa_index_prepare(self._h, _stream(stream)))
 
     def close(self):
         if getattr(self, "_h", None):

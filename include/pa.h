@@ -7,6 +7,8 @@
  * point below replaces one piece of that API (file:line in the reference):
  *
  *   pa_index_build           KmerReference.__init__ / _build_kmer_mapping   src/kmer.py:113-150
+ *   pa_index_build_ex        the same, the align-side view deferred        src/kmer.py:113-133
+ *   pa_index_prepare         (the deferred view, before the first align)
  *   pa_index_lookup          KmerReference.get_kmer_references / __getitem__ src/kmer.py:284-298
  *   pa_index_class_genomes   (genome set of a k-mer, i.e. the keys of kmers[kmer]) src/kmer.py:130
  *   pa_index_extsim_stats    KmerReference._compute_genome_stats + the pairwise
@@ -133,6 +135,19 @@ pa_status pa_device_count(int32_t *n);
 /* genomes: concatenated ASCII; genome_off: n_genomes+1 offsets (CSR). */
 pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *genome_off, uint32_t n_genomes,
                          int64_t k, void *stream, pa_index **out);
+/* The same with build flags.  PA_BUILD_DEFER_TILES: build the k-mer table and
+ * the genome sets only; the align-side view (genome tiling, neighbour bits,
+ * Bloom filter -- DESIGN.md section 3) is made by pa_index_prepare or by the
+ * first pa_align / pa_align_detail call.  For an index that may only feed
+ * pa_index_extsim_stats (KmerReference(..., filter_similar=True) builds, then
+ * filters: src/kmer.py:113-133, 252-263) before it is rebuilt from the kept
+ * genomes.  pa_index_build = pa_index_build_ex(..., 0, ...). */
+#define PA_BUILD_DEFER_TILES 1u
+pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t *genome_off, uint32_t n_genomes,
+                            int64_t k, uint32_t flags, void *stream, pa_index **out);
+/* Make a deferred build's align-side view now (no-op otherwise); returns when
+ * it is done. */
+pa_status pa_index_prepare(pa_index *idx, void *stream);
 void pa_index_free(pa_index *idx);
 pa_status pa_index_get_info(const pa_index *idx, pa_index_info *out);
 /* n k-mers of length kmer_len packed back to back; cls_out[i] = class id or -1
