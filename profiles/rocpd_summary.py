@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 database (--kernel-trace [--pmc ...]) into a text table.
 
-    python profiles/rocpd_summary.py gpurun_out/prof_c2/run_results.db > profiles/r01_c2_kernel_stats.txt
+    python profiles/rocpd_summary.py gpurun_out/prof_c2/run_results.db > profiles/r02/c2_kernel_stats.txt
 
 Per kernel: dispatch count, average / total duration; and, when the database
 holds PMC samples, the per-dispatch average of every counter.
@@ -38,6 +38,12 @@ def main(path: str) -> None:
             print(f"  {k[:70]}")
             for cname, v in sorted(d.items()):
                 print(f"      {cname:32s} {v:18.1f}")
+            wc = d.get("SQ_WAVE_CYCLES")
+            if wc:  # per-wave shares of the resident cycles
+                for cname in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                              "SQ_ACTIVE_INST_VMEM"):
+                    if cname in d:
+                        print(f"      {cname + ' / SQ_WAVE_CYCLES':48s} {d[cname] / wc:8.3f}")
 
 
 if __name__ == "__main__":

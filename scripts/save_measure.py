@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Copy one scripts/measure.sh result into profiles/r02/: the bench line, the
+rocprofv3 kernel summary of the same workload and its SQ counter pass, each
+summarised by profiles/rocpd_summary.py, plus the git commit measured.
+
+    python scripts/save_measure.py <tag> [name]      (name defaults to the tag)
+"""
+import glob
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag: str, name: str) -> None:
+    src = os.path.join(REPO, "gpurun_out", f"ms_{tag}")
+    dst = os.path.join(REPO, "profiles", "r02")
+    os.makedirs(dst, exist_ok=True)
+    head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True, text=True).stdout.strip()
+    with open(os.path.join(src, "args")) as f:
+        args = f.read().strip()
+    with open(os.path.join(src, "bench.json")) as f:
+        line = f.read()
+    with open(os.path.join(dst, f"bench_{name}.json"), "w") as f:
+        f.write(line)
+    summ = os.path.join(REPO, "profiles", "rocpd_summary.py")
+    for kind, label in (("trace", "kernel_stats"), ("sq", "sq")):
+        dbs = glob.glob(os.path.join(src, kind, "**", "*.db"), recursive=True)
+        if not dbs:
+            continue
+        out = subprocess.run([sys.executable, summ, dbs[0]], capture_output=True, text=True, check=True).stdout
+        with open(os.path.join(dst, f"{name}_{label}.txt"), "w") as f:
+            f.write(f"# bench.py --config {args}; measured at commit {head} (+ working tree)\n" + out)
+    print("saved", name)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else sys.argv[1])
