@@ -160,10 +160,12 @@ __device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint6
 // NP single-word probes in flight together, a whole 64-B line (4 slots) per
 // step: tables are whole lines (cap % 4 == 0), so a search costs ~1-2 round
 // trips even at a high load factor, where slot-by-slot probing (table_find)
-// pays one dependent load per slot.  Bit i of `found` / cls[i]: key i's result.
+// pays one dependent load per slot.  Bit i of `found` / cls[i]: key i's result
+// (keys outside `act` are not looked up).
 template <int NP>
 __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, const HomeCfg &hc,
-                                                const uint64_t (&key)[NP], uint32_t (&cls)[NP]) {
+                                                const uint64_t (&key)[NP], uint32_t (&cls)[NP],
+                                                uint32_t act = (1u << NP) - 1) {
     uint64_t pos[NP];
 #pragma unroll
     for (int i = 0; i < NP; i++) {
@@ -171,7 +173,7 @@ __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, c
         kk.w[0] = key[i];
         pos[i] = home_of<1>(kk, key_hash(kk), hc);
     }
-    uint32_t act = (1u << NP) - 1, found = 0;
+    uint32_t found = 0;
     while (act) {
         Slot<1> s[NP][4];
 #pragma unroll

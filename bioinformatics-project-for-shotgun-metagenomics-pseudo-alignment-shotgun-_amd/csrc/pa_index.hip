@@ -190,33 +190,68 @@ __global__ void k_hll(const uint8_t *__restrict__ codes, uint64_t gstart, uint64
     }
 }
 
-// Singletons -> final slot values; multi slots -> list storage.
+// Singletons -> final slot values; multi slots -> list storage.  Each block
+// owns one contiguous range of slots: it first sums the list sizes of its
+// multi slots and takes its storage with ONE atomic (a bump per wave made
+// ~10^7 same-address atomics on C5 and cost 144 ms on C2), then hands out
+// offsets inside the range by block-wide scans.
 template <int NW>
-__global__ void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg, uint32_t *aux,
-                             uint64_t *off, unsigned long long *bump, unsigned long long *n_multi) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const int lane = lane_id();
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < cap; base += stride) {  // uniform trip count
-        const uint64_t s = base + threadIdx.x;
+__global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg, uint32_t *aux,
+                                                    uint64_t *off, unsigned long long *bump,
+                                                    unsigned long long *n_multi) {
+    __shared__ unsigned long long s_red[2][4];
+    __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_wave[4];
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t per = ((cap + gridDim.x - 1) / gridDim.x + 255) & ~255ull;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(cap, lo + per);
+    if (lo >= hi) return;
+    // phase A: this range's list storage and multi slots (deg is 0 at empty slots)
+    unsigned long long tot = 0, nm = 0;
+    for (uint64_t s = lo + threadIdx.x; s < hi; s += 256) {
+        const uint32_t d = deg[s];
+        if (d >= 2) tot += d, nm++;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        tot += __shfl_down(tot, o);
+        nm += __shfl_down(nm, o);
+    }
+    if (lane == 0) s_red[0][wv] = tot, s_red[1][wv] = nm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long T = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+        const unsigned long long M = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
+        s_base = T ? atomicAdd(bump, T) : 0ull;
+        if (M) atomicAdd(n_multi, M);
+    }
+    __syncthreads();
+    unsigned long long run = s_base;
+    // phase B: singletons get their class, multi slots their list offsets
+    for (uint64_t b = lo; b < hi; b += 256) {
+        const uint64_t s = b + threadIdx.x;
         uint32_t d = 0;
-        if (s < cap && table[s].key[0] != EMPTY) {
+        if (s < hi && table[s].key[0] != EMPTY) {
             d = deg[s];
             if (d == 1) {
                 table[s].cls = aux[s];
                 d = 0;
             }
         }
-        // one bump allocation per wave (a single global counter would serialise ~10^7 atomics)
         const uint32_t incl = wave_incl_scan(d);
-        const uint64_t multi = __ballot(d >= 2);
-        uint64_t wbase = 0;
-        if (lane == 63 && incl) wbase = atomicAdd(bump, (unsigned long long)incl);
-        wbase = shfl64(wbase, 63);
-        if (lane == 0 && multi) atomicAdd(n_multi, (unsigned long long)__popcll(multi));
+        if (lane == 63) s_wave[wv] = incl;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            before += i < wv ? s_wave[i] : 0u;
+            total += s_wave[i];
+        }
         if (d >= 2) {
-            off[s] = wbase + incl - d;
+            off[s] = run + before + incl - d;
             aux[s] = 0;
         }
+        run += total;
+        __syncthreads();  // s_wave is rewritten by the next chunk
     }
 }
 
@@ -499,7 +534,7 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
                            const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
                            const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local,
-                           int pass) {
+                           int pass, const uint64_t *__restrict__ bloom, uint32_t bloom_lg) {
     unsigned long long *nb = (unsigned long long *)nb_out;  // full: 64-bit words, present | specific << 32
     uint32_t *nb32 = (uint32_t *)nb_out;                    // else 32-bit words, present
     const int sh = 64 - 2 * k;
@@ -537,7 +572,17 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
             uint32_t cls3[3];
 #pragma unroll
             for (int b = 0; b < 3; b++) keys[b] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
-            const uint32_t f = probe_lines<3>(table, hc, keys, cls3);  // the three substitutions together
+            uint32_t act = 7u;
+            if (bloom) {  // surely absent neighbours are not probed; most share the window's Bloom line
+#pragma unroll
+                for (int b = 0; b < 3; b++) {
+                    uint64_t wi, bm;
+                    bloom_word(keys[b], k, bloom_lg, wi, bm);
+                    if ((bloom[wi] & bm) != bm) act &= ~(1u << b);
+                }
+                if (!act) continue;
+            }
+            const uint32_t f = probe_lines<3>(table, hc, keys, cls3, act);  // the substitutions together
 #pragma unroll
             for (int b = 0; b < 3; b++) {
                 if (!((f >> b) & 1u)) continue;
@@ -932,11 +977,36 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 if (n * 3 * wb <= free_b / 4 * 3) {
                     B_HIP(hipMalloc(&idx->tile_nb, n * 3 * wb + 64));
                     B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 3 * wb + 64, st));
+                    // a build-time Bloom filter of the keys (~16 bits per key, in
+                    // HBM; freed below): most of the 3k neighbours of a window are
+                    // absent and share the window's Bloom line (minimizer-chosen),
+                    // so a probe costs an L2 hit instead of a table line.
+                    // PA_NB_BLOOM=0 turns it off (A/B)
+                    uint64_t *bb = nullptr;
+                    uint32_t bb_lg = 6;
+                    const char *nbb = std::getenv("PA_NB_BLOOM");
+                    if (!(nbb && nbb[0] == '0') && idx->n_kmers > 0) {
+                        while (bb_lg < 36 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;
+                        size_t fb = 0, tb = 0;
+                        if (hipMemGetInfo(&fb, &tb) != hipSuccess) fb = 0;
+                        while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
+                        if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && hipMalloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
+                            B_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
+                            hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                               dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, bb, bb_lg, k);
+                        } else {
+                            bb = nullptr;
+                        }
+                    }
                     for (int pass = 0; pass < 2; pass++)
                         hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
                                            st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
                                            idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
-                                           pass);
+                                           pass, bb, bb_lg);
+                    if (bb) {
+                        B_HIP(hipStreamSynchronize(st));
+                        hipFree(bb);
+                    }
                     idx->nb_spec = full ? 1 : 0;
                     idx->device_bytes += n * 3 * wb;
                 }
