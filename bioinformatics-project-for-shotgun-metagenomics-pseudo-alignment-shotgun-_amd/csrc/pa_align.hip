@@ -701,18 +701,22 @@ pa_status ensure_workspace(pa_index *idx, size_t bytes) {
     return PA_OK;
 }
 
+pa_status reserve_queues(pa_index *idx, uint64_t n) {
+    if (idx->queue_cap >= n) return PA_OK;
+    hipFree(idx->queue);
+    hipFree(idx->queue_hard);
+    idx->queue = idx->queue_hard = nullptr;
+    idx->queue_cap = 0;
+    PA_HIP(hipMalloc(&idx->queue, n * 4));
+    PA_HIP(hipMalloc(&idx->queue_hard, n * 4));
+    idx->queue_cap = n;
+    return PA_OK;
+}
+
 pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t base, pa_result *acc,
                 hipStream_t st) {
     if (r->n == 0) return PA_OK;
-    if (idx->queue_cap < r->n) {
-        hipFree(idx->queue);
-        hipFree(idx->queue_hard);
-        idx->queue = idx->queue_hard = nullptr;
-        idx->queue_cap = 0;
-        PA_HIP(hipMalloc(&idx->queue, r->n * 4));
-        PA_HIP(hipMalloc(&idx->queue_hard, r->n * 4));
-        idx->queue_cap = r->n;
-    }
+    PA_TRY(reserve_queues(idx, r->n));
     AlignArgs a = make_args(idx, r, p, base);
     const uint32_t G = idx->n_genomes;
     a.stats = (unsigned long long *)acc->sum_block;

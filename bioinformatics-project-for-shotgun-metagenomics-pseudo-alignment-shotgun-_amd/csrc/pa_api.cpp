@@ -414,6 +414,20 @@ pa_status pa_align(const pa_index *idx, const pa_reads *reads, const pa_params *
     return pa::align(const_cast<pa_index *>(idx), reads, dp, read_index_base, acc, as_stream(stream));
 }
 
+pa_status pa_align_fastq_file(const pa_index *idx, const char *path, const pa_params *params,
+                              uint64_t read_index_base, pa_result *acc, int32_t threads, uint64_t window_bytes,
+                              void *stream, uint64_t *n_reads) {
+    PA_CHECK(idx && path && acc, PA_EINVAL, "NULL argument");
+    PA_CHECK(acc->n_genomes == idx->n_genomes, PA_EINVAL, "result was created for a different index");
+    PA_CHECK(acc->device == idx->device, PA_EINVAL, "index and result must live on the same device");
+    pa::DevParams dp;
+    PA_TRY(to_dev_params(params, idx->n_genomes, &dp));
+    PA_HIP(hipSetDevice(idx->device));
+    if (n_reads) *n_reads = 0;
+    return pa::align_fastq_file(const_cast<pa_index *>(idx), path, dp, read_index_base, acc, threads > 0 ? threads : 8,
+                                window_bytes ? window_bytes : (128ull << 20), as_stream(stream), n_reads);
+}
+
 pa_status pa_align_detail(const pa_index *idx, const pa_reads *reads, const pa_params *params, uint8_t *read_type,
                           uint32_t *filtered_kmers, uint32_t *redundant_kmers, uint64_t *list_off, uint32_t *lists,
                           uint64_t list_cap, uint64_t *list_total, void *stream) {

@@ -1,0 +1,548 @@
+// pa_fastq.hip -- FASTQ files parsed ON THE DEVICE, streamed into the align
+// pass (pa_align_fastq_file).
+//
+// The reference reads a whole FASTQ file into a str (src/data_file.py:117-158),
+// parses it with a regular expression (src/records.py:245-302) and aligns the
+// records one by one (src/kmer.py:600-620).  Here the host only moves bytes:
+// the file is read in windows (multi-threaded pread, or zlib for .gz) into
+// pinned buffers and copied to HBM on a copy stream, and the device does the
+// rest on the align stream, window after window while the host reads the next:
+//
+//   k_nl_count / scan / k_nl_write   line breaks of the window (4 KiB tiles,
+//                                    16 B per lane, coalesced)
+//   k_window_meta                    complete records in the window; the
+//                                    incomplete tail is carried into the next
+//   k_records                        per record: header / "+" / lengths, the
+//                                    id's hash into a device set (duplicates)
+//   scan, k_compact                  every byte checked against its line's
+//                                    class; sequence and quality bytes packed
+//                                    into the align path's columns (CSR)
+//   pa::align                        the window's reads (global read index =
+//                                    record index in the file)
+//
+// Accepted is a strict subset of the reference grammar: LF line ends only,
+// exactly four lines per record from the first byte on, "@" + id of bytes
+// 0x21-0x7E / space / tab that neither starts nor ends with space or tab,
+// a non-empty A C G T sequence, a "+" line, qualities 0x21-0x7E of the
+// sequence's length, one optional final line break, ids unique.  Inside it the
+// records are exactly the reference's; anything else -- a CRLF file, a "+id"
+// line, a blank line, a duplicate id -- returns PA_ENOTCANON and the caller
+// parses the file with the exact grammar (records.py), which reproduces the
+// reference's records or its exception.
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pa_device.h"
+#include "pa_internal.h"
+
+using namespace pad;
+
+namespace {
+
+constexpr int kTile = 4096;         // bytes per newline tile (256 lanes x 16 B)
+constexpr int kScanBlock = 1024;    // items per block of the three-phase scan
+constexpr uint64_t kCarryMax = 1ull << 20;  // longest record carried between windows
+constexpr uint32_t kErrGrammar = 1u, kErrDup = 2u, kErrSet = 4u;
+
+struct Meta {                 // window bookkeeping, device -> host once per window
+    unsigned long long n_nl;  // line breaks in the window
+    unsigned long long n_rec; // complete records
+    unsigned long long end;   // first byte after the last complete record (absolute)
+    unsigned long long max_len;
+    unsigned long long err;
+};
+
+// Per-byte "is a line feed" bits of a dword, in [lo, hi) of absolute positions.
+__device__ __forceinline__ uint32_t lf_bits(uint32_t x, uint64_t p, uint64_t lo, uint64_t hi) {
+    const uint32_t v = x ^ 0x0A0A0A0Au;
+    const uint32_t z = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);  // 0x80 in every zero byte
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) m |= ((z >> (8 * b + 7)) & 1u) << b;
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+        if (p + b < lo || p + b >= hi) m &= ~(1u << b);
+    return m;
+}
+
+// 16 line-feed bits of the lane's chunk (bit j <-> byte 16 t + j of the tile).
+__device__ __forceinline__ uint32_t chunk_lf(const uint8_t *D, uint64_t c0, uint64_t lo, uint64_t hi) {
+    if (c0 + 16 <= lo || c0 >= hi) return 0u;
+    const uint4 v = *(const uint4 *)(D + c0);
+    return lf_bits(v.x, c0, lo, hi) | (lf_bits(v.y, c0 + 4, lo, hi) << 4) | (lf_bits(v.z, c0 + 8, lo, hi) << 8) |
+           (lf_bits(v.w, c0 + 12, lo, hi) << 12);
+}
+
+// Block-wide exclusive scan of one uint32 per thread (256 threads); *total = sum.
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_wave, uint32_t &total) {
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) s_wave[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        before += i < wv ? s_wave[i] : 0u;
+        total += s_wave[i];
+    }
+    __syncthreads();
+    return before + incl - v;
+}
+
+__global__ __launch_bounds__(256) void k_nl_count(const uint8_t *D, uint64_t t0, uint64_t lo, uint64_t hi,
+                                                  uint32_t *tile_cnt) {
+    __shared__ uint32_t s_wave[4];
+    const uint64_t c0 = t0 + (uint64_t)blockIdx.x * kTile + 16 * threadIdx.x;
+    const uint32_t c = __popc(chunk_lf(D, c0, lo, hi));
+    uint32_t total;
+    block_excl_scan256(c, s_wave, total);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_nl_write(const uint8_t *D, uint64_t t0, uint64_t lo, uint64_t hi,
+                                                  const unsigned long long *tile_off, uint32_t *nl) {
+    __shared__ uint32_t s_wave[4];
+    const uint64_t c0 = t0 + (uint64_t)blockIdx.x * kTile + 16 * threadIdx.x;
+    uint32_t m = chunk_lf(D, c0, lo, hi);
+    uint32_t total;
+    uint64_t o = tile_off[blockIdx.x] + block_excl_scan256(__popc(m), s_wave, total);
+    while (m) {
+        const int j = __builtin_ctz(m);
+        m &= m - 1;
+        nl[o++] = (uint32_t)(c0 + j);
+    }
+}
+
+// Three-phase exclusive scan of n uint32 (in) into n + 1 uint64 (out[n] = sum).
+__global__ __launch_bounds__(256) void k_scan_sums(const uint32_t *in, uint64_t n, unsigned long long *bsum) {
+    __shared__ unsigned long long s[4];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+    unsigned long long v = 0;
+    for (uint32_t i = threadIdx.x; i < kScanBlock; i += 256)
+        if (b0 + i < n) v += in[b0 + i];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    if (lane_id() == 0) s[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ __launch_bounds__(1024) void k_scan_blocks(unsigned long long *bsum, uint64_t nb,
+                                                      unsigned long long *total) {
+    __shared__ unsigned long long s[1024];
+    const uint64_t per = (nb + 1023) / 1024;
+    const uint64_t a = threadIdx.x * per, e = min(nb, a + per);
+    unsigned long long v = 0;
+    for (uint64_t i = a; i < e; i++) v += bsum[i];
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const unsigned long long x = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0ull;
+        __syncthreads();
+        s[threadIdx.x] += x;
+        __syncthreads();
+    }
+    unsigned long long run = s[threadIdx.x] - v;
+    for (uint64_t i = a; i < e; i++) {
+        const unsigned long long x = bsum[i];
+        bsum[i] = run;
+        run += x;
+    }
+    if (threadIdx.x == 1023) *total = s[1023];
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t *in, uint64_t n, const unsigned long long *bsum,
+                                                    unsigned long long *out) {
+    __shared__ uint32_t s_wave[4];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+    unsigned long long run = bsum[blockIdx.x];
+    for (uint32_t c = 0; c < kScanBlock; c += 256) {
+        const uint64_t i = b0 + c + threadIdx.x;
+        const uint32_t v = i < n ? in[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_excl_scan256(v, s_wave, total);
+        if (i < n) out[i] = run + ex;
+        run += total;
+    }
+    if (b0 + kScanBlock >= n && threadIdx.x == 0) out[n] = run;
+}
+
+// Complete records of the window: the last window may end without a line
+// feed (one optional final line break); any other window ends at the line
+// feed of its last complete record, the rest is carried.
+__global__ void k_window_meta(const uint8_t *D, uint64_t lo, uint64_t hi, int last, uint32_t *nl,
+                              const unsigned long long *n_nl, Meta *meta) {
+    if (threadIdx.x || blockIdx.x) return;
+    uint64_t lines = *n_nl;
+    meta->n_nl = lines;
+    uint64_t end = lo;
+    if (last) {
+        if (hi > lo && D[hi - 1] != '\n') nl[lines++] = (uint32_t)hi;  // the final line, no line feed
+        if (lines % 4) meta->err |= kErrGrammar;
+        end = hi;
+    } else if (lines >= 4) {
+        end = (uint64_t)nl[(lines / 4) * 4 - 1] + 1;
+    }
+    meta->n_rec = lines / 4;
+    meta->end = end;
+}
+
+__device__ __forceinline__ bool id_byte(uint8_t c) { return c >= 0x21 && c <= 0x7E; }
+
+// One record per thread: header, "+" line, lengths, the id's hash.
+__global__ void k_records(const uint8_t *D, uint64_t lo, const uint32_t *nl, const Meta *meta, uint32_t *len,
+                          unsigned long long *ids, uint64_t ids_cap, Meta *meta_out) {
+    const uint64_t R = meta->n_rec;
+    uint32_t bad = 0, mx = 0;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t hs = r ? (uint64_t)nl[4 * r - 1] + 1 : lo, he = nl[4 * r];
+        const uint64_t ss = he + 1, se = nl[4 * r + 1], ps = se + 1, pe = nl[4 * r + 2], qs = pe + 1,
+                       qe = nl[4 * r + 3];
+        const uint64_t n = se - ss;
+        bool ok = he >= hs + 2 && D[hs] == '@' && id_byte(D[hs + 1]) && id_byte(D[he - 1]);
+        ok = ok && n >= 1 && pe == ps + 1 && D[ps] == '+' && qe - qs == n && n < (1ull << 31);
+        // the id (the header without "@": no leading / trailing blank, so the
+        // reference's stripped identifier is these bytes): FNV-1a, mixed
+        uint64_t h = 0xCBF29CE484222325ull;
+        if (ok)
+            for (uint64_t p = hs + 1; p < he; p++) {
+                const uint8_t c = D[p];
+                ok = ok && (id_byte(c) || c == ' ' || c == '\t');
+                h = (h ^ c) * 0x100000001B3ull;
+            }
+        len[r] = ok ? (uint32_t)n : 0u;
+        if (!ok) {
+            bad |= kErrGrammar;
+            continue;
+        }
+        mx = max(mx, (uint32_t)n);
+        h = fmix64(h ^ (he - hs));
+        if (h == 0) h = 1;
+        uint64_t pos = h & (ids_cap - 1);
+        for (uint32_t it = 0;; it++) {
+            if (it >= 4096) {
+                bad |= kErrSet;
+                break;
+            }
+            const unsigned long long old = atomicCAS(&ids[pos], 0ull, (unsigned long long)h);
+            if (old == 0ull) break;
+            if (old == h) {  // the same id hash: a duplicate id (or a 2^-64 collision) -> the exact parser
+                bad |= kErrDup;
+                break;
+            }
+            pos = (pos + 1) & (ids_cap - 1);
+        }
+    }
+    if (bad) atomicOr(&meta_out->err, (unsigned long long)bad);
+    if (mx) atomicMax(&meta_out->max_len, (unsigned long long)mx);
+}
+
+// Every byte of the window's complete records against its line's class;
+// sequence and quality bytes to their columns.  Line index of a byte = line
+// feeds before it (tile offset + block scan + bits below it in the chunk).
+__global__ __launch_bounds__(256) void k_compact(const uint8_t *D, uint64_t t0, uint64_t lo, const Meta *meta,
+                                                 const unsigned long long *tile_off, const uint32_t *nl,
+                                                 const unsigned long long *rec_off, uint8_t *seq, uint8_t *qual,
+                                                 Meta *meta_out) {
+    __shared__ uint32_t s_wave[4];
+    const uint64_t hi = meta->end;
+    const uint64_t c0 = t0 + (uint64_t)blockIdx.x * kTile + 16 * threadIdx.x;
+    const uint32_t m = chunk_lf(D, c0, lo, hi);
+    uint32_t total;
+    const uint64_t li0 = tile_off[blockIdx.x] + block_excl_scan256(__popc(m), s_wave, total);
+    if (c0 + 16 <= lo || c0 >= hi) return;
+    const uint4 v = *(const uint4 *)(D + c0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint64_t li = li0;
+    uint64_t ls = li ? (uint64_t)nl[li - 1] + 1 : lo;  // start of the line holding byte c0 (or lo)
+    uint32_t bad = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint64_t p = c0 + j;
+        const uint8_t c = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+        if (p < lo || p >= hi) continue;
+        if ((m >> j) & 1u) {  // a line feed ends line li
+            li++;
+            ls = p + 1;
+            continue;
+        }
+        const uint32_t type = (uint32_t)(li & 3);
+        const uint64_t r = li >> 2, col = p - ls;
+        if (type == 1) {
+            if (!(c == 'A' || c == 'C' || c == 'G' || c == 'T')) bad = 1;
+            else if (rec_off[r] + col < rec_off[r + 1]) seq[rec_off[r] + col] = c;
+        } else if (type == 3) {
+            if (!id_byte(c)) bad = 1;
+            else if (rec_off[r] + col < rec_off[r + 1]) qual[rec_off[r] + col] = c;
+        }
+    }
+    if (bad) atomicOr(&meta_out->err, (unsigned long long)kErrGrammar);
+}
+
+struct Source {  // plain file (positional reads on host threads) or gzip stream
+    int fd = -1;
+    gzFile gz = nullptr;
+    uint64_t size = 0, pos = 0;
+    bool eof = false;
+    int threads = 8;
+
+    // Read up to n bytes into dst; returns the count, sets eof at the end.
+    bool read(uint8_t *dst, uint64_t n, uint64_t &got) {
+        got = 0;
+        if (gz) {
+            while (got < n) {
+                const int r = gzread(gz, dst + got, (unsigned)std::min<uint64_t>(n - got, 1u << 30));
+                if (r < 0) return false;
+                if (r == 0) {
+                    eof = true;
+                    break;
+                }
+                got += (uint64_t)r;
+            }
+            if (!eof && gzeof(gz)) eof = true;
+            return true;
+        }
+        const uint64_t want = std::min<uint64_t>(n, size - pos);
+        const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, want >> 22));
+        std::vector<std::thread> th;
+        std::vector<int> ok(nt, 1);
+        for (int t = 0; t < nt; t++)
+            th.emplace_back([&, t] {
+                uint64_t a = want * t / nt, e = want * (t + 1) / nt;
+                while (a < e) {
+                    const ssize_t r = pread(fd, dst + a, (size_t)std::min<uint64_t>(e - a, 1u << 30), (off_t)(pos + a));
+                    if (r <= 0) {
+                        ok[t] = 0;
+                        return;
+                    }
+                    a += (uint64_t)r;
+                }
+            });
+        for (auto &x : th) x.join();
+        for (int x : ok)
+            if (!x) return false;
+        pos += want;
+        got = want;
+        eof = pos >= size;
+        return true;
+    }
+};
+
+}  // namespace
+
+namespace pa {
+
+pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,
+                           int threads, uint64_t window, hipStream_t st, uint64_t *n_reads) {
+    Source src;
+    src.threads = std::max(1, threads);
+    {
+        const size_t pl = strlen(path);
+        const bool gz = pl >= 3 && strcmp(path + pl - 3, ".gz") == 0;
+        if (gz) {
+            src.gz = gzopen(path, "rb");
+            if (!src.gz) {
+                set_error(std::string("cannot open ") + path);
+                return PA_EIO;
+            }
+            gzbuffer(src.gz, 1 << 20);
+        } else {
+            src.fd = open(path, O_RDONLY);
+            struct stat sb;
+            if (src.fd < 0 || fstat(src.fd, &sb) != 0) {
+                if (src.fd >= 0) close(src.fd);
+                set_error(std::string("cannot open ") + path);
+                return PA_EIO;
+            }
+            src.size = (uint64_t)sb.st_size;
+        }
+    }
+    const uint64_t W = std::max<uint64_t>(window, 1 << 16) & ~(uint64_t)(kTile - 1);
+    const uint64_t dbytes = kCarryMax + W + 2 * kTile;       // one device text buffer
+    const uint64_t max_tiles = (kCarryMax + W) / kTile + 2;
+    const uint64_t max_nl = kCarryMax + W + 8;  // (a text of line feeds only: every byte)
+    const uint64_t max_rec = (kCarryMax + W) / 8 + 2;
+    const uint64_t est_rec = src.gz ? (1ull << 24) : src.size / 16 + 1024;
+    uint64_t ids_cap = 1024;
+    while (ids_cap < 2 * est_rec) ids_cap <<= 1;
+
+    uint8_t *H[2] = {nullptr, nullptr}, *D[2] = {nullptr, nullptr}, *seq = nullptr, *qual = nullptr;
+    uint32_t *tile_cnt = nullptr, *nl = nullptr, *len = nullptr;
+    unsigned long long *tile_off = nullptr, *bsum = nullptr, *rec_off = nullptr, *ids = nullptr, *tot = nullptr;
+    Meta *meta = nullptr, *h_meta = nullptr;
+    hipStream_t cs = nullptr;
+    hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_carry[2] = {nullptr, nullptr};
+    std::thread reader;
+    pa_status rc = PA_OK;
+    auto cleanup = [&]() {
+        if (reader.joinable()) reader.join();
+        if (cs) hipStreamSynchronize(cs);
+        hipStreamSynchronize(st);
+        for (int i = 0; i < 2; i++) {
+            hipHostFree(H[i]);
+            hipFree(D[i]);
+            if (ev_h2d[i]) hipEventDestroy(ev_h2d[i]);
+            if (ev_carry[i]) hipEventDestroy(ev_carry[i]);
+        }
+        hipFree(seq); hipFree(qual); hipFree(tile_cnt); hipFree(nl); hipFree(len); hipFree(tile_off);
+        hipFree(bsum); hipFree(rec_off); hipFree(ids); hipFree(tot); hipFree(meta);
+        hipHostFree(h_meta);
+        if (cs) hipStreamDestroy(cs);
+        if (src.gz) gzclose(src.gz);
+        if (src.fd >= 0) close(src.fd);
+    };
+#define F_HIP(call)                                                                                      \
+    do {                                                                                                 \
+        hipError_t e_ = (call);                                                                          \
+        if (e_ != hipSuccess) {                                                                          \
+            set_error(std::string("HIP error in pa_align_fastq_file: ") + hipGetErrorString(e_) + " (" #call ")"); \
+            cleanup();                                                                                   \
+            return e_ == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;                                   \
+        }                                                                                                \
+    } while (0)
+    for (int i = 0; i < 2; i++) {
+        F_HIP(hipHostMalloc((void **)&H[i], W, hipHostMallocDefault));
+        F_HIP(hipMalloc(&D[i], dbytes));
+        F_HIP(hipEventCreateWithFlags(&ev_h2d[i], hipEventDisableTiming));
+        F_HIP(hipEventCreateWithFlags(&ev_carry[i], hipEventDisableTiming));
+    }
+    F_HIP(hipMalloc(&seq, kCarryMax + W + kReadPad));
+    F_HIP(hipMalloc(&qual, kCarryMax + W + kReadPad));
+    F_HIP(hipMalloc(&tile_cnt, max_tiles * 4));
+    F_HIP(hipMalloc(&tile_off, (max_tiles + 1) * 8));
+    F_HIP(hipMalloc(&nl, max_nl * 4));
+    F_HIP(hipMalloc(&len, max_rec * 4));
+    F_HIP(hipMalloc(&rec_off, (max_rec + 1) * 8));
+    F_HIP(hipMalloc(&bsum, (std::max(max_tiles, max_rec) / kScanBlock + 2) * 8));
+    F_HIP(hipMalloc(&ids, ids_cap * 8));
+    F_HIP(hipMalloc(&tot, 8));
+    F_HIP(hipMalloc(&meta, sizeof(Meta)));
+    F_HIP(hipHostMalloc((void **)&h_meta, sizeof(Meta), hipHostMallocDefault));
+    F_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    F_HIP(hipMemsetAsync(ids, 0, ids_cap * 8, st));
+    F_HIP(hipMemsetAsync(meta, 0, sizeof(Meta), st));
+    // the index's align-side view and the align queues, while window 0 is read
+    uint64_t got_next = 0;
+    bool read_ok = true;
+    reader = std::thread([&] { read_ok = src.read(H[0], W, got_next); });
+    rc = index_prepare(idx, st);
+    if (rc == PA_OK) rc = reserve_queues(idx, max_rec);
+    if (rc != PA_OK) {
+        cleanup();
+        return rc;
+    }
+    reader.join();
+    if (!read_ok) {
+        set_error(std::string("read error in ") + path);
+        cleanup();
+        return PA_EIO;
+    }
+    uint64_t carry = 0, records = 0, prev_end = 0;
+    int cur = 0;
+    bool last = src.eof, fail_grammar = false;
+    uint64_t got = got_next;
+    F_HIP(hipMemcpyAsync(D[0] + kCarryMax, H[0], got, hipMemcpyHostToDevice, cs));
+    F_HIP(hipEventRecord(ev_h2d[0], cs));
+    for (uint64_t win = 0;; win++) {
+        // the host reads window win + 1 into the other pinned buffer meanwhile
+        const int nxt = cur ^ 1;
+        bool next_started = false;
+        if (!last) {
+            if (win > 0) F_HIP(hipEventSynchronize(ev_h2d[nxt]));  // its previous copy is done
+            reader = std::thread([&, nxt] { read_ok = src.read(H[nxt], W, got_next); });
+            next_started = true;
+        }
+        // this window's text: [lo, hi) of D[cur], the carried tail in front of it
+        const uint64_t lo = kCarryMax - carry, hi = kCarryMax + got, t0 = lo & ~15ull;
+        F_HIP(hipStreamWaitEvent(st, ev_h2d[cur], 0));
+        if (carry) F_HIP(hipMemcpyAsync(D[cur] + lo, D[nxt] + prev_end, carry, hipMemcpyDeviceToDevice, st));
+        F_HIP(hipEventRecord(ev_carry[cur], st));
+        if (hi == lo) break;  // (an empty last window: nothing after the previous records)
+        const uint64_t ntiles = (hi - t0 + kTile - 1) / kTile;
+        const unsigned sgrid = (unsigned)((ntiles + kScanBlock - 1) / kScanBlock);
+        F_HIP(hipMemsetAsync(meta, 0, offsetof(Meta, max_len), st));
+        hipLaunchKernelGGL(k_nl_count, dim3((unsigned)ntiles), dim3(256), 0, st, D[cur], t0, lo, hi, tile_cnt);
+        hipLaunchKernelGGL(k_scan_sums, dim3(sgrid), dim3(256), 0, st, tile_cnt, ntiles, bsum);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, bsum, (uint64_t)sgrid, tot);
+        hipLaunchKernelGGL(k_scan_apply, dim3(sgrid), dim3(256), 0, st, tile_cnt, ntiles, bsum, tile_off);
+        hipLaunchKernelGGL(k_nl_write, dim3((unsigned)ntiles), dim3(256), 0, st, D[cur], t0, lo, hi, tile_off, nl);
+        hipLaunchKernelGGL(k_window_meta, dim3(1), dim3(1), 0, st, D[cur], lo, hi, last ? 1 : 0, nl, tot, meta);
+        F_HIP(hipGetLastError());
+        F_HIP(hipMemcpyAsync(h_meta, meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
+        F_HIP(hipStreamSynchronize(st));
+        const uint64_t R = h_meta->n_rec, end = h_meta->end;
+        if (h_meta->err || (R == 0 && !last) || (!last && hi - end > kCarryMax) || R > max_rec) {
+            fail_grammar = true;  // (a record longer than the carry limit is left to the host parser too)
+            break;
+        }
+        if (R > 0) {
+            const unsigned rgrid = (unsigned)std::min<uint64_t>((R + 255) / 256, 65536);
+            const unsigned lgrid = (unsigned)((R + kScanBlock - 1) / kScanBlock);
+            hipLaunchKernelGGL(k_records, dim3(rgrid), dim3(256), 0, st, D[cur], lo, nl, meta, len, ids, ids_cap, meta);
+            hipLaunchKernelGGL(k_scan_sums, dim3(lgrid), dim3(256), 0, st, len, R, bsum);
+            hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, bsum, (uint64_t)lgrid, tot);
+            hipLaunchKernelGGL(k_scan_apply, dim3(lgrid), dim3(256), 0, st, len, R, bsum, rec_off);
+            hipLaunchKernelGGL(k_compact, dim3((unsigned)((end - t0 + kTile - 1) / kTile)), dim3(256), 0, st, D[cur],
+                               t0, lo, meta, tile_off, nl, rec_off, seq, qual, meta);
+            F_HIP(hipGetLastError());
+            F_HIP(hipMemcpyAsync(h_meta, meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
+            F_HIP(hipStreamSynchronize(st));
+            if (h_meta->err) {
+                fail_grammar = true;
+                break;
+            }
+            pa_reads r{};
+            r.device = idx->device;
+            r.n = R;
+            r.n_bases = 0;  // (not read by the align path)
+            r.max_len = (uint32_t)h_meta->max_len;
+            r.seq = seq;
+            r.qual = qual;
+            r.off = (uint64_t *)rec_off;
+            rc = align(idx, &r, prm, base + records, acc, st);
+            if (rc != PA_OK) break;
+            records += R;
+        }
+        if (last) break;
+        carry = hi - end;
+        prev_end = end;
+        // the next window's copy waits for this window's carry copy (which reads D[cur]'s tail later
+        // only from the next window's perspective: D[nxt] is rewritten next)
+        if (next_started) {
+            reader.join();
+            if (!read_ok) {
+                set_error(std::string("read error in ") + path);
+                rc = PA_EIO;
+                break;
+            }
+            got = got_next;
+            last = src.eof;
+            F_HIP(hipStreamWaitEvent(cs, ev_carry[cur], 0));
+            F_HIP(hipMemcpyAsync(D[nxt] + kCarryMax, H[nxt], got, hipMemcpyHostToDevice, cs));
+            F_HIP(hipEventRecord(ev_h2d[nxt], cs));
+        }
+        cur = nxt;
+    }
+#undef F_HIP
+    if (reader.joinable()) reader.join();
+    if (rc == PA_OK && records == 0) fail_grammar = true;  // no records: the exact parser raises
+    if (rc == PA_OK && fail_grammar) {
+        set_error("FASTQ file outside the device-parsed subset of the grammar (or a duplicate id)");
+        rc = PA_ENOTCANON;
+    }
+    if (rc == PA_OK && n_reads) *n_reads = records;
+    cleanup();
+    return rc;
+}
+
+}  // namespace pa

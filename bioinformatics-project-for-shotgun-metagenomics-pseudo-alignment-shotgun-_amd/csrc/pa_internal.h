@@ -144,6 +144,9 @@ pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uin
                        uint32_t *hr, uint64_t *list_off, uint32_t *lists, uint64_t list_cap, uint64_t *list_total,
                        hipStream_t st);
 pa_status ensure_workspace(pa_index *idx, size_t bytes);
+pa_status reserve_queues(pa_index *idx, uint64_t n);  // align queues for batches of up to n reads
+pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,
+                           int threads, uint64_t window, hipStream_t st, uint64_t *n_reads);
 pa_status result_reset(pa_result *res, hipStream_t st);
 void index_release(pa_index *idx);
 }  // namespace pa

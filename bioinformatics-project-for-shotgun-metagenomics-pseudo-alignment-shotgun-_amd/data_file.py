@@ -28,12 +28,16 @@ class DataFile:
     EXTENSIONS: Optional[Set[str]] = None
 
     def __init__(self, file_path: str) -> None:
-        if not self.EXTENSIONS:
-            raise NotImplementedError("EXTENSIONS must be defined.")
-        if not any(file_path.endswith(ext) for ext in self.EXTENSIONS):
-            raise InvalidExtensionError(f"Invalid file extension. Expected one of {self.EXTENSIONS}, got {file_path}")
+        self.check_extension(file_path)
         self.container: RecordContainer = self.get_container_type()
         self.parse_file(file_path)
+
+    @classmethod
+    def check_extension(cls, file_path: str) -> None:
+        if not cls.EXTENSIONS:
+            raise NotImplementedError("EXTENSIONS must be defined.")
+        if not any(file_path.endswith(ext) for ext in cls.EXTENSIONS):
+            raise InvalidExtensionError(f"Invalid file extension. Expected one of {cls.EXTENSIONS}, got {file_path}")
 
     def get_container_type(self) -> RecordContainer:
         raise NotImplementedError("This method must be implemented in subclasses.")

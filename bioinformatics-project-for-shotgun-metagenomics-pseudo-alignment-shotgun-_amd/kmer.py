@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import gzip
 import json
+import os
 import pickle
 from collections import defaultdict, namedtuple
 from enum import Enum
@@ -368,8 +369,12 @@ class _Batch:
         self.base, self.ids, self.seq, self.qual, self.off, self.params = base, ids, seq, qual, off, params
         self.mrq, self.all_dropped, self.entries, self._dropped = mrq, all_dropped, None, None
 
+    def load(self) -> None:
+        pass
+
     def dropped(self) -> Optional[np.ndarray]:
         """Reads dropped by --min-read-quality (not in PseudoAlignment.reads), or None if none can be."""
+        self.load()
         if self.all_dropped:
             return np.ones(len(self.ids), dtype=bool)
         if self.mrq is None:
@@ -377,6 +382,23 @@ class _Batch:
         if self._dropped is None:
             self._dropped = _dropped_mask(self.qual, self.off, self.mrq)
         return self._dropped
+
+
+class _FileBatch(_Batch):
+    """A FASTQ file aligned by pa_align_fastq_file: its columns (ids, bases,
+    qualities) are parsed from the file only when per-read results or ids are
+    asked for."""
+
+    __slots__ = ("path", "n")
+
+    def __init__(self, base, path, params, mrq, n):
+        super().__init__(base, None, None, None, None, params, mrq)
+        self.path, self.n = path, n
+
+    def load(self) -> None:
+        if self.ids is None:
+            from data_file import FASTAQFile
+            self.ids, self.seq, self.qual, self.off = _columnar(FASTAQFile(self.path).container)
 
 
 def _dropped_mask(qual: np.ndarray, off: np.ndarray, mrq) -> np.ndarray:
@@ -435,7 +457,7 @@ class PseudoAlignment:
         if self._ids is None:
             ids: Set[str] = set()
             for b in self._batches:
-                d = b.dropped()
+                d = b.dropped()  # (loads a file batch's columns)
                 ids.update(b.ids if d is None else (i for i, x in zip(b.ids, d) if not x))
             ids.update(i for _, i, _ in self._host)
             self._ids = ids
@@ -480,6 +502,46 @@ class PseudoAlignment:
         ids, seq, qual, off = _columnar(reads_container)
         self._align_columns(ids, seq, qual, off, m, p, min_read_quality, min_kmer_quality, max_genomes,
                             unique_batch=isinstance(reads_container, FASTAQRecordContainer))
+
+    def align_reads_from_file(self, reads_file: str, m: int = 1, p: int = 1, min_read_quality: Optional[int] = None,
+                              min_kmer_quality: Optional[int] = None, max_genomes: Optional[int] = None) -> None:
+        """FASTAQFile(reads_file).container + align_reads_from_container as one
+        device pass (pa_align_fastq_file: the file is parsed on the GPU and
+        aligned in windows while the host reads the next).  Per-read results
+        (``reads``) parse the file again when asked for.  A file outside the
+        device-parsed subset of the grammar, a duplicate id, arguments the
+        reference rejects, or reads already added take the exact path."""
+        from data_file import FASTAQFile
+        fresh = not self._batches and not self._host and self._result is None
+        err = _check_align_args(self.kmer_reference, m, p, min_read_quality, min_kmer_quality, max_genomes)
+        n = None
+        if fresh and err is None and os.environ.get("PA_STREAM", "1") != "0":
+            FASTAQFile.check_extension(reads_file)
+            ref = self.kmer_reference
+            result = N.Result(ref.index)
+            prm = N.Params.make(m, p, min_read_quality, min_kmer_quality, max_genomes)
+            n = N.align_fastq_file(ref.index, reads_file, prm, self._next_index, result)
+            if n is None:
+                result.close()
+        if n is None:
+            self.align_reads_from_container(FASTAQFile(reads_file).container, m, p, min_read_quality,
+                                            min_kmer_quality, max_genomes)
+            return
+        if min_read_quality is not None:
+            self.filter_read_quality_flag = True
+        if min_kmer_quality is not None:
+            self.filter_kmer_quality_flag = True
+        if max_genomes is not None:
+            self.filter_max_genomes_flag = True
+        self._result = result
+        stats, _, _, _ = result.fetch()
+        self._gpu_stats = stats
+        self.filtered_quality_reads += int(stats[3])
+        self.filtered_quality_kmers += int(stats[4])
+        self.filtered_hr_kmers += int(stats[5])
+        self._batches.append(_FileBatch(self._next_index, reads_file, prm, min_read_quality, n))
+        self._next_index += n
+        self._streamed_records = n  # (diagnostics: the device-parsed path was taken)
 
     def _align_columns(self, ids, seq, qual, off, m, p, mrq, mkq, mg, unique_batch=False) -> None:
         n = len(ids)
@@ -542,6 +604,7 @@ class PseudoAlignment:
             if b.all_dropped:
                 continue
             if b.entries is None:
+                b.load()
                 reads = N.Reads.upload(b.seq, b.qual, b.off, device=ref.index.device)
                 types, _, _, loff, lists = N.align_detail(ref.index, reads, b.params)
                 reads.close()

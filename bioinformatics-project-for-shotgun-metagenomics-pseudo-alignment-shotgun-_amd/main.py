@@ -82,9 +82,12 @@ def create_reference(fasta_file: str, kmer_size: int, filter_similar: bool = Fal
 
 def create_alignment_from_reference(kmer_reference: KmerReference, reads_file: str, m: int, p: int,
                                     min_read_quality, min_kmer_quality, max_genomes) -> PseudoAlignment:
-    reads = FASTAQFile(reads_file).container
+    # the FASTQ file goes straight to the device (parsed there, aligned in
+    # windows); a file outside that subset of the grammar is parsed the exact
+    # way (FASTAQFile), which also raises the reference's errors
+    FASTAQFile.check_extension(reads_file)
     alignment = PseudoAlignment(kmer_reference)
-    alignment.align_reads_from_container(reads, m, p, min_read_quality, min_kmer_quality, max_genomes)
+    alignment.align_reads_from_file(reads_file, m, p, min_read_quality, min_kmer_quality, max_genomes)
     return alignment
 
 

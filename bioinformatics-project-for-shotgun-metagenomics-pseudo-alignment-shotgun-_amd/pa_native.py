@@ -33,7 +33,7 @@ EXPORTS = (
     "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_reads_download", "pa_reads_free",
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
     "pa_result_copy_in", "pa_result_free",
-    "pa_align", "pa_align_detail", "pa_align_batch",
+    "pa_align", "pa_align_detail", "pa_align_batch", "pa_align_fastq_file",
     "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_counters_reduce",
     "pa_profile_enable", "pa_profile_read",
     "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free",
@@ -127,6 +127,8 @@ def lib():
         "pa_align": (I32, [P, P, ctypes.POINTER(Params), U64, P, P]),
         "pa_align_detail": (I32, [P, P, ctypes.POINTER(Params), P, P, P, P, P, U64, ctypes.POINTER(U64), P]),
         "pa_align_batch": (I32, [P, P, P, P, U64, U64, ctypes.POINTER(Params), ctypes.POINTER(Stats), P, P, P, P]),
+        "pa_align_fastq_file": (I32, [P, ctypes.c_char_p, ctypes.POINTER(Params), U64, P, I32, U64, P,
+                                      ctypes.POINTER(U64)]),
         "pa_comm_unique_id": (I32, [P]),
         "pa_comm_init": (I32, [I32, I32, I32, P, PP]),
         "pa_comm_free": (I32, [P]),
@@ -550,6 +552,25 @@ def counters_reduce(result: "Result", comm, stream=None) -> None:
 def align(index: Index, reads: Reads, params: Params, read_index_base: int, result: Result, stream=None) -> None:
     _check(lib().pa_align(index.handle, reads.handle, ctypes.byref(params), int(read_index_base), result.handle,
                           _stream(stream)))
+
+
+def align_fastq_file(index: Index, path: str, params: Params, read_index_base: int, result: Result,
+                     threads: Optional[int] = None, window_bytes: int = 0, stream=None) -> Optional[int]:
+    """pa_align_fastq_file: the FASTQ file parsed on the device and aligned in
+    windows; returns the number of records, or None when the file is outside
+    the device-parsed subset of the grammar (``result`` then holds a partial
+    sum: reset it and take the exact path)."""
+    n = U64(0)
+    if window_bytes <= 0:
+        env = os.environ.get("PA_STREAM_WINDOW")
+        window_bytes = int(env) if env and env.isdigit() else 0
+    st = lib().pa_align_fastq_file(index.handle, os.fsencode(path), ctypes.byref(params), int(read_index_base),
+                                   result.handle, int(threads or ingest_threads()), int(window_bytes),
+                                   _stream(stream), ctypes.byref(n))
+    if st == PA_ENOTCANON:
+        return None
+    _check(st)
+    return int(n.value)
 
 
 def align_detail(index: Index, reads: Reads, params: Params, stream=None):

@@ -19,6 +19,9 @@
  *                            genomes_mapped_to (PseudoAlignment.reads)      src/kmer.py:542, 551-561
  *   pa_result_fetch          PseudoAlignment.get_summary inputs             src/kmer.py:622-657
  *   pa_align_batch           one-shot host-buffer form of pa_align
+ *   pa_align_fastq_file      FASTAQFile + align_reads_from_container as one
+ *                            device-parsed stream                          src/data_file.py:134-158,
+ *                                                                          src/kmer.py:600-620
  *   pa_counters_reduce       the multi-GPU sum/min of PseudoAlignment counters
  *                            (read shards of one job); the
  *                            reference is single-process, so this has no
@@ -218,6 +221,22 @@ pa_status pa_align_detail(const pa_index *idx, const pa_reads *reads, const pa_p
 pa_status pa_align_batch(const pa_index *idx, const uint8_t *seq, const uint8_t *qual, const uint64_t *read_off,
                          uint64_t n_reads, uint64_t read_index_base, const pa_params *params, pa_stats *stats,
                          uint64_t *unique_reads, uint64_t *ambiguous_reads, uint64_t *first_key, void *stream);
+
+/* A FASTQ file straight into the align pass (FASTAQFile(path).container +
+ * PseudoAlignment.align_reads_from_container, src/data_file.py:134-158,
+ * src/records.py:245-302, src/kmer.py:600-620): the host reads the file in
+ * windows of window_bytes (0: 128 MiB; threads readers, or zlib for ".gz") into
+ * pinned buffers; the DEVICE finds the records, checks them against the
+ * grammar, hashes the ids into a duplicate set, packs the read columns and
+ * aligns each window while the host reads the next.  Record i of the file is
+ * global read read_index_base + i; *n_reads = records.  PA_ENOTCANON: the
+ * file is outside the device-parsed subset of the grammar (LF line ends, "+"
+ * lines, ids without outer blanks, see csrc/pa_fastq.hip), holds a duplicate
+ * id or no record -- `acc` then holds a partial sum: reset it and parse the
+ * file the exact way (which also raises the reference's errors). */
+pa_status pa_align_fastq_file(const pa_index *idx, const char *path, const pa_params *params,
+                              uint64_t read_index_base, pa_result *acc, int32_t threads, uint64_t window_bytes,
+                              void *stream, uint64_t *n_reads);
 
 /* ---- multi-GPU reduce (RCCL over xGMI) ------------------------------------------- */
 

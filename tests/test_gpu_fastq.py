@@ -1,0 +1,130 @@
+"""Device-parsed FASTQ files (pa_align_fastq_file, csrc/pa_fastq.hip) against
+the exact path (FASTAQFile(path).container + align_reads_from_container,
+src/data_file.py:134-158, src/records.py:245-302, src/kmer.py:600-620).
+
+Every file is aligned both ways through the drop-in API; the summaries must be
+identical (key order included), and files outside the device-parsed subset of
+the grammar must fall back to the exact path -- which raises the reference's
+own errors.  Small windows (PA_STREAM_WINDOW) make records straddle window
+boundaries (the carried tail)."""
+
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pa_native as N
+import synth
+from data_file import FASTAQFile
+from kmer import KmerReference, PseudoAlignment
+from records import FASTARecordContainer
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if N.device_count() < 1:
+        pytest.fail("no HIP device visible (no CPU fallback exists)")
+    gens = synth.family_genomes(8, 30000, seed=5, family_size=4, sub_rate=0.02, conserved_len=800)
+    c = FASTARecordContainer()
+    c.parse_records(synth.fasta_text([f"g{i} test genome" for i in range(len(gens))], gens, width=70))
+    return gens, KmerReference(31, c)
+
+
+def reads_text(gens, n, seed, lens=(150,), ids=None, plus="+", nl="\n", final_nl=True):
+    rng = np.random.default_rng(seed)
+    parts = []
+    for i in range(n):
+        L = int(lens[i % len(lens)])
+        seq, qual, _ = synth.sample_reads(gens, 1, L, seed=seed * 1000 + i, err_rate=0.02)
+        rid = ids[i] if ids is not None else f"r{i} len={L}"
+        parts.append(f"@{rid}{nl}{bytes(seq[0]).decode()}{nl}{plus}{nl}{bytes(qual[0]).decode()}")
+    return nl.join(parts) + (nl if final_nl else "")
+
+
+def both_ways(ref_obj, path, **kw):
+    a = PseudoAlignment(ref_obj)
+    a.align_reads_from_file(path, **kw)
+    b = PseudoAlignment(ref_obj)
+    b.align_reads_from_container(FASTAQFile(path).container, **kw)
+    return a, b
+
+
+PARAMS = [dict(), dict(m=2, p=0), dict(min_read_quality=58, min_kmer_quality=60, max_genomes=2)]
+
+
+@pytest.mark.parametrize("window", [0, 65536])
+@pytest.mark.parametrize("kw", PARAMS)
+def test_streamed_equals_exact(ref, tmp_path, monkeypatch, window, kw):
+    gens, r = ref
+    monkeypatch.setenv("PA_STREAM_WINDOW", str(window))
+    p = tmp_path / "reads.fq"
+    p.write_text(reads_text(gens, 3000, seed=11, lens=(150, 100, 31, 20, 176, 250)))
+    a, b = both_ways(r, str(p), **kw)
+    assert getattr(a, "_streamed_records", None) == 3000  # the device path was taken
+    assert json.dumps(a.get_summary(), indent=4) == json.dumps(b.get_summary(), indent=4)
+
+
+def test_streamed_reads_dict_and_gz(ref, tmp_path, monkeypatch):
+    gens, r = ref
+    monkeypatch.setenv("PA_STREAM_WINDOW", "65536")
+    text = reads_text(gens, 1500, seed=12, final_nl=False)
+    p = tmp_path / "reads.fq.gz"
+    with gzip.open(p, "wt") as f:
+        f.write(text)
+    a, b = both_ways(r, str(p), m=1, p=1)
+    assert getattr(a, "_streamed_records", None) == 1500
+    assert a.get_summary() == b.get_summary()
+    assert a.reads == b.reads  # per-read results: the file parsed again on demand
+
+
+@pytest.mark.parametrize("variant", ["crlf", "plus_id", "blank_end", "lead_space_id"])
+def test_outside_subset_falls_back(ref, tmp_path, variant):
+    gens, r = ref
+    if variant == "crlf":
+        text = reads_text(gens, 200, seed=13, nl="\r\n")
+    elif variant == "plus_id":
+        text = reads_text(gens, 200, seed=13, plus="+")
+        text = text.replace("\n+\n", "\n+ \n", 1)
+    elif variant == "blank_end":
+        text = reads_text(gens, 200, seed=13) + "\n"
+    else:
+        text = reads_text(gens, 200, seed=13, ids=[f" r{i}" for i in range(200)])
+    p = tmp_path / "reads.fq"
+    p.write_bytes(text.encode())
+    a = PseudoAlignment(r)
+    try:
+        a.align_reads_from_file(str(p))
+    except Exception as e:  # the exact path's verdict: the reference's exception
+        with pytest.raises(type(e)):
+            FASTAQFile(str(p))
+        return
+    assert getattr(a, "_streamed_records", None) is None
+    b = PseudoAlignment(r)
+    b.align_reads_from_container(FASTAQFile(str(p)).container)
+    assert a.get_summary() == b.get_summary()
+
+
+def test_duplicate_id_raises_reference_error(ref, tmp_path):
+    gens, r = ref
+    ids = [f"r{i}" for i in range(100)]
+    ids[77] = "r3"
+    p = tmp_path / "dup.fq"
+    p.write_text(reads_text(gens, 100, seed=14, ids=ids))
+    with pytest.raises(Exception) as ei:
+        PseudoAlignment(r).align_reads_from_file(str(p))
+    assert "Duplicate" in type(ei.value).__name__ or "uplicate" in str(ei.value)
+
+
+def test_empty_and_bad_extension(ref, tmp_path):
+    _, r = ref
+    p = tmp_path / "empty.fq"
+    p.write_text("")
+    with pytest.raises(Exception):
+        PseudoAlignment(r).align_reads_from_file(str(p))
+    with pytest.raises(Exception) as ei:
+        PseudoAlignment(r).align_reads_from_file(str(tmp_path / "reads.txt"))
+    assert type(ei.value).__name__ == "InvalidExtensionError"
