@@ -36,7 +36,10 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstddef>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -344,6 +347,14 @@ namespace pa {
 
 pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,
                            int threads, uint64_t window, hipStream_t st, uint64_t *n_reads) {
+    // PA_STREAM_TIMING=1: where the time goes (stderr)
+    const bool timing = std::getenv("PA_STREAM_TIMING") && std::getenv("PA_STREAM_TIMING")[0] == '1';
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t_start = now();
+    double t_alloc = 0, t_prepare = 0, t_wait_read = 0, t_wait_meta = 0, t_wait_rec = 0;
     Source src;
     src.threads = std::max(1, threads);
     {
@@ -431,17 +442,22 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
     F_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
     F_HIP(hipMemsetAsync(ids, 0, ids_cap * 8, st));
     F_HIP(hipMemsetAsync(meta, 0, sizeof(Meta), st));
+    t_alloc = ms(t_start, now());
     // the index's align-side view and the align queues, while window 0 is read
     uint64_t got_next = 0;
     bool read_ok = true;
     reader = std::thread([&] { read_ok = src.read(H[0], W, got_next); });
+    auto tw = now();
     rc = index_prepare(idx, st);
     if (rc == PA_OK) rc = reserve_queues(idx, max_rec);
     if (rc != PA_OK) {
         cleanup();
         return rc;
     }
+    t_prepare = ms(tw, now());
+    tw = now();
     reader.join();
+    t_wait_read += ms(tw, now());
     if (!read_ok) {
         set_error(std::string("read error in ") + path);
         cleanup();
@@ -479,7 +495,9 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         hipLaunchKernelGGL(k_window_meta, dim3(1), dim3(1), 0, st, D[cur], lo, hi, last ? 1 : 0, nl, tot, meta);
         F_HIP(hipGetLastError());
         F_HIP(hipMemcpyAsync(h_meta, meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
+        tw = now();
         F_HIP(hipStreamSynchronize(st));
+        t_wait_meta += ms(tw, now());
         const uint64_t R = h_meta->n_rec, end = h_meta->end;
         if (h_meta->err || (R == 0 && !last) || (!last && hi - end > kCarryMax) || R > max_rec) {
             fail_grammar = true;  // (a record longer than the carry limit is left to the host parser too)
@@ -496,7 +514,9 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
                                t0, lo, meta, tile_off, nl, rec_off, seq, qual, meta);
             F_HIP(hipGetLastError());
             F_HIP(hipMemcpyAsync(h_meta, meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
+            tw = now();
             F_HIP(hipStreamSynchronize(st));
+            t_wait_rec += ms(tw, now());
             if (h_meta->err) {
                 fail_grammar = true;
                 break;
@@ -519,7 +539,9 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         // the next window's copy waits for this window's carry copy (which reads D[cur]'s tail later
         // only from the next window's perspective: D[nxt] is rewritten next)
         if (next_started) {
+            tw = now();
             reader.join();
+            t_wait_read += ms(tw, now());
             if (!read_ok) {
                 set_error(std::string("read error in ") + path);
                 rc = PA_EIO;
@@ -541,7 +563,13 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         rc = PA_ENOTCANON;
     }
     if (rc == PA_OK && n_reads) *n_reads = records;
+    const auto t_c = now();
     cleanup();
+    if (timing)
+        fprintf(stderr, "[pa_stream] %llu records: alloc %.1f ms, index prepare %.1f ms, waits: reader %.1f, window "
+                        "meta %.1f, records %.1f ms; cleanup %.1f ms; total %.1f ms\n",
+                (unsigned long long)records, t_alloc, t_prepare, t_wait_read, t_wait_meta, t_wait_rec, ms(t_c, now()),
+                ms(t_start, now()));
     return rc;
 }
 

@@ -25,11 +25,21 @@ import gzip
 import json
 import os
 import sys
+import time
 from typing import List, Optional
+
+_T0 = time.perf_counter()
 
 from constants import DEFAULT_AMBIGUOUS_THRESHOLD, DEFAULT_SIMILARITY_THRESHOLD, DEFAULT_UNIQUE_THRESHOLD
 from data_file import FASTAFile, FASTAQFile, InvalidExtensionError, NoRecordsInDataFile
 from kmer import AddingExistingRead, KmerReference, NotValidatingUniqueMapping, PseudoAlignment
+
+_TIMING = os.environ.get("PA_CLI_TIMING") == "1"  # stage times on stderr (diagnostic)
+
+
+def _stage(name: str) -> None:
+    if _TIMING:
+        print(f"[pa_cli] {name}: {time.perf_counter() - _T0:.3f} s", file=sys.stderr, flush=True)
 
 
 def validate_file_readable(filepath: str, description: str) -> None:
@@ -76,6 +86,7 @@ def _load_reference(reference_file: str) -> KmerReference:
 def create_reference(fasta_file: str, kmer_size: int, filter_similar: bool = False,
                      similarity_threshold: float = 0.95) -> KmerReference:
     container = FASTAFile(fasta_file).container
+    _stage("fasta parsed")
     return KmerReference(kmer_size, container, filter_similar=filter_similar,
                          similarity_threshold=similarity_threshold)
 
@@ -86,8 +97,10 @@ def create_alignment_from_reference(kmer_reference: KmerReference, reads_file: s
     # windows); a file outside that subset of the grammar is parsed the exact
     # way (FASTAQFile), which also raises the reference's errors
     FASTAQFile.check_extension(reads_file)
+    _stage("reference built")
     alignment = PseudoAlignment(kmer_reference)
     alignment.align_reads_from_file(reads_file, m, p, min_read_quality, min_kmer_quality, max_genomes)
+    _stage("reads aligned")
     return alignment
 
 
@@ -172,6 +185,7 @@ def _run(args: argparse.Namespace) -> None:
 
 
 def main(argv: Optional[List[str]] = None) -> None:
+    _stage("imports done")
     args = parse_arguments(argv)
     _check_task(args)
     # falsy -> default, as src/main.py:337-342 (so -m 0 and -p 0 become 1)
@@ -183,6 +197,7 @@ def main(argv: Optional[List[str]] = None) -> None:
         args.similarity_threshold = DEFAULT_SIMILARITY_THRESHOLD
     try:
         _run(args)
+        _stage("printed")
     except gzip.BadGzipFile:
         sys.exit("Error: Incorrect format of input file.")
     except (InvalidExtensionError, NoRecordsInDataFile, NotValidatingUniqueMapping, AddingExistingRead,

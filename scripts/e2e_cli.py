@@ -102,15 +102,23 @@ def main():
     host_equal = json.dumps(pb.get_summary(), indent=4) == summary
     del rc, pb
 
+    cmd = [sys.executable, os.path.join(PKG, "main.py"), "-t", "dumpalign", "-g", fa, "-k", "31", "--reads", fq]
     t = time.perf_counter()
-    r = subprocess.run([sys.executable, os.path.join(PKG, "main.py"), "-t", "dumpalign", "-g", fa, "-k", "31",
-                        "--reads", fq], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     cli_s = time.perf_counter() - t
+    # the same command again with stage times on stderr (not the timed run)
+    t = time.perf_counter()
+    rt = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                        env=dict(os.environ, PA_CLI_TIMING="1", PA_STREAM_TIMING="1"))
+    stages = {"wall_s": time.perf_counter() - t, "stderr": rt.stderr.strip().splitlines()[-12:]}
+    t = time.perf_counter()
+    subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); import main" % PKG])
+    stages["python_and_imports_s"] = time.perf_counter() - t
     out = {"workload": f"dumpalign C2: 50 x 2 Mbp FASTA, {args.reads} x 150 bp FASTQ, k=31",
            "fastq_bytes": os.path.getsize(fq), "cli_wall_s": cli_s, "cli_reads_per_s": args.reads / cli_s,
            "cli_rc": r.returncode, "cli_stdout_equals_api": r.stdout == summary + "\n",
            "device_parse_path_taken": streamed, "host_path_summary_equal": host_equal,
-           "phases": ph, "ingest_threads": N.ingest_threads(),
+           "phases": ph, "cli_stages": stages, "ingest_threads": N.ingest_threads(),
            "fastq_device_parse_align_GBps": os.path.getsize(fq) / ph["fastq_device_parse_align_s"] / 1e9,
            "fastq_host_parse_GBps": os.path.getsize(fq) / ph["host_parse_fastq_s"] / 1e9}
     if r.returncode:
