@@ -716,6 +716,7 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
 pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t base, pa_result *acc,
                 hipStream_t st) {
     if (r->n == 0) return PA_OK;
+    PA_TRY(index_note_reads(idx, r->n, st));  // (the neighbour bits, once enough reads came)
     PA_TRY(reserve_queues(idx, r->n));
     AlignArgs a = make_args(idx, r, p, base);
     const uint32_t G = idx->n_genomes;

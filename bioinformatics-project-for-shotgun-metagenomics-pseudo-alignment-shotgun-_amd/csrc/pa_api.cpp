@@ -14,6 +14,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pa_internal.h"
@@ -59,6 +60,24 @@ extern "C" {
 const char *pa_last_error(void) { return pa::g_err.c_str(); }
 
 const char *pa_version(void) { return "libpa 0.1 (gfx950)"; }
+
+namespace {
+struct RuntimeStarter {  // joined at exit, before the HIP runtime's own teardown (it was loaded first)
+    std::thread th;
+    ~RuntimeStarter() {
+        if (th.joinable()) th.join();
+    }
+};
+RuntimeStarter g_runtime_starter;
+}  // namespace
+
+pa_status pa_runtime_start(int32_t device) {
+    if (g_runtime_starter.th.joinable()) return PA_OK;
+    g_runtime_starter.th = std::thread([device] {
+        if (hipSetDevice(device) == hipSuccess) hipFree(nullptr);
+    });
+    return PA_OK;
+}
 
 pa_status pa_device_count(int32_t *n) {
     PA_CHECK(n != nullptr, PA_EINVAL, "n must not be NULL");
@@ -426,6 +445,44 @@ pa_status pa_align_fastq_file(const pa_index *idx, const char *path, const pa_pa
     if (n_reads) *n_reads = 0;
     return pa::align_fastq_file(const_cast<pa_index *>(idx), path, dp, read_index_base, acc, threads > 0 ? threads : 8,
                                 window_bytes ? window_bytes : (128ull << 20), as_stream(stream), n_reads);
+}
+
+pa_status pa_index_dumpref(const pa_index *idx, const uint8_t *keep, const uint32_t *desc_of, uint32_t n_desc,
+                           const char *const *desc_json, int32_t fd, int32_t threads, uint64_t *desc_unique,
+                           uint64_t *desc_multi, uint64_t *desc_order, uint32_t *desc_last_genome, uint64_t *n_kmers) {
+    PA_CHECK(idx && desc_of && desc_json && desc_unique && desc_multi && desc_order && desc_last_genome, PA_EINVAL,
+             "NULL argument");
+    PA_CHECK(fd >= 0, PA_EINVAL, "bad file descriptor");
+    for (uint32_t d = 0; d < n_desc; d++) PA_CHECK(desc_json[d], PA_EINVAL, "NULL description");
+    PA_HIP(hipSetDevice(idx->device));
+    return pa::index_dumpref(idx, keep, desc_of, n_desc, desc_json, fd, threads > 0 ? threads : 8, desc_unique,
+                             desc_multi, desc_order, desc_last_genome, n_kmers, nullptr);
+}
+
+pa_status pa_fastq_prefetch_start(const char *path, int32_t device, int32_t threads, uint64_t window_bytes,
+                                  pa_fastq_prefetch **out) {
+    PA_CHECK(path && out, PA_EINVAL, "NULL argument");
+    *out = nullptr;
+    PA_CHECK(device >= 0, PA_EINVAL, "no such device");
+    // (no HIP call here: the runtime starts on the prefetch thread, beside the caller's FASTA parse;
+    // a bad device is reported by pa_align_fastq_prefetched)
+    return pa::fastq_prefetch_start(path, device, threads > 0 ? threads : 8,
+                                    window_bytes ? window_bytes : (128ull << 20), out);
+}
+
+void pa_fastq_prefetch_free(pa_fastq_prefetch *pf) { pa::fastq_prefetch_free(pf); }
+
+pa_status pa_align_fastq_prefetched(const pa_index *idx, pa_fastq_prefetch *pf, const pa_params *params,
+                                    uint64_t read_index_base, pa_result *acc, void *stream, uint64_t *n_reads) {
+    PA_CHECK(idx && pf && acc, PA_EINVAL, "NULL argument");
+    PA_CHECK(acc->n_genomes == idx->n_genomes, PA_EINVAL, "result was created for a different index");
+    PA_CHECK(acc->device == idx->device, PA_EINVAL, "index and result must live on the same device");
+    pa::DevParams dp;
+    PA_TRY(to_dev_params(params, idx->n_genomes, &dp));
+    PA_HIP(hipSetDevice(idx->device));
+    if (n_reads) *n_reads = 0;
+    return pa::align_fastq_prefetched(const_cast<pa_index *>(idx), pf, dp, read_index_base, acc, as_stream(stream),
+                                      n_reads);
 }
 
 pa_status pa_align_detail(const pa_index *idx, const pa_reads *reads, const pa_params *params, uint8_t *read_type,

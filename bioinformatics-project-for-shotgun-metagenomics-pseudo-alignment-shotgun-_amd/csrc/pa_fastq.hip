@@ -41,6 +41,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -345,10 +347,399 @@ struct Source {  // plain file (positional reads on host threads) or gzip stream
 
 namespace pa {
 
+// Device buffers of the per-window parse (sized for windows of up to `span`
+// bytes of text) and the id set of the whole file.
+struct ParseBufs {
+    uint8_t *seq = nullptr, *qual = nullptr;
+    uint32_t *tile_cnt = nullptr, *nl = nullptr, *len = nullptr;
+    unsigned long long *tile_off = nullptr, *bsum = nullptr, *rec_off = nullptr, *ids = nullptr, *tot = nullptr;
+    Meta *meta = nullptr, *h_meta = nullptr;
+    uint64_t ids_cap = 0, max_rec = 0;
+
+    hipError_t alloc(uint64_t span, uint64_t est_rec, hipStream_t st) {
+        const uint64_t max_tiles = span / kTile + 2;
+        const uint64_t max_nl = span + 8;  // (a text of line feeds only: every byte)
+        max_rec = span / 8 + 2;
+        ids_cap = 1024;
+        while (ids_cap < 2 * est_rec) ids_cap <<= 1;
+        hipError_t e = hipSuccess;
+        auto m = [&](void **p, uint64_t b) {
+            if (e == hipSuccess) e = hipMalloc(p, b);
+        };
+        m((void **)&seq, span + kReadPad);
+        m((void **)&qual, span + kReadPad);
+        m((void **)&tile_cnt, max_tiles * 4);
+        m((void **)&tile_off, (max_tiles + 1) * 8);
+        m((void **)&nl, max_nl * 4);
+        m((void **)&len, max_rec * 4);
+        m((void **)&rec_off, (max_rec + 1) * 8);
+        m((void **)&bsum, (std::max(max_tiles, max_rec) / kScanBlock + 2) * 8);
+        m((void **)&ids, ids_cap * 8);
+        m((void **)&tot, 8);
+        m((void **)&meta, sizeof(Meta));
+        if (e == hipSuccess) e = hipHostMalloc((void **)&h_meta, sizeof(Meta), hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMemsetAsync(ids, 0, ids_cap * 8, st);
+        if (e == hipSuccess) e = hipMemsetAsync(meta, 0, sizeof(Meta), st);
+        return e;
+    }
+    void release() {
+        hipFree(seq); hipFree(qual); hipFree(tile_cnt); hipFree(nl); hipFree(len); hipFree(tile_off);
+        hipFree(bsum); hipFree(rec_off); hipFree(ids); hipFree(tot); hipFree(meta);
+        hipHostFree(h_meta);
+        *this = ParseBufs{};
+    }
+};
+
+// Window outcome: records aligned, the end of the last complete record, or a
+// reason to leave the file to the exact host parser.
+struct WindowOut {
+    uint64_t records = 0, end = 0;
+    bool fail = false;
+};
+
+// Parse the text [lo, hi) of D (t0 = lo & ~15; `last`: the file ends at hi)
+// and align its complete records as global reads base, base + 1, ...
+// Host waits: the window's record count (one sync), then the grammar flags of
+// its bytes (a second one).
+pa_status parse_align_window(ParseBufs &B, const uint8_t *D, uint64_t lo, uint64_t hi, bool last, pa_index *idx,
+                             const DevParams &prm, uint64_t base, pa_result *acc, hipStream_t st, WindowOut &out,
+                             double *t_meta, double *t_rec) {
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    out = WindowOut{};
+    out.end = lo;
+    const uint64_t t0 = lo & ~15ull;
+    const uint64_t ntiles = (hi - t0 + kTile - 1) / kTile;
+    const unsigned sgrid = (unsigned)((ntiles + kScanBlock - 1) / kScanBlock);
+    PA_HIP(hipMemsetAsync(B.meta, 0, offsetof(Meta, max_len), st));
+    hipLaunchKernelGGL(k_nl_count, dim3((unsigned)ntiles), dim3(256), 0, st, D, t0, lo, hi, B.tile_cnt);
+    hipLaunchKernelGGL(k_scan_sums, dim3(sgrid), dim3(256), 0, st, B.tile_cnt, ntiles, B.bsum);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, B.bsum, (uint64_t)sgrid, B.tot);
+    hipLaunchKernelGGL(k_scan_apply, dim3(sgrid), dim3(256), 0, st, B.tile_cnt, ntiles, B.bsum, B.tile_off);
+    hipLaunchKernelGGL(k_nl_write, dim3((unsigned)ntiles), dim3(256), 0, st, D, t0, lo, hi, B.tile_off, B.nl);
+    hipLaunchKernelGGL(k_window_meta, dim3(1), dim3(1), 0, st, D, lo, hi, last ? 1 : 0, B.nl, B.tot, B.meta);
+    PA_HIP(hipGetLastError());
+    PA_HIP(hipMemcpyAsync(B.h_meta, B.meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
+    auto tw = now();
+    PA_HIP(hipStreamSynchronize(st));
+    *t_meta += ms(tw, now());
+    const uint64_t R = B.h_meta->n_rec, end = B.h_meta->end;
+    if (B.h_meta->err || (R == 0 && !last) || R > B.max_rec) {
+        out.fail = true;
+        return PA_OK;
+    }
+    out.end = end;
+    if (R == 0) return PA_OK;
+    const unsigned rgrid = (unsigned)std::min<uint64_t>((R + 255) / 256, 65536);
+    const unsigned lgrid = (unsigned)((R + kScanBlock - 1) / kScanBlock);
+    hipLaunchKernelGGL(k_records, dim3(rgrid), dim3(256), 0, st, D, lo, B.nl, B.meta, B.len, B.ids, B.ids_cap, B.meta);
+    hipLaunchKernelGGL(k_scan_sums, dim3(lgrid), dim3(256), 0, st, B.len, R, B.bsum);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, B.bsum, (uint64_t)lgrid, B.tot);
+    hipLaunchKernelGGL(k_scan_apply, dim3(lgrid), dim3(256), 0, st, B.len, R, B.bsum, B.rec_off);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)((end - t0 + kTile - 1) / kTile)), dim3(256), 0, st, D, t0, lo,
+                       B.meta, B.tile_off, B.nl, B.rec_off, B.seq, B.qual, B.meta);
+    PA_HIP(hipGetLastError());
+    PA_HIP(hipMemcpyAsync(B.h_meta, B.meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
+    tw = now();
+    PA_HIP(hipStreamSynchronize(st));
+    *t_rec += ms(tw, now());
+    if (B.h_meta->err) {
+        out.fail = true;
+        return PA_OK;
+    }
+    pa_reads r{};
+    r.device = idx->device;
+    r.n = R;
+    r.n_bases = 0;  // (not read by the align path)
+    r.max_len = (uint32_t)B.h_meta->max_len;
+    r.seq = B.seq;
+    r.qual = B.qual;
+    r.off = (uint64_t *)B.rec_off;
+    PA_TRY(align(idx, &r, prm, base, acc, st));
+    out.records = R;
+    return PA_OK;
+}
+
+bool env_on(const char *name) {
+    const char *e = std::getenv(name);
+    return e && e[0] == '1';
+}
+
+}  // namespace pa
+
+// ---- prefetch: the whole file into device memory, in the background ---------------
+
+struct pa_fastq_prefetch {
+    int device = 0;
+    std::string path;
+    uint64_t size = 0;
+    uint64_t window = 0;
+    uint8_t *text = nullptr;    // device: the file, plus kTile * 2 bytes of slack for the 16-B tile loads
+    pa::ParseBufs bufs;         // the per-window parse buffers (made by the prefetch thread too)
+    hipStream_t st = nullptr;   // the prefetch thread's copy stream
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t ready = 0;         // bytes of the file on the device (copies complete)
+    bool done = false;
+    pa_status rc = PA_OK;
+    std::string err;
+    int threads = 8;
+    double t_total_ms = 0;
+    uint64_t est_records = ~0ull;  // records in the file, from the line feeds of its first chunk (set before ready > 0)
+};
+
+namespace {
+
+// The prefetch thread: parallel positional reads into a ring of pinned chunks,
+// each copied to its place in `text` in file order.
+void prefetch_run(pa_fastq_prefetch *pf) {
+    const auto t_start = std::chrono::steady_clock::now();
+    auto fail = [&](pa_status rc, const std::string &msg) {
+        std::lock_guard<std::mutex> g(pf->mu);
+        pf->rc = rc;
+        pf->err = msg;
+        pf->done = true;
+        pf->cv.notify_all();
+    };
+    hipError_t e = hipSetDevice(pf->device);
+    size_t free_b = 0, total_b = 0;
+    if (e == hipSuccess) e = hipMemGetInfo(&free_b, &total_b);
+    // a file that would take more than a quarter of the free device memory
+    // (text + parse buffers ~ 21 B per window byte) is left to the windowed stream
+    if (e == hipSuccess && pf->size + 24 * pf->window > free_b / 4) {
+        fail(PA_EUNSUPPORTED, "FASTQ file too large to prefetch whole");
+        return;
+    }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&pf->st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&pf->text, pf->size + 2 * kTile + 16);
+    if (e == hipSuccess) e = pf->bufs.alloc(pf->window + 16, pf->size / 16 + 1024, pf->st);
+    if (e != hipSuccess) {
+        fail(e == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE,
+             std::string("HIP error in the FASTQ prefetch: ") + hipGetErrorString(e));
+        return;
+    }
+    const int fd = open(pf->path.c_str(), O_RDONLY);
+    if (fd < 0) {
+        fail(PA_EIO, "cannot open " + pf->path);
+        return;
+    }
+    uint64_t kChunk = 16ull << 20;  // PA_PREFETCH_CHUNK: another chunk size (tests: many chunks, ring wrap)
+    if (const char *c = std::getenv("PA_PREFETCH_CHUNK")) kChunk = std::max<uint64_t>(4096, std::strtoull(c, nullptr, 10));
+    const int nslot = 8;
+    const uint64_t nchunk = (pf->size + kChunk - 1) / kChunk;
+    const int nread = std::max(1, std::min(pf->threads, nslot - 2));
+    uint8_t *ring = nullptr;
+    e = hipHostMalloc((void **)&ring, kChunk * nslot, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        close(fd);
+        fail(PA_ENOMEM, std::string("pinned ring of the FASTQ prefetch: ") + hipGetErrorString(e));
+        return;
+    }
+    // chunk c goes to slot c % nslot; state[slot] = the chunk it holds once read (-1 free)
+    std::mutex rm;
+    std::condition_variable rcv;
+    std::vector<int64_t> slot_chunk(nslot, -1), slot_free_for(nslot);
+    for (int s = 0; s < nslot; s++) slot_free_for[s] = s;  // the next chunk allowed into the slot
+    bool read_error = false, abort = false;
+    std::vector<std::thread> readers;
+    for (int t = 0; t < nread; t++)
+        readers.emplace_back([&, t] {
+            for (uint64_t c = t; c < nchunk; c += nread) {
+                const int s = (int)(c % nslot);
+                {
+                    std::unique_lock<std::mutex> g(rm);
+                    rcv.wait(g, [&] { return abort || slot_free_for[s] == (int64_t)c; });
+                    if (abort) return;
+                }
+                const uint64_t a = c * kChunk, n = std::min(kChunk, pf->size - a);
+                uint64_t got = 0;
+                while (got < n) {
+                    const ssize_t r = pread(fd, ring + (uint64_t)s * kChunk + got, n - got, (off_t)(a + got));
+                    if (r <= 0) break;
+                    got += (uint64_t)r;
+                }
+                std::lock_guard<std::mutex> g(rm);
+                if (got < n) read_error = true;
+                slot_chunk[s] = (int64_t)c;
+                rcv.notify_all();
+            }
+        });
+    pa_status rc = PA_OK;
+    std::string msg;
+    for (uint64_t c = 0; c < nchunk; c++) {
+        const int s = (int)(c % nslot);
+        {
+            std::unique_lock<std::mutex> g(rm);
+            rcv.wait(g, [&] { return read_error || slot_chunk[s] == (int64_t)c; });
+            if (read_error) {
+                rc = PA_EIO;
+                msg = "read error in " + pf->path;
+                break;
+            }
+        }
+        const uint64_t a = c * kChunk, n = std::min(kChunk, pf->size - a);
+        if (c == 0) {  // records ~ line feeds / 4 of the first chunk, scaled to the file
+            const uint8_t *h = ring;
+            const uint64_t m = std::min<uint64_t>(n, 4ull << 20);
+            uint64_t nl = 0;
+            for (uint64_t i = 0; i < m; i++) nl += h[i] == '\n';
+            pf->est_records = m ? (uint64_t)((double)pf->size * (double)(nl / 4 + 1) / (double)m) : 0;
+        }
+        e = hipMemcpyAsync(pf->text + a, ring + (uint64_t)s * kChunk, n, hipMemcpyHostToDevice, pf->st);
+        if (e == hipSuccess) e = hipStreamSynchronize(pf->st);
+        if (e != hipSuccess) {
+            rc = PA_EDEVICE;
+            msg = std::string("HIP error in the FASTQ prefetch copy: ") + hipGetErrorString(e);
+            break;
+        }
+        {
+            std::lock_guard<std::mutex> g(rm);
+            slot_chunk[s] = -1;
+            slot_free_for[s] = (int64_t)(c + nslot);
+            rcv.notify_all();
+        }
+        {
+            std::lock_guard<std::mutex> g(pf->mu);
+            pf->ready = a + n;
+            pf->cv.notify_all();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(rm);
+        abort = true;
+        rcv.notify_all();
+    }
+    for (auto &x : readers) x.join();
+    close(fd);
+    hipHostFree(ring);
+    pf->t_total_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (rc != PA_OK) {
+        fail(rc, msg);
+        return;
+    }
+    std::lock_guard<std::mutex> g(pf->mu);
+    pf->done = true;
+    pf->cv.notify_all();
+}
+
+}  // namespace
+
+namespace pa {
+
+pa_status fastq_prefetch_start(const char *path, int device, int threads, uint64_t window, pa_fastq_prefetch **out) {
+    *out = nullptr;
+    const size_t pl = strlen(path);
+    if (pl >= 3 && strcmp(path + pl - 3, ".gz") == 0) {
+        set_error("pa_fastq_prefetch_start: gzip files are read by the windowed stream (pa_align_fastq_file)");
+        return PA_EUNSUPPORTED;
+    }
+    struct stat sb;
+    if (stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) {
+        set_error(std::string("cannot open ") + path);
+        return PA_EIO;
+    }
+    auto *pf = new pa_fastq_prefetch();
+    pf->device = device;
+    pf->path = path;
+    pf->size = (uint64_t)sb.st_size;
+    pf->window = std::max<uint64_t>(window, 1 << 16) & ~(uint64_t)(kTile - 1);
+    pf->threads = std::max(1, threads);
+    pf->th = std::thread(prefetch_run, pf);
+    *out = pf;
+    return PA_OK;
+}
+
+void fastq_prefetch_free(pa_fastq_prefetch *pf) {
+    if (!pf) return;
+    if (pf->th.joinable()) pf->th.join();
+    hipSetDevice(pf->device);
+    if (pf->st) hipStreamSynchronize(pf->st);
+    hipFree(pf->text);
+    pf->bufs.release();
+    if (pf->st) hipStreamDestroy(pf->st);
+    delete pf;
+}
+
+// The prefetched file, parsed and aligned window by window as soon as each
+// window's bytes are on the device: no carries (the text is contiguous), the
+// index's align-side view made while the copies run.
+pa_status align_fastq_prefetched(pa_index *idx, pa_fastq_prefetch *pf, const DevParams &prm, uint64_t base,
+                                 pa_result *acc, hipStream_t st, uint64_t *n_reads) {
+    const bool timing = env_on("PA_STREAM_TIMING");
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t_start = now();
+    double t_meta = 0, t_rec = 0, t_wait = 0;
+    if (pf->device != idx->device) {
+        set_error("pa_align_fastq_prefetched: the prefetch and the index live on different devices");
+        return PA_EINVAL;
+    }
+    double t_prepare = 0;
+    auto wait_for = [&](uint64_t need) -> pa_status {
+        const auto tw = now();
+        std::unique_lock<std::mutex> g(pf->mu);
+        pf->cv.wait(g, [&] { return pf->done || pf->ready >= need; });
+        t_wait += ms(tw, now());
+        if (pf->rc != PA_OK) {
+            set_error(pf->err);
+            return pf->rc;
+        }
+        return PA_OK;
+    };
+    {  // (the parse buffers exist once a byte is on the device, or the thread is done)
+        const pa_status rc = wait_for(1);
+        if (rc == PA_EUNSUPPORTED)  // not prefetched (too large): the windowed stream
+            return align_fastq_file(idx, pf->path.c_str(), prm, base, acc, pf->threads, pf->window, st, n_reads);
+        PA_TRY(rc);
+    }
+    {  // the align-side view, for the reads this file holds (a file of few reads skips the neighbour bits)
+        const auto tp = now();
+        PA_TRY(index_prepare(idx, st, pf->est_records));
+        t_prepare = ms(tp, now());
+    }
+    PA_TRY(reserve_queues(idx, pf->bufs.max_rec));
+    // the parse stream must see the prefetch thread's allocations and memsets
+    PA_HIP(hipStreamSynchronize(pf->st));
+    uint64_t lo = 0, records = 0;
+    bool fail = pf->size == 0;
+    while (!fail) {
+        const uint64_t hi = std::min(pf->size, lo + pf->window);
+        PA_TRY(wait_for(hi));
+        const bool last = hi == pf->size;
+        WindowOut w;
+        PA_TRY(parse_align_window(pf->bufs, pf->text, lo, hi, last, idx, prm, base + records, acc, st, w, &t_meta,
+                                  &t_rec));
+        if (w.fail) {
+            fail = true;
+            break;
+        }
+        records += w.records;
+        if (last) break;
+        lo = w.end;
+    }
+    if (records == 0) fail = true;  // no records: the exact parser raises
+    PA_HIP(hipStreamSynchronize(st));
+    if (timing)
+        fprintf(stderr, "[pa_stream] prefetched %llu records: prefetch thread %.1f ms, prepare %.1f ms, waits: "
+                        "copies %.1f, window meta %.1f, records %.1f ms; total %.1f ms\n",
+                (unsigned long long)records, pf->t_total_ms, t_prepare, t_wait, t_meta, t_rec, ms(t_start, now()));
+    if (fail) {
+        set_error("FASTQ file outside the device-parsed subset of the grammar (or a duplicate id)");
+        return PA_ENOTCANON;
+    }
+    if (n_reads) *n_reads = records;
+    return PA_OK;
+}
 pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,
                            int threads, uint64_t window, hipStream_t st, uint64_t *n_reads) {
     // PA_STREAM_TIMING=1: where the time goes (stderr)
-    const bool timing = std::getenv("PA_STREAM_TIMING") && std::getenv("PA_STREAM_TIMING")[0] == '1';
+    const bool timing = env_on("PA_STREAM_TIMING");
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
@@ -380,17 +771,10 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
     }
     const uint64_t W = std::max<uint64_t>(window, 1 << 16) & ~(uint64_t)(kTile - 1);
     const uint64_t dbytes = kCarryMax + W + 2 * kTile;       // one device text buffer
-    const uint64_t max_tiles = (kCarryMax + W) / kTile + 2;
-    const uint64_t max_nl = kCarryMax + W + 8;  // (a text of line feeds only: every byte)
-    const uint64_t max_rec = (kCarryMax + W) / 8 + 2;
     const uint64_t est_rec = src.gz ? (1ull << 24) : src.size / 16 + 1024;
-    uint64_t ids_cap = 1024;
-    while (ids_cap < 2 * est_rec) ids_cap <<= 1;
 
-    uint8_t *H[2] = {nullptr, nullptr}, *D[2] = {nullptr, nullptr}, *seq = nullptr, *qual = nullptr;
-    uint32_t *tile_cnt = nullptr, *nl = nullptr, *len = nullptr;
-    unsigned long long *tile_off = nullptr, *bsum = nullptr, *rec_off = nullptr, *ids = nullptr, *tot = nullptr;
-    Meta *meta = nullptr, *h_meta = nullptr;
+    uint8_t *H[2] = {nullptr, nullptr}, *D[2] = {nullptr, nullptr};
+    ParseBufs B;
     hipStream_t cs = nullptr;
     hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_carry[2] = {nullptr, nullptr};
     std::thread reader;
@@ -405,9 +789,7 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
             if (ev_h2d[i]) hipEventDestroy(ev_h2d[i]);
             if (ev_carry[i]) hipEventDestroy(ev_carry[i]);
         }
-        hipFree(seq); hipFree(qual); hipFree(tile_cnt); hipFree(nl); hipFree(len); hipFree(tile_off);
-        hipFree(bsum); hipFree(rec_off); hipFree(ids); hipFree(tot); hipFree(meta);
-        hipHostFree(h_meta);
+        B.release();
         if (cs) hipStreamDestroy(cs);
         if (src.gz) gzclose(src.gz);
         if (src.fd >= 0) close(src.fd);
@@ -427,21 +809,8 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         F_HIP(hipEventCreateWithFlags(&ev_h2d[i], hipEventDisableTiming));
         F_HIP(hipEventCreateWithFlags(&ev_carry[i], hipEventDisableTiming));
     }
-    F_HIP(hipMalloc(&seq, kCarryMax + W + kReadPad));
-    F_HIP(hipMalloc(&qual, kCarryMax + W + kReadPad));
-    F_HIP(hipMalloc(&tile_cnt, max_tiles * 4));
-    F_HIP(hipMalloc(&tile_off, (max_tiles + 1) * 8));
-    F_HIP(hipMalloc(&nl, max_nl * 4));
-    F_HIP(hipMalloc(&len, max_rec * 4));
-    F_HIP(hipMalloc(&rec_off, (max_rec + 1) * 8));
-    F_HIP(hipMalloc(&bsum, (std::max(max_tiles, max_rec) / kScanBlock + 2) * 8));
-    F_HIP(hipMalloc(&ids, ids_cap * 8));
-    F_HIP(hipMalloc(&tot, 8));
-    F_HIP(hipMalloc(&meta, sizeof(Meta)));
-    F_HIP(hipHostMalloc((void **)&h_meta, sizeof(Meta), hipHostMallocDefault));
+    F_HIP(B.alloc(kCarryMax + W, est_rec, st));
     F_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-    F_HIP(hipMemsetAsync(ids, 0, ids_cap * 8, st));
-    F_HIP(hipMemsetAsync(meta, 0, sizeof(Meta), st));
     t_alloc = ms(t_start, now());
     // the index's align-side view and the align queues, while window 0 is read
     uint64_t got_next = 0;
@@ -449,7 +818,7 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
     reader = std::thread([&] { read_ok = src.read(H[0], W, got_next); });
     auto tw = now();
     rc = index_prepare(idx, st);
-    if (rc == PA_OK) rc = reserve_queues(idx, max_rec);
+    if (rc == PA_OK) rc = reserve_queues(idx, B.max_rec);
     if (rc != PA_OK) {
         cleanup();
         return rc;
@@ -479,63 +848,24 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
             next_started = true;
         }
         // this window's text: [lo, hi) of D[cur], the carried tail in front of it
-        const uint64_t lo = kCarryMax - carry, hi = kCarryMax + got, t0 = lo & ~15ull;
+        const uint64_t lo = kCarryMax - carry, hi = kCarryMax + got;
         F_HIP(hipStreamWaitEvent(st, ev_h2d[cur], 0));
         if (carry) F_HIP(hipMemcpyAsync(D[cur] + lo, D[nxt] + prev_end, carry, hipMemcpyDeviceToDevice, st));
         F_HIP(hipEventRecord(ev_carry[cur], st));
         if (hi == lo) break;  // (an empty last window: nothing after the previous records)
-        const uint64_t ntiles = (hi - t0 + kTile - 1) / kTile;
-        const unsigned sgrid = (unsigned)((ntiles + kScanBlock - 1) / kScanBlock);
-        F_HIP(hipMemsetAsync(meta, 0, offsetof(Meta, max_len), st));
-        hipLaunchKernelGGL(k_nl_count, dim3((unsigned)ntiles), dim3(256), 0, st, D[cur], t0, lo, hi, tile_cnt);
-        hipLaunchKernelGGL(k_scan_sums, dim3(sgrid), dim3(256), 0, st, tile_cnt, ntiles, bsum);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, bsum, (uint64_t)sgrid, tot);
-        hipLaunchKernelGGL(k_scan_apply, dim3(sgrid), dim3(256), 0, st, tile_cnt, ntiles, bsum, tile_off);
-        hipLaunchKernelGGL(k_nl_write, dim3((unsigned)ntiles), dim3(256), 0, st, D[cur], t0, lo, hi, tile_off, nl);
-        hipLaunchKernelGGL(k_window_meta, dim3(1), dim3(1), 0, st, D[cur], lo, hi, last ? 1 : 0, nl, tot, meta);
-        F_HIP(hipGetLastError());
-        F_HIP(hipMemcpyAsync(h_meta, meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
-        tw = now();
-        F_HIP(hipStreamSynchronize(st));
-        t_wait_meta += ms(tw, now());
-        const uint64_t R = h_meta->n_rec, end = h_meta->end;
-        if (h_meta->err || (R == 0 && !last) || (!last && hi - end > kCarryMax) || R > max_rec) {
-            fail_grammar = true;  // (a record longer than the carry limit is left to the host parser too)
+        WindowOut w;
+        rc = parse_align_window(B, D[cur], lo, hi, last, idx, prm, base + records, acc, st, w, &t_wait_meta,
+                                &t_wait_rec);
+        if (rc != PA_OK) break;
+        // (a record longer than the carry limit is left to the host parser too)
+        if (w.fail || (!last && hi - w.end > kCarryMax)) {
+            fail_grammar = true;
             break;
         }
-        if (R > 0) {
-            const unsigned rgrid = (unsigned)std::min<uint64_t>((R + 255) / 256, 65536);
-            const unsigned lgrid = (unsigned)((R + kScanBlock - 1) / kScanBlock);
-            hipLaunchKernelGGL(k_records, dim3(rgrid), dim3(256), 0, st, D[cur], lo, nl, meta, len, ids, ids_cap, meta);
-            hipLaunchKernelGGL(k_scan_sums, dim3(lgrid), dim3(256), 0, st, len, R, bsum);
-            hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, bsum, (uint64_t)lgrid, tot);
-            hipLaunchKernelGGL(k_scan_apply, dim3(lgrid), dim3(256), 0, st, len, R, bsum, rec_off);
-            hipLaunchKernelGGL(k_compact, dim3((unsigned)((end - t0 + kTile - 1) / kTile)), dim3(256), 0, st, D[cur],
-                               t0, lo, meta, tile_off, nl, rec_off, seq, qual, meta);
-            F_HIP(hipGetLastError());
-            F_HIP(hipMemcpyAsync(h_meta, meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
-            tw = now();
-            F_HIP(hipStreamSynchronize(st));
-            t_wait_rec += ms(tw, now());
-            if (h_meta->err) {
-                fail_grammar = true;
-                break;
-            }
-            pa_reads r{};
-            r.device = idx->device;
-            r.n = R;
-            r.n_bases = 0;  // (not read by the align path)
-            r.max_len = (uint32_t)h_meta->max_len;
-            r.seq = seq;
-            r.qual = qual;
-            r.off = (uint64_t *)rec_off;
-            rc = align(idx, &r, prm, base + records, acc, st);
-            if (rc != PA_OK) break;
-            records += R;
-        }
+        records += w.records;
         if (last) break;
-        carry = hi - end;
-        prev_end = end;
+        carry = hi - w.end;
+        prev_end = w.end;
         // the next window's copy waits for this window's carry copy (which reads D[cur]'s tail later
         // only from the next window's perspective: D[nxt] is rewritten next)
         if (next_started) {

@@ -915,6 +915,66 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
 // is freed -- at the end of pa_index_build, or deferred (PA_BUILD_DEFER_TILES)
 // to pa_index_prepare / the first align call, so that an index used only for
 // EXTSIM statistics (src/kmer.py:152-263) never pays for it.
+// One-substitution neighbour bits of the genome tiling (k_nb_build, tile_nb):
+// 24 B per base, made once per index (C2: ~50 ms of kernels, ~0.12 s with the
+// allocation) -- they repay themselves after ~4 reads per genome base.
+pa_status build_nb(pa_index *idx, hipStream_t st) {
+    const uint64_t n = idx->tile_n;
+    const int k = (int)idx->k;
+    const uint32_t G = idx->n_genomes;
+    Slot<1> *table = (Slot<1> *)idx->table;
+#define B_HIP(call) PA_HIP(call)
+    // one-substitution neighbours: 24 B per base (present | specific) when
+    // that leaves a quarter of the free memory, else 12 B (present only:
+    // a present neighbour is then probed), else none; PA_NO_NB=1 skips
+    // them, PA_NB_HALF=1 forces the 12-B form (A/B measurements, tests)
+    size_t free_b = 0, total_b = 0;
+    const char *no_nb = std::getenv("PA_NO_NB"), *nb_half = std::getenv("PA_NB_HALF");
+    if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+        const bool full = n * 24 <= free_b / 4 * 3 && !(nb_half && nb_half[0] == '1') && !idx->force_large;
+        const uint64_t wb = full ? 8 : 4;
+        if (n * 3 * wb <= free_b / 4 * 3) {
+            B_HIP(hipMalloc(&idx->tile_nb, n * 3 * wb + 64));
+            B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 3 * wb + 64, st));
+            // a build-time Bloom filter of the keys (~16 bits per key, in
+            // HBM; freed below): most of the 3k neighbours of a window are
+            // absent and share the window's Bloom line (minimizer-chosen),
+            // so a probe costs an L2 hit instead of a table line.
+            // PA_NB_BLOOM=0 turns it off (A/B)
+            uint64_t *bb = nullptr;
+            uint32_t bb_lg = 6;
+            const char *nbb = std::getenv("PA_NB_BLOOM");
+            if (!(nbb && nbb[0] == '0') && idx->n_kmers > 0) {
+                while (bb_lg < 36 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;
+                size_t fb = 0, tb = 0;
+                if (hipMemGetInfo(&fb, &tb) != hipSuccess) fb = 0;
+                while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
+                if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && hipMalloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
+                    B_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
+                    hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                       dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, bb, bb_lg, k);
+                } else {
+                    bb = nullptr;
+                }
+            }
+            for (int pass = 0; pass < 2; pass++)
+                hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
+                                   st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                   idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
+                                   pass, bb, bb_lg);
+            if (bb) {
+                B_HIP(hipStreamSynchronize(st));
+                hipFree(bb);
+            }
+            idx->nb_spec = full ? 1 : 0;
+            idx->device_bytes += n * 3 * wb;
+        }
+    }
+#undef B_HIP
+    idx->nb_pending = 0;
+    return PA_OK;
+}
+
 template <int NW>
 pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
     const uint32_t G = idx->n_genomes;
@@ -965,51 +1025,13 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_tile_walk, dim3((unsigned)std::min<uint64_t>((n_blocks + 3) / 4, 1u << 20)), dim3(256),
                                0, st, idx->tile_cls, idx->tile_pk, n, G, idx->tile_lw, n_blocks);
             idx->device_bytes += n_blocks * 32;
-            // one-substitution neighbours: 24 B per base (present | specific) when
-            // that leaves a quarter of the free memory, else 12 B (present only:
-            // a present neighbour is then probed), else none; PA_NO_NB=1 skips
-            // them, PA_NB_HALF=1 forces the 12-B form (A/B measurements, tests)
-            size_t free_b = 0, total_b = 0;
-            const char *no_nb = std::getenv("PA_NO_NB"), *nb_half = std::getenv("PA_NB_HALF");
-            if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-                const bool full = n * 24 <= free_b / 4 * 3 && !(nb_half && nb_half[0] == '1') && !idx->force_large;
-                const uint64_t wb = full ? 8 : 4;
-                if (n * 3 * wb <= free_b / 4 * 3) {
-                    B_HIP(hipMalloc(&idx->tile_nb, n * 3 * wb + 64));
-                    B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 3 * wb + 64, st));
-                    // a build-time Bloom filter of the keys (~16 bits per key, in
-                    // HBM; freed below): most of the 3k neighbours of a window are
-                    // absent and share the window's Bloom line (minimizer-chosen),
-                    // so a probe costs an L2 hit instead of a table line.
-                    // PA_NB_BLOOM=0 turns it off (A/B)
-                    uint64_t *bb = nullptr;
-                    uint32_t bb_lg = 6;
-                    const char *nbb = std::getenv("PA_NB_BLOOM");
-                    if (!(nbb && nbb[0] == '0') && idx->n_kmers > 0) {
-                        while (bb_lg < 36 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;
-                        size_t fb = 0, tb = 0;
-                        if (hipMemGetInfo(&fb, &tb) != hipSuccess) fb = 0;
-                        while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
-                        if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && hipMalloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
-                            B_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
-                            hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
-                                               dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, bb, bb_lg, k);
-                        } else {
-                            bb = nullptr;
-                        }
-                    }
-                    for (int pass = 0; pass < 2; pass++)
-                        hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
-                                           st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                           idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
-                                           pass, bb, bb_lg);
-                    if (bb) {
-                        B_HIP(hipStreamSynchronize(st));
-                        hipFree(bb);
-                    }
-                    idx->nb_spec = full ? 1 : 0;
-                    idx->device_bytes += n * 3 * wb;
-                }
+            // one-substitution neighbours (build_nb): now, or -- when the caller
+            // expects too few reads to repay them -- on the align that brings the
+            // reads past that point (index_maybe_nb)
+            if (idx->nb_skip) {
+                idx->nb_pending = 1;
+            } else {
+                PA_TRY(build_nb(idx, st));
             }
             // the Bloom filter of the keys, for the lane kernel's probes of windows
             // off the walk (almost all absent): worth it while it stays in the
@@ -1100,10 +1122,19 @@ void index_release(pa_index *idx) {
     idx->table = nullptr;
 }
 
-pa_status index_prepare(pa_index *idx, hipStream_t st) {
+pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st) {
+    idx->reads_seen += n;
+    if (!idx->nb_pending || idx->reads_seen < kNbReadsPerBase * idx->tile_n) return PA_OK;
+    return build_nb(idx, st);
+}
+
+pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
     if (!idx->tiles_pending) return PA_OK;
     idx->tiles_pending = 0;
+    const uint64_t bases = idx->h_goff.empty() ? 0 : idx->h_goff.back();
+    idx->nb_skip = reads_hint != ~0ull && reads_hint < kNbReadsPerBase * bases;
     pa_status rc = build_tiles_nw<1>(idx, st);  // (tiles are made for single-word keys only)
+    idx->nb_skip = 0;
     if (rc != PA_OK) {  // the index stays usable without its align-side view
         hipFree(idx->tile_cls); hipFree(idx->tile_pk); hipFree(idx->tile_lw); hipFree(idx->tile_nb);
         hipFree(idx->tile_gblk); hipFree(idx->bloom);

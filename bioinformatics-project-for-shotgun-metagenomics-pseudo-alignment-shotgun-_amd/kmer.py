@@ -13,6 +13,13 @@ attributes, return values and exceptions.  What changes is where the work runs:
   is materialised on first access by the per-read kernel (``pa_align_detail``).
 * ``KmerReference.kmers`` -- positions included -- is an introspection view
   built on the host on first access; nothing on the align path reads it.
+  ``KmerReference.get_summary`` (dumpref) is made on the device instead
+  (``pa_index_dumpref``: k-mers in insertion order by a device sort, the JSON
+  text streamed by host threads), so it scales to references whose dict the
+  reference could not hold.
+* ``.kdb`` / ``.aln`` files load through a restricted unpickler that admits
+  only the classes such files hold -- this package's, or the reference's
+  same-named ones, so files written by the reference load too.
 
 Results (per-genome unique/ambiguous counts, filtered_* counters, the Summary
 key order) are bit-exact to the reference; see DESIGN.md for the quirk list
@@ -27,6 +34,7 @@ import gzip
 import json
 import os
 import pickle
+import tempfile
 from collections import defaultdict, namedtuple
 from enum import Enum
 from typing import Any, Dict, Iterator, List, Optional, Sequence, Set, Tuple, Union
@@ -153,6 +161,42 @@ def extsim_filter(index: N.Index, identifiers: Sequence[str], genome_lengths: Se
     return set(kept), info
 
 
+class _KdbUnpickler(pickle.Unpickler):
+    """Loader of .kdb / .aln files (src/kmer.py:265-282, 671-699): only the
+    classes such files hold are resolved -- this package's, whose module and
+    class names are the reference's own (kmer.KmerReference, records.Record,
+    ...), so a file written by the reference resolves to these classes and
+    their __setstate__ converts its state.  Anything else is refused."""
+
+    _OWN = {("kmer", n) for n in ("KmerReference", "PseudoAlignment", "ReadMappingType", "KmerSpecifity",
+                                  "ReadMapping", "ReadKmer")} | {("records", "Record")}
+    _LIB = {("numpy", "ndarray"), ("numpy", "dtype"), ("numpy.core.multiarray", "_reconstruct"),
+            ("numpy._core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "scalar"),
+            ("numpy._core.multiarray", "scalar"), ("builtins", "set"), ("builtins", "frozenset"),
+            ("collections", "defaultdict"), ("collections", "OrderedDict")}
+
+    def find_class(self, module: str, name: str):
+        if (module, name) in self._OWN:
+            if module == "records":
+                import records
+                return getattr(records, name)
+            return globals()[name]
+        if (module, name) in self._LIB:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"{module}.{name} is not a class a .kdb / .aln file holds")
+
+
+def _load_pickle(path: str):
+    with gzip.open(path, "rb") as f:
+        return _KdbUnpickler(f).load()
+
+
+def _write_fd(fd: int, data: bytes) -> None:
+    view = memoryview(data)
+    while view:
+        view = view[os.write(fd, view):]
+
+
 class KmerReference:
     """Device-resident k-mer reference of a FASTA container (src/kmer.py:109-351)."""
 
@@ -164,6 +208,7 @@ class KmerReference:
             raise TypeError(f"k must be an int, got {type(k)}")
         self.genomes: List[Record] = list(fasta_record_container)
         self._all_genomes: Optional[List[Record]] = None  # before EXTSIM dropped any (k-mer view order)
+        self._ref_kmers: Optional[Dict[str, Dict[Record, Set[int]]]] = None  # the dict of a reference-written .kdb
         self.kmer_len: int = k
         self._device = N.default_device() if device is None else int(device)
         self._build()
@@ -207,8 +252,27 @@ class KmerReference:
         return state
 
     def __setstate__(self, state):
+        if "kmers" in state and "_device" not in state:
+            # written by the reference (src/kmer.py:265-282): genomes (the kept
+            # ones after EXTSIM), kmer_len, its kmers dict, similarity_info.  The
+            # device index is built from the genomes; the dict stays the k-mer
+            # view, since after EXTSIM its order comes from genomes the file no
+            # longer holds.
+            self.genomes = list(state["genomes"])
+            self.kmer_len = state["kmer_len"]
+            self._all_genomes = None
+            self._device = N.default_device()
+            if "similarity_info" in state:
+                self.similarity_info = state["similarity_info"]
+            self._build()
+            self._ref_kmers = state["kmers"]
+            self._view = self._ref_kmers
+            return
         self.__dict__.update(state)
+        self.__dict__.setdefault("_ref_kmers", None)
         self._build()
+        if self._ref_kmers is not None:
+            self._view = self._ref_kmers
 
     def save(self, ref_file: str) -> None:
         with gzip.open(ref_file, "wb") as f:
@@ -216,8 +280,7 @@ class KmerReference:
 
     @classmethod
     def load(cls, ref_file: str) -> "KmerReference":
-        with gzip.open(ref_file, "rb") as f:
-            return pickle.load(f)
+        return _load_pickle(ref_file)  # (any object, as pickle.load)
 
     # -- lookups ----------------------------------------------------------------
 
@@ -262,8 +325,57 @@ class KmerReference:
                 result.setdefault(g, set()).update(p)
         return result
 
+    # -- dumpref (src/kmer.py:300-329) ---------------------------------------------
+
+    def write_summary(self, fd: int) -> None:
+        """``json.dumps(self.get_summary(), indent=4)`` written to file descriptor
+        ``fd`` (no final line break): the "Kmers" object streamed from the device
+        index by pa_index_dumpref, then Summary (and Similarity) from its counts."""
+        if self._ref_kmers is not None:  # a reference-written .kdb: its own dict is the k-mer order
+            _write_fd(fd, json.dumps(self._summary_from_view(), indent=4).encode())
+            return
+        if self._all_genomes is None:
+            index, genomes, keep, tmp = self._index, self.genomes, None, False
+        else:
+            # EXTSIM dropped genomes: the reference deletes their entries from the
+            # full dict (src/kmer.py:232-245), so the k-mers keep the full
+            # build's order -- dump an index of every original genome, masked
+            genomes = self._all_genomes
+            index = N.Index([g["genome"] for g in genomes], self.kmer_len, device=self._device, defer_tiles=True)
+            kept = {id(g) for g in self.genomes}
+            keep = np.fromiter((id(g) in kept for g in genomes), dtype=np.uint8, count=len(genomes))
+            tmp = True
+        descs: Dict[str, int] = {}
+        desc_of = np.empty(len(genomes), dtype=np.uint32)
+        for i, g in enumerate(genomes):
+            desc_of[i] = descs.setdefault(g["description"], len(descs))
+        names = list(descs)
+        try:
+            _write_fd(fd, b'{\n    "Kmers": ')
+            uniq, multi, order, last, _ = N.index_dumpref(index, keep, desc_of, [json.dumps(d) for d in names], fd)
+        finally:
+            if tmp:
+                index.close()
+        present = sorted((d for d in range(len(names)) if int(order[d]) != N.NO_ORDER), key=lambda d: int(order[d]))
+        summary = {names[d]: {"total_bases": len(genomes[int(last[d])]["genome"]), "unique_kmers": int(uniq[d]),
+                              "multi_mapping_kmers": int(multi[d])} for d in present}
+        tail: Dict[str, Any] = {"Kmers": 0, "Summary": summary}
+        if hasattr(self, "similarity_info"):
+            tail["Similarity"] = self.similarity_info
+        text = json.dumps(tail, indent=4)
+        _write_fd(fd, text[text.index('"Kmers": 0') + len('"Kmers": 0'):].encode())
+
     def get_summary(self) -> Dict[str, Any]:
-        """dumpref summary (src/kmer.py:300-329), from the introspection view."""
+        """dumpref summary (src/kmer.py:300-329): {"Kmers", "Summary"[, "Similarity"]}."""
+        if self._ref_kmers is not None:
+            return self._summary_from_view()
+        with tempfile.TemporaryFile() as f:
+            self.write_summary(f.fileno())
+            f.seek(0)
+            return json.loads(f.read())
+
+    def _summary_from_view(self) -> Dict[str, Any]:
+        """The same summary from the host view (a reference-written .kdb's dict)."""
         kmers = self.kmers
         details = {km: {g["description"]: sorted(p) for g, p in gs.items()} for km, gs in kmers.items()}
         summary: Dict[str, Dict[str, int]] = defaultdict(
@@ -504,13 +616,16 @@ class PseudoAlignment:
                             unique_batch=isinstance(reads_container, FASTAQRecordContainer))
 
     def align_reads_from_file(self, reads_file: str, m: int = 1, p: int = 1, min_read_quality: Optional[int] = None,
-                              min_kmer_quality: Optional[int] = None, max_genomes: Optional[int] = None) -> None:
+                              min_kmer_quality: Optional[int] = None, max_genomes: Optional[int] = None, *,
+                              prefetch: Optional["N.FastqPrefetch"] = None) -> None:
         """FASTAQFile(reads_file).container + align_reads_from_container as one
         device pass (pa_align_fastq_file: the file is parsed on the GPU and
         aligned in windows while the host reads the next).  Per-read results
         (``reads``) parse the file again when asked for.  A file outside the
         device-parsed subset of the grammar, a duplicate id, arguments the
-        reference rejects, or reads already added take the exact path."""
+        reference rejects, or reads already added take the exact path.
+        ``prefetch``: the same file already on its way to the device
+        (N.FastqPrefetch, started before the index build); consumed here."""
         from data_file import FASTAQFile
         fresh = not self._batches and not self._host and self._result is None
         err = _check_align_args(self.kmer_reference, m, p, min_read_quality, min_kmer_quality, max_genomes)
@@ -520,9 +635,14 @@ class PseudoAlignment:
             ref = self.kmer_reference
             result = N.Result(ref.index)
             prm = N.Params.make(m, p, min_read_quality, min_kmer_quality, max_genomes)
-            n = N.align_fastq_file(ref.index, reads_file, prm, self._next_index, result)
+            if prefetch is not None and prefetch.device == ref.index.device:
+                n = N.align_fastq_prefetched(ref.index, prefetch, prm, self._next_index, result)
+            else:
+                n = N.align_fastq_file(ref.index, reads_file, prm, self._next_index, result)
             if n is None:
                 result.close()
+        if prefetch is not None:
+            prefetch.close()
         if n is None:
             self.align_reads_from_container(FASTAQFile(reads_file).container, m, p, min_read_quality,
                                             min_kmer_quality, max_genomes)
@@ -679,6 +799,13 @@ class PseudoAlignment:
         return state
 
     def __setstate__(self, state):
+        if "reads" in state and "_host" not in state:
+            # written by the reference (src/kmer.py:536-548, 659-699): its reads
+            # dict becomes the host entries, in the same order
+            reads = state.pop("reads")
+            state["_host"] = [(i, rid, e) for i, (rid, e) in enumerate(reads.items())]
+            state["_next_index"] = len(reads)
+            state["_gpu_stats"] = np.zeros(6, dtype=np.uint64)
         self.__dict__.update(state)
         self._result = None
         self._batches = []
@@ -690,5 +817,4 @@ class PseudoAlignment:
 
     @classmethod
     def load(cls, align_file: str) -> "PseudoAlignment":
-        with gzip.open(align_file, "rb") as f:
-            return pickle.load(f)
+        return _load_pickle(align_file)  # (any object, as pickle.load)

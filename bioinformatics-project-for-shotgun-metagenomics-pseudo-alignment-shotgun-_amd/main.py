@@ -13,14 +13,17 @@ checks, default coercions and error exits as src/main.py:61-402:
 * errors end the process with ``sys.exit(message)`` (non-zero, message on
   stderr).
 
-The ``.kdb`` / ``.aln`` files are gzip pickles of this package's objects (the
-reference's files are pickles of its own classes, so neither side can read the
-other's); a loaded reference rebuilds its device index.
+The ``.kdb`` / ``.aln`` files are gzip pickles, loaded by a restricted
+unpickler (kmer._KdbUnpickler) that admits only the classes such files hold;
+the classes keep the reference's module and class names, so files written by
+the reference load too (a loaded reference rebuilds its device index).
+``dumpref`` streams its JSON from the device index (pa_index_dumpref).
 """
 
 from __future__ import annotations
 
 import argparse
+import atexit
 import gzip
 import json
 import os
@@ -29,6 +32,15 @@ import time
 from typing import List, Optional
 
 _T0 = time.perf_counter()
+
+if __name__ == "__main__":  # the HIP runtime starts on a native thread while the modules below import
+    try:
+        import ctypes
+        _here = os.path.dirname(os.path.abspath(__file__))
+        ctypes.CDLL(os.environ.get("PA_LIBRARY", os.path.join(_here, "libpa.so"))).pa_runtime_start(
+            int(os.environ.get("PA_DEVICE", os.environ.get("LOCAL_RANK", "0"))))
+    except (OSError, AttributeError, ValueError):
+        pass  # (no library: pa_native raises at the first device call)
 
 from constants import DEFAULT_AMBIGUOUS_THRESHOLD, DEFAULT_SIMILARITY_THRESHOLD, DEFAULT_UNIQUE_THRESHOLD
 from data_file import FASTAFile, FASTAQFile, InvalidExtensionError, NoRecordsInDataFile
@@ -91,21 +103,52 @@ def create_reference(fasta_file: str, kmer_size: int, filter_similar: bool = Fal
                          similarity_threshold=similarity_threshold)
 
 
+def _prefetch_reads(reads_file: str):
+    """Start moving a plain FASTQ file into device memory (pa_fastq_prefetch_start)
+    so that the copy overlaps the reference build; None where the file takes
+    another path (a .gz or wrong extension, PA_STREAM=0 / PA_PREFETCH=0)."""
+    if os.environ.get("PA_STREAM", "1") == "0" or os.environ.get("PA_PREFETCH", "1") == "0":
+        return None
+    if reads_file.endswith(".gz") or not any(reads_file.endswith(e) for e in FASTAQFile.EXTENSIONS):
+        return None
+    try:
+        import pa_native as N
+        pf = N.FastqPrefetch(reads_file)
+    except Exception:  # (no device, unreadable file: the exact path reports it in the reference's order)
+        return None
+    atexit.register(pf.close)
+    return pf
+
+
 def create_alignment_from_reference(kmer_reference: KmerReference, reads_file: str, m: int, p: int,
-                                    min_read_quality, min_kmer_quality, max_genomes) -> PseudoAlignment:
+                                    min_read_quality, min_kmer_quality, max_genomes,
+                                    prefetch=None) -> PseudoAlignment:
     # the FASTQ file goes straight to the device (parsed there, aligned in
     # windows); a file outside that subset of the grammar is parsed the exact
     # way (FASTAQFile), which also raises the reference's errors
     FASTAQFile.check_extension(reads_file)
     _stage("reference built")
     alignment = PseudoAlignment(kmer_reference)
-    alignment.align_reads_from_file(reads_file, m, p, min_read_quality, min_kmer_quality, max_genomes)
+    alignment.align_reads_from_file(reads_file, m, p, min_read_quality, min_kmer_quality, max_genomes,
+                                    prefetch=prefetch)
     _stage("reads aligned")
     return alignment
 
 
 def _print_json(obj) -> None:
     print(json.dumps(obj, indent=4))
+
+
+def _dump_reference(ref: KmerReference) -> None:
+    """print(json.dumps(ref.get_summary(), indent=4)) (src/main.py:121-127), the
+    text streamed to stdout from the device index instead of built as a dict."""
+    if not isinstance(ref, KmerReference):  # (another object in the file: its own summary, as the reference)
+        _print_json(ref.get_summary())
+        return
+    sys.stdout.flush()
+    fd = sys.stdout.fileno()
+    ref.write_summary(fd)
+    os.write(fd, b"\n")
 
 
 def _check_task(args: argparse.Namespace) -> None:
@@ -144,33 +187,37 @@ def _run(args: argparse.Namespace) -> None:
     elif args.task == "dumpref":
         if args.referencefile:
             validate_file_readable(args.referencefile, "Reference database")
-            _print_json(_load_reference(args.referencefile).get_summary())
+            _dump_reference(_load_reference(args.referencefile))
         elif args.genomefile and args.kmer_size:
             validate_file_readable(args.genomefile, "Genome FASTA")
-            _print_json(create_reference(args.genomefile, args.kmer_size, args.filter_similar,
-                                         args.similarity_threshold).get_summary())
+            _dump_reference(create_reference(args.genomefile, args.kmer_size, args.filter_similar,
+                                             args.similarity_threshold))
     elif args.task == "align":
         validate_file_readable(args.reads, "FASTQ reads")
         validate_file_writable(args.alignfile, "Alignment output")
         if args.referencefile and args.reads and args.alignfile:
             validate_file_readable(args.referencefile, "Reference database")
+            pf = _prefetch_reads(args.reads)
             ref = _load_reference(args.referencefile)
         else:
             validate_file_readable(args.genomefile, "Genome FASTA")
+            pf = _prefetch_reads(args.reads)
             ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
             if args.referencefile:
                 ref.save(args.referencefile)
-        create_alignment_from_reference(ref, args.reads, *filt).save(args.alignfile)
+        create_alignment_from_reference(ref, args.reads, *filt, prefetch=pf).save(args.alignfile)
     elif args.task == "dumpalign":
         if args.referencefile and args.reads:
             validate_file_readable(args.reads, "FASTQ reads")
+            pf = _prefetch_reads(args.reads)
             ref = _load_reference(args.referencefile)
-            _print_json(create_alignment_from_reference(ref, args.reads, *filt).get_summary())
+            _print_json(create_alignment_from_reference(ref, args.reads, *filt, prefetch=pf).get_summary())
         elif args.genomefile and args.kmer_size and args.reads:
             validate_file_readable(args.reads, "FASTQ reads")
             validate_file_readable(args.genomefile, "Genome FASTA")
+            pf = _prefetch_reads(args.reads)
             ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
-            _print_json(create_alignment_from_reference(ref, args.reads, *filt).get_summary())
+            _print_json(create_alignment_from_reference(ref, args.reads, *filt, prefetch=pf).get_summary())
         elif args.alignfile:
             validate_file_readable(args.alignfile, "Alignment output")
             try:
@@ -207,3 +254,12 @@ def main(argv: Optional[List[str]] = None) -> None:
 
 if __name__ == "__main__":
     main()
+    # done: the output is flushed and the process ends without releasing the
+    # device index allocation by allocation (the driver reclaims it at exit);
+    # PA_FAST_EXIT=0 keeps the normal interpreter exit (profilers write their
+    # results from exit handlers)
+    if os.environ.get("PA_FAST_EXIT", "1") != "0":
+        _stage("exit")
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)

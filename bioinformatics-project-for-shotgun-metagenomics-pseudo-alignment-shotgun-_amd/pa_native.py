@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -27,13 +27,14 @@ PA_BUILD_DEFER_TILES = 1
 
 # every symbol declared in include/pa.h
 EXPORTS = (
-    "pa_last_error", "pa_version", "pa_device_count",
+    "pa_last_error", "pa_version", "pa_device_count", "pa_runtime_start",
     "pa_index_build", "pa_index_build_ex", "pa_index_prepare", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
-    "pa_index_extsim_stats",
+    "pa_index_extsim_stats", "pa_index_dumpref",
     "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_reads_download", "pa_reads_free",
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
     "pa_result_copy_in", "pa_result_free",
     "pa_align", "pa_align_detail", "pa_align_batch", "pa_align_fastq_file",
+    "pa_fastq_prefetch_start", "pa_align_fastq_prefetched", "pa_fastq_prefetch_free",
     "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_counters_reduce",
     "pa_profile_enable", "pa_profile_read",
     "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free",
@@ -102,6 +103,7 @@ def lib():
         "pa_last_error": (ctypes.c_char_p, []),
         "pa_version": (ctypes.c_char_p, []),
         "pa_device_count": (I32, [ctypes.POINTER(I32)]),
+        "pa_runtime_start": (I32, [I32]),
         "pa_index_build": (I32, [I32, ctypes.c_char_p, P, U32, I64, P, PP]),
         "pa_index_build_ex": (I32, [I32, ctypes.c_char_p, P, U32, I64, U32, P, PP]),
         "pa_index_prepare": (I32, [P, P]),
@@ -110,6 +112,8 @@ def lib():
         "pa_index_lookup": (I32, [P, ctypes.c_char_p, U64, U32, P, P, P]),
         "pa_index_class_genomes": (I32, [P, I64, P, U32, ctypes.POINTER(U32), P]),
         "pa_index_extsim_stats": (I32, [P, P, U32, P, P, P, P]),
+        "pa_index_dumpref": (I32, [P, P, P, U32, ctypes.POINTER(ctypes.c_char_p), I32, I32, P, P, P, P,
+                                   ctypes.POINTER(U64)]),
         "pa_reads_upload": (I32, [I32, P, P, P, U64, P, PP]),
         "pa_reads_synthesize": (I32, [P, U64, U32, U64, U64, ctypes.c_double, P, PP]),
         "pa_reads_synthesize_mix": (I32, [P, U64, U32, U64, U64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
@@ -129,6 +133,9 @@ def lib():
         "pa_align_batch": (I32, [P, P, P, P, U64, U64, ctypes.POINTER(Params), ctypes.POINTER(Stats), P, P, P, P]),
         "pa_align_fastq_file": (I32, [P, ctypes.c_char_p, ctypes.POINTER(Params), U64, P, I32, U64, P,
                                       ctypes.POINTER(U64)]),
+        "pa_fastq_prefetch_start": (I32, [ctypes.c_char_p, I32, I32, U64, PP]),
+        "pa_align_fastq_prefetched": (I32, [P, P, ctypes.POINTER(Params), U64, P, P, ctypes.POINTER(U64)]),
+        "pa_fastq_prefetch_free": (None, [P]),
         "pa_comm_unique_id": (I32, [P]),
         "pa_comm_init": (I32, [I32, I32, I32, P, PP]),
         "pa_comm_free": (I32, [P]),
@@ -567,6 +574,70 @@ def align_fastq_file(index: Index, path: str, params: Params, read_index_base: i
     st = lib().pa_align_fastq_file(index.handle, os.fsencode(path), ctypes.byref(params), int(read_index_base),
                                    result.handle, int(threads or ingest_threads()), int(window_bytes),
                                    _stream(stream), ctypes.byref(n))
+    if st == PA_ENOTCANON:
+        return None
+    _check(st)
+    return int(n.value)
+
+
+NO_ORDER = 0xFFFFFFFFFFFFFFFF  # pa_index_dumpref: a description no k-mer holds
+
+
+def index_dumpref(index: "Index", keep: Optional[np.ndarray], desc_of: np.ndarray, desc_json: List[str], fd: int,
+                  threads: Optional[int] = None):
+    """pa_index_dumpref: the dumpref "Kmers" object written to ``fd``; returns
+    per-description (unique_kmers, multi_mapping_kmers, first-appearance rank,
+    last genome) arrays and the number of k-mers written."""
+    nd = len(desc_json)
+    names = (ctypes.c_char_p * max(nd, 1))(*[d.encode("ascii") for d in desc_json])
+    uniq = np.zeros(max(nd, 1), dtype=np.uint64)
+    multi = np.zeros(max(nd, 1), dtype=np.uint64)
+    order = np.zeros(max(nd, 1), dtype=np.uint64)
+    last = np.zeros(max(nd, 1), dtype=np.uint32)
+    desc_of = np.ascontiguousarray(desc_of, dtype=np.uint32)
+    keep = None if keep is None else np.ascontiguousarray(keep, dtype=np.uint8)
+    nk = U64(0)
+    _check(lib().pa_index_dumpref(index.handle, _ptr(keep), _ptr(desc_of), nd, names, int(fd),
+                                  int(threads or ingest_threads()), _ptr(uniq), _ptr(multi), _ptr(order), _ptr(last),
+                                  ctypes.byref(nk)))
+    return uniq[:nd], multi[:nd], order[:nd], last[:nd], int(nk.value)
+
+
+class FastqPrefetch:
+    """pa_fastq_prefetch_start: a plain FASTQ file moved into device memory on a
+    background native thread (so the copy overlaps the FASTA parse and the index
+    build); consumed by align_fastq_prefetched, freed by close()."""
+
+    def __init__(self, path: str, device: Optional[int] = None, threads: Optional[int] = None,
+                 window_bytes: int = 0) -> None:
+        self.handle = P()
+        self.path = path
+        self.device = default_device() if device is None else int(device)
+        if window_bytes <= 0:
+            env = os.environ.get("PA_STREAM_WINDOW")
+            window_bytes = int(env) if env and env.isdigit() else 0
+        _check(lib().pa_fastq_prefetch_start(os.fsencode(path), self.device, int(threads or ingest_threads()),
+                                             int(window_bytes), ctypes.byref(self.handle)))
+
+    def close(self) -> None:
+        if self.handle:
+            lib().pa_fastq_prefetch_free(self.handle)
+            self.handle = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def align_fastq_prefetched(index: Index, prefetch: FastqPrefetch, params: Params, read_index_base: int,
+                           result: Result, stream=None) -> Optional[int]:
+    """pa_align_fastq_prefetched: like align_fastq_file on a prefetched file;
+    None when the file is outside the device-parsed subset of the grammar."""
+    n = U64(0)
+    st = lib().pa_align_fastq_prefetched(index.handle, prefetch.handle, ctypes.byref(params), int(read_index_base),
+                                         result.handle, _stream(stream), ctypes.byref(n))
     if st == PA_ENOTCANON:
         return None
     _check(st)

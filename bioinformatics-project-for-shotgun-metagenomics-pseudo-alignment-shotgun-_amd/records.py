@@ -87,6 +87,10 @@ class Record:
         return {"identifier": self.identifier, "sections": self._sections}
 
     def __setstate__(self, state):
+        if "_Record__sections" in state:  # pickled by the reference (src/records.py:74-90: name-mangled dict)
+            self.identifier = state["identifier"]
+            self._sections = dict(state["_Record__sections"])
+            return
         self.identifier = state["identifier"]
         self._sections = state["sections"]
 

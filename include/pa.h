@@ -11,6 +11,8 @@
  *   pa_index_prepare         (the deferred view, before the first align)
  *   pa_index_lookup          KmerReference.get_kmer_references / __getitem__ src/kmer.py:284-298
  *   pa_index_class_genomes   (genome set of a k-mer, i.e. the keys of kmers[kmer]) src/kmer.py:130
+ *   pa_index_dumpref         KmerReference.get_summary ("Kmers" + Summary counts)
+ *                            streamed as JSON text (dumpref)                src/kmer.py:300-329
  *   pa_index_extsim_stats    KmerReference._compute_genome_stats + the pairwise
  *                            intersections of _apply_greedy_filter          src/kmer.py:152-230
  *   pa_align                 PseudoAlignment.align_reads_from_container ->
@@ -22,6 +24,8 @@
  *   pa_align_fastq_file      FASTAQFile + align_reads_from_container as one
  *                            device-parsed stream                          src/data_file.py:134-158,
  *                                                                          src/kmer.py:600-620
+ *   pa_fastq_prefetch_start  the same with the file moved to the device in the
+ *   pa_align_fastq_prefetched  background (overlaps the index build)       src/main.py:286-310
  *   pa_counters_reduce       the multi-GPU sum/min of PseudoAlignment counters
  *                            (read shards of one job); the
  *                            reference is single-process, so this has no
@@ -237,6 +241,45 @@ pa_status pa_align_batch(const pa_index *idx, const uint8_t *seq, const uint8_t 
 pa_status pa_align_fastq_file(const pa_index *idx, const char *path, const pa_params *params,
                               uint64_t read_index_base, pa_result *acc, int32_t threads, uint64_t window_bytes,
                               void *stream, uint64_t *n_reads);
+
+/* The same as one device-resident step: pa_fastq_prefetch_start begins moving
+ * the (plain, not gzip) FASTQ file into device memory on a background thread
+ * (parallel positional reads into a pinned ring, copies in file order) and
+ * returns at once, so that the copy overlaps the caller's FASTA parse and
+ * index build (the dumpalign CLI starts it first); pa_align_fastq_prefetched
+ * then parses and aligns the file window by window (window_bytes, 0: 128 MiB)
+ * as the bytes land, with the records, errors and PA_ENOTCANON of
+ * pa_align_fastq_file.  PA_EUNSUPPORTED for ".gz" paths (use
+ * pa_align_fastq_file).  One align per prefetch; free it afterwards. */
+typedef struct pa_fastq_prefetch pa_fastq_prefetch;
+pa_status pa_fastq_prefetch_start(const char *path, int32_t device, int32_t threads, uint64_t window_bytes,
+                                  pa_fastq_prefetch **out);
+pa_status pa_align_fastq_prefetched(const pa_index *idx, pa_fastq_prefetch *prefetch, const pa_params *params,
+                                    uint64_t read_index_base, pa_result *acc, void *stream, uint64_t *n_reads);
+void pa_fastq_prefetch_free(pa_fastq_prefetch *prefetch);
+
+/* dumpref (KmerReference.get_summary, src/kmer.py:300-329; CLI src/main.py:121-158):
+ * the "Kmers" object of the summary written to file descriptor fd as
+ * json.dumps(indent=4) text at nesting level 1 ("{" ... "\n    }", or "{}"),
+ * from the device index: k-mers in the reference's insertion order (first
+ * occurrence in FASTA order), each with its genomes' descriptions and sorted
+ * positions.  desc_of[g] numbers genome g's description (desc_json[d]: its
+ * JSON string literal, quotes included); genomes sharing a description merge
+ * as dict keys do.  keep[g] (NULL: all): genomes left by EXTSIM -- the index
+ * must then hold ALL genomes, so that the surviving k-mers keep the full
+ * build's order (src/kmer.py:232-245).  Per description: k-mers held by it
+ * with one genome / several (unique_kmers / multi_mapping_kmers), its rank of
+ * first appearance (the Summary key order; UINT64_MAX if absent) and the last
+ * genome met with it (its total_bases); *n_kmers = k-mers written. */
+pa_status pa_index_dumpref(const pa_index *idx, const uint8_t *keep, const uint32_t *desc_of, uint32_t n_desc,
+                           const char *const *desc_json, int32_t fd, int32_t threads, uint64_t *desc_unique,
+                           uint64_t *desc_multi, uint64_t *desc_order, uint32_t *desc_last_genome, uint64_t *n_kmers);
+
+/* Start the HIP runtime and device `device` on a background thread and return
+ * at once (a command-line run calls it first, so the runtime's start-up of
+ * ~0.15 s overlaps its imports and FASTA parse); later calls wait for it as
+ * for any runtime start.  Always PA_OK (errors surface at the first real call). */
+pa_status pa_runtime_start(int32_t device);
 
 /* ---- multi-GPU reduce (RCCL over xGMI) ------------------------------------------- */
 

@@ -10,7 +10,10 @@ the reference that are pure host control flow:
 * the EXTSIM greedy pass (``src/kmer.py:179-230``), fed with the per-identifier
   k-mer statistics that ``ora_extsim_stats`` computes (``src/kmer.py:152-177``);
 * ``PseudoAlignment.get_summary`` (``src/kmer.py:622-657``), computed the
-  reference's way, by walking per-read genome lists in read order.
+  reference's way, by walking per-read genome lists in read order;
+* ``KmerReference.get_summary`` (dumpref, ``src/kmer.py:300-329``) over the
+  reference's own dict (``src/kmer.py:135-150``, pruned by identifier as
+  ``src/kmer.py:232-245`` does), pure Python: small references only.
 """
 
 from __future__ import annotations
@@ -18,6 +21,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+from collections import defaultdict
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -299,3 +303,42 @@ def extsim(identifiers: Sequence[str], genome_lengths: Sequence[int], index: Ora
             kept.append(ident)
     keep_ids = set(kept)
     return [i for i, ident in enumerate(identifiers) if ident in keep_ids], info
+
+
+def dumpref_summary(genomes: Sequence[Tuple[str, str]], k: int, kept_ids=None, similarity_info=None) -> dict:
+    """KmerReference.get_summary() (src/kmer.py:300-329) restated on the
+    reference's dict: ``genomes`` = (description, sequence) in FASTA order;
+    ``kept_ids``: identifiers EXTSIM kept (None: no filtering)."""
+    kmers: Dict[str, Dict[int, set]] = {}
+    for gi, (_, seq) in enumerate(genomes):
+        if k <= 0 or k > len(seq):  # extract_kmers_from_genome, src/kmer.py:84-94
+            continue
+        for pos in range(len(seq) - k + 1):
+            km = seq[pos:pos + k]
+            if "N" in km:  # src/kmer.py:145
+                continue
+            kmers.setdefault(km, {}).setdefault(gi, set()).add(pos)
+    if kept_ids is not None:  # _remove_filtered_genomes_from_kmers, src/kmer.py:232-245
+        for km in list(kmers):
+            m = kmers[km]
+            for gi in list(m):
+                if genomes[gi][0] not in kept_ids:
+                    del m[gi]
+            if not m:
+                del kmers[km]
+    details = {km: {genomes[gi][0]: sorted(p) for gi, p in m.items()} for km, m in kmers.items()}
+    summary: Dict[str, dict] = defaultdict(lambda: {"total_bases": 0, "unique_kmers": 0, "multi_mapping_kmers": 0})
+    per: Dict[str, set] = defaultdict(set)
+    for km, m in kmers.items():
+        for gi in m:
+            d = genomes[gi][0]
+            summary[d]["total_bases"] = len(genomes[gi][1])
+            per[d].add(km)
+    for d, kms in per.items():
+        u = sum(1 for km in kms if len(kmers[km]) == 1)
+        summary[d]["unique_kmers"] = u
+        summary[d]["multi_mapping_kmers"] = len(kms) - u
+    out = {"Kmers": details, "Summary": dict(summary)}
+    if similarity_info is not None:
+        out["Similarity"] = similarity_info
+    return out

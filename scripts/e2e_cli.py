@@ -59,6 +59,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--dir", default="/tmp/pa_e2e")
+    ap.add_argument("--keep", action="store_true", help="leave the generated files in --dir (profiling runs)")
     args = ap.parse_args()
     os.makedirs(args.dir, exist_ok=True)
     fa, fq = os.path.join(args.dir, "c2.fa"), os.path.join(args.dir, "c2.fq")
@@ -112,20 +113,31 @@ def main():
                         env=dict(os.environ, PA_CLI_TIMING="1", PA_STREAM_TIMING="1"))
     stages = {"wall_s": time.perf_counter() - t, "stderr": rt.stderr.strip().splitlines()[-12:]}
     t = time.perf_counter()
+    rs = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                        env=dict(os.environ, PA_CLI_TIMING="1", PA_FAST_EXIT="0"))
+    stages["normal_exit"] = {"wall_s": time.perf_counter() - t, "stderr": rs.stderr.strip().splitlines()[-3:]}
+    t = time.perf_counter()
     subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); import main" % PKG])
     stages["python_and_imports_s"] = time.perf_counter() - t
+    # dumpref of the C2 reference (46 M k-mers: ~6 GB of JSON) to /dev/null
+    t = time.perf_counter()
+    with open(os.devnull, "w") as dn:
+        rd = subprocess.run([sys.executable, os.path.join(PKG, "main.py"), "-t", "dumpref", "-g", fa, "-k", "31"],
+                            stdout=dn, stderr=subprocess.PIPE, text=True)
+    dumpref = {"wall_s": time.perf_counter() - t, "rc": rd.returncode}
     out = {"workload": f"dumpalign C2: 50 x 2 Mbp FASTA, {args.reads} x 150 bp FASTQ, k=31",
            "fastq_bytes": os.path.getsize(fq), "cli_wall_s": cli_s, "cli_reads_per_s": args.reads / cli_s,
            "cli_rc": r.returncode, "cli_stdout_equals_api": r.stdout == summary + "\n",
            "device_parse_path_taken": streamed, "host_path_summary_equal": host_equal,
-           "phases": ph, "cli_stages": stages, "ingest_threads": N.ingest_threads(),
+           "phases": ph, "cli_stages": stages, "dumpref_c2_to_devnull": dumpref, "ingest_threads": N.ingest_threads(),
            "fastq_device_parse_align_GBps": os.path.getsize(fq) / ph["fastq_device_parse_align_s"] / 1e9,
            "fastq_host_parse_GBps": os.path.getsize(fq) / ph["host_parse_fastq_s"] / 1e9}
     if r.returncode:
         out["cli_stderr"] = r.stderr[-2000:]
     print(json.dumps(out), flush=True)
-    for p in (fa, fq):
-        os.remove(p)
+    if not args.keep:
+        for p in (fa, fq):
+            os.remove(p)
 
 
 if __name__ == "__main__":

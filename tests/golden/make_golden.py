@@ -21,7 +21,17 @@ Files written:
   reference ``dumpalign`` CLI for several flag sets;
 * ``extsim_cases.json`` - EXTSIM similarity_info / kept genomes / post-filter
   summaries;
-* ``parser_cases.json`` - FASTA/FASTQ grammar acceptance and error vectors.
+* ``parser_cases.json`` - FASTA/FASTQ grammar acceptance and error vectors;
+* ``dumpref_cases.json`` - the reference CLI's ``dumpref`` stdout for small
+  references (duplicate headers, N runs, k > 32, EXTSIM drops whose k-mers
+  come before kept ones), and for config 1 its length and SHA-256;
+* ``config1.kdb`` / ``config1_sim.kdb`` / ``config1.aln`` - a reference and an
+  alignment SAVED BY THE REFERENCE CLI (``-t reference``, ``-t align``), for
+  the loader of reference-written files; ``dumpref_cases.json`` also holds the
+  reference's stdout of ``dumpref -r`` / ``dumpalign -r`` / ``dumpalign -a``
+  on them.
+
+    python tests/golden/make_golden.py [part ...]   (parts: unit config1 extsim parser dumpref)
 """
 
 from __future__ import annotations
@@ -30,6 +40,7 @@ import json
 import os
 import random
 import shutil
+import hashlib
 import subprocess
 import sys
 import tempfile
@@ -324,11 +335,79 @@ def make_parser_cases():
     print("parser cases:", len(fasta_inputs) + len(fastq_inputs))
 
 
+# ----------------------------------------------------------------------------
+# dumpref, and files saved by the reference CLI
+# ----------------------------------------------------------------------------
+
+def ref_cli(args):
+    r = subprocess.run([sys.executable, "main.py"] + args, cwd=REFDIR, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+def make_dumpref():
+    cases = []
+    cases.append({"name": "extsim_drop_first", "genomes": [("A", "ACGTACCCCCGGGGGACGTA"), ("B", "GGGGGACGTA")],
+                  "k": 5, "filter": 0.5})
+    cases.append({"name": "test_filter_similar", "genomes": [("GenomeA", "AGCTAGCTAGCT"), ("GenomeB", "AGCTAGCTAGCT"),
+                                                             ("GenomeC", "TGCATGCATGCA")], "k": 4, "filter": 0.95})
+    cases.append({"name": "plain_three", "genomes": [("GenomeA", "AGCTAGCTAGCT"), ("GenomeB", "AGCTAGCTAGCT"),
+                                                     ("GenomeC", "TGCATGCATGCA")], "k": 4, "filter": None})
+    cases.append({"name": "duplicate_headers", "genomes": [("dup x", "ACGTTGCAACGTAAC"), ("other", "TTGCAACGTAACGGT"),
+                                                           ("dup x", "CAACGTAACGGTTTT"), ("last", "GGGG")],
+                  "k": 4, "filter": None})
+    cases.append({"name": "n_runs_and_short", "genomes": [("g1", "ACGTNNACGTACGTAACNGTACGT"), ("g2", "ACG"),
+                                                          ("g3", "NNNNNNNN"), ("g4", "CGTACGTAACGTAC")],
+                  "k": 6, "filter": None})
+    rng = random.Random(5)
+    big = ["".join(rng.choice("ACGT") for _ in range(120)) for _ in range(3)]
+    big[2] = big[0][:70] + big[2][70:]
+    cases.append({"name": "k33_multiword", "genomes": [(f"w{i}", g) for i, g in enumerate(big)], "k": 33,
+                  "filter": None})
+    for s_, (thr, sub, fam) in enumerate([(0.5, 0.05, 4), (0.9, 0.01, 3)]):
+        gens = synth.family_genomes(6, 200, seed=300 + s_, family_size=fam, sub_rate=sub, conserved_len=20,
+                                    n_rate=0.0, n_run=0)
+        cases.append({"name": f"family_{s_}", "genomes": [(f"f{s_}_{i} fam", bytes(g).decode())
+                                                          for i, g in enumerate(gens)], "k": 9 + s_, "filter": thr})
+    for c in cases:
+        path = os.path.join(SCRATCH, c["name"] + ".fa")
+        with open(path, "w") as f:
+            f.write(fasta_of(c["genomes"]))
+        args = ["-t", "dumpref", "-g", path, "-k", str(c["k"])]
+        if c["filter"] is not None:
+            args += ["--filter-similar", "--similarity-threshold", str(c["filter"])]
+        c["stdout"] = ref_cli(args)
+    fa1 = os.path.join(HERE, "config1.fa")
+    fq1 = os.path.join(HERE, "config1.fq")
+    out = {"cases": cases}
+    big_out = {}
+    for name, extra in (("config1", []), ("config1_sim", ["--filter-similar", "--similarity-threshold", "0.3"])):
+        txt = ref_cli(["-t", "dumpref", "-g", fa1, "-k", "21"] + extra)
+        big_out[name] = {"args": extra, "length": len(txt), "sha256": hashlib.sha256(txt.encode()).hexdigest(),
+                         "head": txt[:3000], "tail": txt[-3000:]}
+        kdb = os.path.join(HERE, name + ".kdb")
+        ref_cli(["-t", "reference", "-g", fa1, "-k", "21", "-r", kdb] + extra)
+        big_out[name]["dumpref_r_sha256"] = hashlib.sha256(ref_cli(["-t", "dumpref", "-r", kdb]).encode()).hexdigest()
+        big_out[name]["dumpalign_r"] = ref_cli(["-t", "dumpalign", "-r", kdb, "--reads", fq1, "-m", "2"])
+    aln = os.path.join(HERE, "config1.aln")
+    # (the reference's `align -g -k` without -r saves the reference to None and
+    # raises TypeError, src/main.py:366-370, so the alignment is made from -r)
+    ref_cli(["-t", "align", "-r", os.path.join(HERE, "config1.kdb"), "--reads", fq1, "-a", aln, "-p", "3",
+             "--min-kmer-quality", "58", "--max-genomes", "2"])
+    big_out["config1_aln"] = {"dumpalign_a": ref_cli(["-t", "dumpalign", "-a", aln])}
+    out["config1"] = big_out
+    with open(os.path.join(HERE, "dumpref_cases.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("dumpref cases:", len(cases), {k: v.get("length") for k, v in big_out.items()})
+
+
 if __name__ == "__main__":
+    parts = sys.argv[1:] or ["unit", "config1", "extsim", "parser", "dumpref"]
     try:
-        make_unit_cases()
-        make_config1()
-        make_extsim()
-        make_parser_cases()
+        for part, fn in (("unit", make_unit_cases), ("config1", make_config1), ("extsim", make_extsim),
+                         ("parser", make_parser_cases), ("dumpref", make_dumpref)):
+            if part in parts:
+                fn()
     finally:
         shutil.rmtree(SCRATCH, ignore_errors=True)

@@ -6,7 +6,10 @@ Every file is aligned both ways through the drop-in API; the summaries must be
 identical (key order included), and files outside the device-parsed subset of
 the grammar must fall back to the exact path -- which raises the reference's
 own errors.  Small windows (PA_STREAM_WINDOW) make records straddle window
-boundaries (the carried tail)."""
+boundaries (the carried tail).  The prefetched form (pa_fastq_prefetch_start +
+pa_align_fastq_prefetched: the file moved to the device on a background
+thread while the index is built, as the dumpalign CLI does) is held to the
+same bar, with small copy chunks so that the pinned ring wraps."""
 
 import gzip
 import json
@@ -128,3 +131,47 @@ def test_empty_and_bad_extension(ref, tmp_path):
     with pytest.raises(Exception) as ei:
         PseudoAlignment(r).align_reads_from_file(str(tmp_path / "reads.txt"))
     assert type(ei.value).__name__ == "InvalidExtensionError"
+
+
+@pytest.mark.parametrize("window,chunk", [(0, 0), (65536, 4096), (65536, 100000)])
+@pytest.mark.parametrize("kw", PARAMS)
+def test_prefetched_equals_exact(ref, tmp_path, monkeypatch, window, chunk, kw):
+    gens, r = ref
+    monkeypatch.setenv("PA_STREAM_WINDOW", str(window))
+    if chunk:
+        monkeypatch.setenv("PA_PREFETCH_CHUNK", str(chunk))
+    p = tmp_path / "reads.fq"
+    p.write_text(reads_text(gens, 3000, seed=15, lens=(150, 100, 31, 20, 176, 250)))
+    pf = N.FastqPrefetch(str(p))
+    a = PseudoAlignment(r)
+    a.align_reads_from_file(str(p), prefetch=pf, **kw)
+    assert not pf.handle  # consumed and freed
+    assert getattr(a, "_streamed_records", None) == 3000
+    b = PseudoAlignment(r)
+    b.align_reads_from_container(FASTAQFile(str(p)).container, **kw)
+    assert json.dumps(a.get_summary(), indent=4) == json.dumps(b.get_summary(), indent=4)
+
+
+def test_prefetched_outside_subset_and_gz(ref, tmp_path, monkeypatch):
+    gens, r = ref
+    monkeypatch.setenv("PA_PREFETCH_CHUNK", "8192")
+    p = tmp_path / "reads.fq"
+    p.write_bytes(reads_text(gens, 300, seed=16, nl="\r\n").encode())
+    a = PseudoAlignment(r)
+    a.align_reads_from_file(str(p), prefetch=N.FastqPrefetch(str(p)))
+    assert getattr(a, "_streamed_records", None) is None  # the exact path
+    b = PseudoAlignment(r)
+    b.align_reads_from_container(FASTAQFile(str(p)).container)
+    assert a.get_summary() == b.get_summary()
+    ids = [f"r{i}" for i in range(300)]
+    ids[250] = "r3"
+    d = tmp_path / "dup.fq"
+    d.write_text(reads_text(gens, 300, seed=17, ids=ids))
+    with pytest.raises(Exception) as ei:
+        PseudoAlignment(r).align_reads_from_file(str(d), prefetch=N.FastqPrefetch(str(d)))
+    assert "uplicate" in type(ei.value).__name__ + str(ei.value)
+    g = tmp_path / "reads.fq.gz"
+    with gzip.open(g, "wt") as f:
+        f.write(reads_text(gens, 10, seed=18))
+    with pytest.raises(N.PaUnsupported):
+        N.FastqPrefetch(str(g))

@@ -246,6 +246,52 @@ def test_fast_kernel_vs_oracle(cfg):
                                         mkq=full["mkq"], mg=full["mg"]), idents, full["mrq"], full["mkq"], full["mg"])
 
 
+NO_NB = [c for c in SYNTH if c[4] <= 31 and c[0] in (12, 25, 500, 70)]
+
+
+@pytest.mark.parametrize("cfg", NO_NB, ids=[f"G{c[0]}_k{c[4]}_L{c[6]}" for c in NO_NB])
+def test_fast_kernel_vs_oracle_without_neighbour_bits(cfg, monkeypatch):
+    monkeypatch.setenv("PA_NO_NB", "1")
+    test_fast_kernel_vs_oracle(cfg)
+
+
+def test_neighbour_bits_deferred_then_built(tmp_path):
+    """A FASTQ file of few reads is aligned before the neighbour bits exist
+    (index_prepare's reads_hint); the align that brings the reads past
+    kNbReadsPerBase per genome base builds them; results equal the oracle
+    throughout."""
+    from kmer import KmerReference, PseudoAlignment
+    from records import FASTARecordContainer
+    gens = synth.family_genomes(4, 15000, seed=41, family_size=2, sub_rate=0.01, conserved_len=300)
+    c = FASTARecordContainer()
+    c.parse_records(synth.fasta_text([f"d{i}" for i in range(4)], gens, width=60))
+    ref = KmerReference(31, c)
+    oix = O.OracleIndex(gens, 31)
+    seq, qual, _ = synth.sample_reads(gens, 2000, 150, seed=42, err_rate=0.01)
+    p = tmp_path / "few.fq"
+    p.write_text(synth.fastq_text([f"f{i}" for i in range(2000)], seq, qual))
+    pa = PseudoAlignment(ref)
+    pa.align_reads_from_file(str(p), prefetch=N.FastqPrefetch(str(p)))
+    assert getattr(pa, "_streamed_records", None) == 2000
+    bytes_before = ref.index.info().device_bytes
+    s, q, off = seq.reshape(-1), qual.reshape(-1), np.arange(0, 2001 * 150, 150, dtype=np.uint64)
+    o = oix.align(s.tobytes(), q.tobytes(), off, read_base=0, detail=False)
+    stats, *_ = pa._result.fetch()
+    assert stats.tolist() == o.stats.tolist()
+    # 300 k reads > 4 x 60 kb: this align builds the neighbour bits first
+    seq2, qual2, _ = synth.sample_reads(gens, 300000, 150, seed=43, err_rate=0.01)
+    s2, q2 = seq2.reshape(-1), qual2.reshape(-1)
+    off2 = np.arange(0, 300001 * 150, 150, dtype=np.uint64)
+    reads = N.Reads.upload(s2, q2, off2)
+    res = N.Result(ref.index)
+    N.align(ref.index, reads, N.Params.make(1, 1, None, None, None), 5000, res)
+    assert ref.index.info().device_bytes > bytes_before  # the neighbour bits now exist
+    o2 = oix.align(s2.tobytes(), q2.tobytes(), off2, read_base=5000, detail=False)
+    st2, uq, am, fk = res.fetch()
+    assert st2.tolist() == o2.stats.tolist() and uq.tolist() == o2.unique.tolist()
+    assert am.tolist() == o2.ambiguous.tolist()
+
+
 def test_detail_kernel_vs_oracle_per_read():
     gens, s, q, off = _synthetic_case(9, 6000, 3, 0.02, 27, 2500, 130, 0.01, seed=77)
     index = N.Index(gens, 27)
@@ -383,8 +429,13 @@ def _walk_adversarial_case(seed, n_genomes, k):
     return gens, s, q, off
 
 
+@pytest.mark.parametrize("nb", ["nb", "no_nb"])
 @pytest.mark.parametrize("n_genomes,k", [(6, 31), (12, 21), (90, 25), (5, 13)])
-def test_walk_adversarial_vs_oracle(n_genomes, k):
+def test_walk_adversarial_vs_oracle(n_genomes, k, nb, monkeypatch):
+    # no_nb: the tiles without neighbour bits (an index prepared for a file of
+    # few reads, see index_prepare's reads_hint) -- every mismatch window probed
+    if nb == "no_nb":
+        monkeypatch.setenv("PA_NO_NB", "1")
     gens, s, q, off = _walk_adversarial_case(1000 + n_genomes + k, n_genomes, k)
     index = N.Index(gens, k)
     oix = O.OracleIndex(gens, k)

@@ -300,3 +300,32 @@ def test_native_parse_file_matches_universal_newlines(kind, tmp_path):
         with open(path, "r", encoding="utf-8") as f:
             assert _records_of(c, kind) == _regex(kind, f.read()), repr(text)
     assert accepted > 500
+
+
+def test_reference_written_kdb_and_aln_load(monkeypatch, tmp_path):
+    """Files saved by the reference CLI (tests/golden/config1*.kdb, config1.aln,
+    made by make_golden.py) load through the restricted unpickler; their own
+    dicts give the reference's dumpref / dumpalign output (no device needed:
+    the index build is stubbed here, the GPU tests run the real one)."""
+    import gzip as gz
+    import hashlib
+    import pickle
+
+    import kmer
+    monkeypatch.setattr(kmer.KmerReference, "_build", lambda self: setattr(self, "_view", None))
+    cases = json.load(open(os.path.join(GOLD, "dumpref_cases.json")))["config1"]
+    for name in ("config1", "config1_sim"):
+        ref = kmer.KmerReference.load(os.path.join(GOLD, name + ".kdb"))
+        assert isinstance(ref, kmer.KmerReference) and ref.kmer_len == 21
+        text = json.dumps(ref.get_summary(), indent=4) + "\n"
+        assert hashlib.sha256(text.encode()).hexdigest() == cases[name]["dumpref_r_sha256"]
+        assert all(isinstance(g, kmer.Record) for g in ref.genomes)
+    aln = kmer.PseudoAlignment.load(os.path.join(GOLD, "config1.aln"))
+    assert json.dumps(aln.get_summary(), indent=4) + "\n" == cases["config1_aln"]["dumpalign_a"]
+    assert all(isinstance(e["mapping_type"], kmer.ReadMappingType) for e in aln.reads.values())
+    # anything but the classes such files hold is refused
+    bad = tmp_path / "bad.kdb"
+    with gz.open(bad, "wb") as f:
+        f.write(b"cos\ngetcwd\n(tR.")
+    with pytest.raises(pickle.UnpicklingError):
+        kmer.KmerReference.load(str(bad))

@@ -104,3 +104,41 @@ def test_oracle_parallel_shards_equal_single_thread():
         assert par.unique.tolist() == one.unique.tolist()
         assert par.ambiguous.tolist() == one.ambiguous.tolist()
         assert par.first_key.tolist() == one.first_key.tolist()
+
+
+# ---- dumpref (src/kmer.py:300-329) --------------------------------------------------
+
+DUMPREF = load("dumpref_cases.json")
+
+
+def _fasta_genomes(path):
+    """(description, sequence) of a FASTA file, through the drop-in parser."""
+    from data_file import FASTAFile
+    return [(r["description"], r["genome"]) for r in FASTAFile(path).container]
+
+
+@pytest.mark.parametrize("case", DUMPREF["cases"], ids=[c["name"] for c in DUMPREF["cases"]])
+def test_oracle_dumpref_cases(case):
+    gold = json.loads(case["stdout"])
+    kept = None
+    if case["filter"] is not None:
+        kept = {i for i, v in gold["Similarity"].items() if v["kept"] == "yes"}
+    out = O.dumpref_summary(case["genomes"], case["k"], kept, gold.get("Similarity"))
+    assert json.dumps(out, indent=4) + "\n" == case["stdout"]
+
+
+def test_oracle_dumpref_config1():
+    import hashlib
+    genomes = _fasta_genomes(os.path.join(GOLD, "config1.fa"))
+    text = json.dumps(O.dumpref_summary(genomes, 21), indent=4) + "\n"
+    g = DUMPREF["config1"]["config1"]
+    assert len(text) == g["length"] and hashlib.sha256(text.encode()).hexdigest() == g["sha256"]
+    # EXTSIM at 0.3 drops genomes: kept set from the oracle's own EXTSIM pass
+    seqs = [s for _, s in genomes]
+    idx = O.OracleIndex(seqs, 21)
+    kept_i, info = O.extsim([d for d, _ in genomes], [len(s) for s in seqs], idx, 0.3)
+    assert len(kept_i) < len(genomes)
+    kept = {genomes[i][0] for i in kept_i}
+    text = json.dumps(O.dumpref_summary(genomes, 21, kept, info), indent=4) + "\n"
+    g = DUMPREF["config1"]["config1_sim"]
+    assert len(text) == g["length"] and hashlib.sha256(text.encode()).hexdigest() == g["sha256"]
