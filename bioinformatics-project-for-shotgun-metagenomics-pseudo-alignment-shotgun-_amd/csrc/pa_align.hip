@@ -887,3 +887,13 @@ pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uin
 }
 
 }  // namespace pa
+
+namespace {
+__global__ void k_warm_align() {}
+}  // namespace
+
+namespace pa {
+// Loads this file's code object (a first launch from a module loads it): the
+// CLI's runtime-start thread calls it so that the load overlaps host work.
+void warm_align(hipStream_t st) { hipLaunchKernelGGL(k_warm_align, dim3(1), dim3(64), 0, st); }
+}  // namespace pa

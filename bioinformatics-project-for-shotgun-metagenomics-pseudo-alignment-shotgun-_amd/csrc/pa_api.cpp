@@ -14,6 +14,9 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -74,7 +77,17 @@ RuntimeStarter g_runtime_starter;
 pa_status pa_runtime_start(int32_t device) {
     if (g_runtime_starter.th.joinable()) return PA_OK;
     g_runtime_starter.th = std::thread([device] {
-        if (hipSetDevice(device) == hipSuccess) hipFree(nullptr);
+        const auto t0 = std::chrono::steady_clock::now();
+        if (hipSetDevice(device) == hipSuccess && hipFree(nullptr) == hipSuccess) {
+            pa::warm_index(nullptr);  // the code objects too, not at the first real launch
+            pa::warm_align(nullptr);
+            pa::warm_fastq(nullptr);
+            pa::warm_dump(nullptr);
+            hipDeviceSynchronize();
+        }
+        if (const char *e = std::getenv("PA_CLI_TIMING"); e && e[0] == '1')
+            fprintf(stderr, "[pa_runtime] HIP runtime started in %.1f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     });
     return PA_OK;
 }
@@ -109,21 +122,8 @@ pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t 
         PA_CHECK(genome_off[g + 1] >= genome_off[g], PA_EINVAL, "genome_off must be non-decreasing");
     const uint64_t total = genome_off[n_genomes] - genome_off[0];
     PA_CHECK(total == 0 || genomes != nullptr, PA_EINVAL, "genomes must not be NULL");
-    // FASTA grammar: genome text is uppercase ACGTN (src/constants.py:1-6, src/records.py:225-233)
-    {
-        static bool ok_tab[256];
-        static bool init = false;
-        if (!init) {
-            for (int i = 0; i < 256; i++) ok_tab[i] = (i == 'A' || i == 'C' || i == 'G' || i == 'T' || i == 'N');
-            init = true;
-        }
-        const unsigned char *s = (const unsigned char *)genomes + genome_off[0];
-        for (uint64_t i = 0; i < total; i++)
-            if (!ok_tab[s[i]]) {
-                set_error("genome text may only contain A, C, G, T and N (byte " + std::to_string(i) + ")");
-                return PA_EINVAL;
-            }
-    }
+    // (FASTA grammar: genome text is uppercase ACGTN, src/constants.py:1-6, src/records.py:225-233 --
+    // checked on the device by the build's encode pass, PA_EINVAL with the first bad byte)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         set_error("no HIP device available (libpa.so has no CPU fallback)");

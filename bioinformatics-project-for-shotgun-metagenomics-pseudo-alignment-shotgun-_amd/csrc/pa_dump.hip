@@ -506,3 +506,13 @@ pa_status index_dumpref(const pa_index *idx, const uint8_t *keep, const uint32_t
 }
 
 }  // namespace pa
+
+namespace {
+__global__ void k_warm_dump() {}
+}  // namespace
+
+namespace pa {
+// Loads this file's code object (a first launch from a module loads it): the
+// CLI's runtime-start thread calls it so that the load overlaps host work.
+void warm_dump(hipStream_t st) { hipLaunchKernelGGL(k_warm_dump, dim3(1), dim3(64), 0, st); }
+}  // namespace pa

@@ -39,6 +39,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <string>
 #include <vector>
 
 #include "pa_device.h"
@@ -51,15 +54,65 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kRun = 16;  // windows per thread in the genome scans
 
+// Windows per thread of the per-genome build scans (insert, fill, tile
+// classes): PA_BUILD_RUN overrides (A/B).  Fewer per thread = more threads in
+// flight per genome launch (the scans are chains of dependent random atomics).
+inline int build_run() {
+    static const int r = [] {
+        const char *e = std::getenv("PA_BUILD_RUN");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 && v <= 256 ? v : kRun;
+    }();
+    return r;
+}
+
+// PA_CLI_TIMING=1: the build's phases on stderr (host wall clock, after a sync)
+struct PhaseTimer {
+    bool on;
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t0, t;
+    std::string out;
+    explicit PhaseTimer(hipStream_t s) : st(s) {
+        const char *e = std::getenv("PA_CLI_TIMING");
+        on = e && e[0] == '1';
+        t0 = t = std::chrono::steady_clock::now();
+    }
+    void mark(const char *name) {
+        if (!on) return;
+        hipStreamSynchronize(st);
+        const auto n = std::chrono::steady_clock::now();
+        char b[96];
+        snprintf(b, sizeof b, "%s%s %.1f", out.empty() ? "" : ", ", name,
+                 std::chrono::duration<double, std::milli>(n - t).count());
+        out += b;
+        t = n;
+    }
+    ~PhaseTimer() {
+        if (on)
+            fprintf(stderr, "[pa_build] %s ms; total %.1f ms\n", out.c_str(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
 inline unsigned grid_for(uint64_t n, unsigned block = kBlock) {
     uint64_t g = (n + block - 1) / block;
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, 1u << 30));
 }
 
-__global__ void k_encode(const uint8_t *__restrict__ ascii, uint8_t *__restrict__ codes, uint64_t n) {
+// ASCII -> 2-bit codes (4: N); *bad = the first byte outside A C G T N (the
+// FASTA grammar's genome alphabet), ~0 if none.
+__global__ void k_encode(const uint8_t *__restrict__ ascii, uint8_t *__restrict__ codes, uint64_t n,
+                         unsigned long long *bad) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (; i < n; i += stride) codes[i] = (uint8_t)base_code(ascii[i]);
+    unsigned long long first = ~0ull;
+    for (; i < n; i += stride) {
+        const uint8_t ch = ascii[i];
+        const uint32_t c = base_code(ch);
+        codes[i] = (uint8_t)c;
+        if (c > 3 && ch != 'N' && first == ~0ull) first = i;
+    }
+    if (first != ~0ull) atomicMin(bad, first);
 }
 
 __global__ void k_fill_u64(uint64_t *p, uint64_t n, uint64_t v) {
@@ -128,11 +181,11 @@ template <int NW>
 __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
                                uint64_t mask0, uint32_t g, Slot<NW> *table, HomeCfg hc, uint32_t *deg,
                                uint32_t *last_g, uint32_t *first_g, unsigned long long *n_kmers, uint32_t *err,
-                               int tile) {
+                               int tile, int wpt) {
     const uint64_t cap = hc.cap;
-    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
     if (w0 >= nwin) return;
-    uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
+    uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
     const uint8_t *s = codes + gstart + w0;
     Key<NW> key;
 #pragma unroll
@@ -259,11 +312,11 @@ __global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t ca
 template <int NW>
 __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
                              uint64_t mask0, uint32_t g, const Slot<NW> *table, HomeCfg hc, const uint32_t *deg,
-                             uint32_t *last_g, uint32_t *fill, const uint64_t *off, uint32_t *lists) {
+                             uint32_t *last_g, uint32_t *fill, const uint64_t *off, uint32_t *lists, int wpt) {
     const uint64_t cap = hc.cap;
-    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
     if (w0 >= nwin) return;
-    uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
+    uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
     const uint8_t *s = codes + gstart + w0;
     Key<NW> key;
 #pragma unroll
@@ -449,10 +502,10 @@ __global__ void k_tile_pack(const uint8_t *__restrict__ codes, uint64_t n, uint6
 template <int NW>
 __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k, uint64_t mask0,
                            Slot<NW> *table, HomeCfg hc, uint32_t *tile_cls, uint32_t g, uint32_t G,
-                           const uint32_t *__restrict__ class_genomes, int local) {
-    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kRun;
+                           const uint32_t *__restrict__ class_genomes, int local, int wpt) {
+    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
     if (w0 >= nwin) return;
-    uint64_t w1 = min(w0 + (uint64_t)kRun, nwin);
+    uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
     const uint8_t *s = codes + gstart + w0;
     Key<NW> key;
 #pragma unroll
@@ -764,6 +817,7 @@ template <int NW>
 pa_status build_nw(pa_index *idx, hipStream_t st) {
     const uint32_t G = idx->n_genomes;
     const int k = (int)idx->k;
+    const int wpt = build_run();
     const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
     const uint64_t cap = idx->cap;
     Slot<NW> *table = (Slot<NW> *)idx->table;
@@ -799,9 +853,9 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
         if (k <= 0 || (uint64_t)k > len) continue;
         uint64_t nwin = len - k + 1;
-        hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
+        hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
                            idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, deg, last_g, aux, cnt + 0,
-                           err, idx->tile_n > 0 ? 1 : 0);
+                           err, idx->tile_n > 0 ? 1 : 0, wpt);
     }
     B_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_build_prep<NW>, dim3(grid_for(cap, kBlock) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0,
@@ -827,9 +881,9 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
             if ((uint64_t)k > len) continue;
             uint64_t nwin = len - k + 1;
-            hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
+            hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
                                idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, deg, last_g, aux,
-                               off, lists);
+                               off, lists, wpt);
         }
         B_HIP(hipGetLastError());
         // distinct genome sets: a hash over the multi slots' genome lists.  A
@@ -979,6 +1033,7 @@ template <int NW>
 pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
     const uint32_t G = idx->n_genomes;
     const int k = (int)idx->k;
+    const int wpt = build_run();
     const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
     Slot<NW> *table = (Slot<NW> *)idx->table;
 #define B_HIP(call) PA_HIP(call)
@@ -997,9 +1052,9 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
             if ((uint64_t)k > len) continue;
             uint64_t nwin = len - k + 1;
-            hipLaunchKernelGGL(k_tile_cls<NW>, dim3(grid_for((nwin + kRun - 1) / kRun)), dim3(kBlock), 0, st,
+            hipLaunchKernelGGL(k_tile_cls<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
                                idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls, g, G,
-                               idx->class_genomes, idx->tpos_local);
+                               idx->class_genomes, idx->tpos_local, wpt);
         }
         {  // genome of every 2^16-th position: genome_of is then one or two goff steps
             const uint64_t nb_ = (n >> 16) + 2;
@@ -1146,6 +1201,7 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
 
 pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
                       hipStream_t st, bool defer_tiles) {
+    PhaseTimer tm(st);
     idx->k = k;
     idx->nw = k > 0 ? key_words(k) : 1;
     idx->n_genomes = n;
@@ -1180,16 +1236,28 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     PA_HIP(hipMemcpyAsync(idx->goff, idx->h_goff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
     if (total > 0) {
         uint8_t *ascii = nullptr;  // ASCII staging buffer, freed before the table is allocated
+        unsigned long long *bad = nullptr, h_bad = ~0ull;
         PA_HIP(hipMalloc(&ascii, total));
-        hipError_t e = hipMemcpyAsync(ascii, genomes + goff[0], total, hipMemcpyHostToDevice, st);
+        PA_HIP(hipMalloc(&bad, 8));
+        tm.mark("alloc");
+        hipError_t e = hipMemsetAsync(bad, 0xFF, 8, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(ascii, genomes + goff[0], total, hipMemcpyHostToDevice, st);
+        tm.mark("upload");
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_encode, dim3(grid_for(total) > 65536 ? 65536 : grid_for(total)), dim3(kBlock), 0, st,
-                               ascii, idx->codes, total);
-            e = hipStreamSynchronize(st);
+                               ascii, idx->codes, total, bad);
+            e = hipMemcpyAsync(&h_bad, bad, 8, hipMemcpyDeviceToHost, st);
         }
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
         hipFree(ascii);
+        hipFree(bad);
         PA_HIP(e);
+        if (h_bad != ~0ull) {
+            set_error("genome text may only contain A, C, G, T and N (byte " + std::to_string(h_bad) + ")");
+            return PA_EINVAL;
+        }
     }
+    tm.mark("encode");
     // Table capacity (whole 64-B lines).  Load 1/4 of the genome windows when
     // the table fits a third of the free device memory (absent keys -- the
     // sequencing-error windows -- then end in their home slot 3 times out of
@@ -1271,6 +1339,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     PA_HIP(hipMalloc(&idx->table, idx->cap * sb));
     PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
     idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
+    tm.mark("table");
     if (k <= 0 || windows == 0) return PA_OK;
     pa_status rc = PA_EUNSUPPORTED;
     switch (idx->nw) {
@@ -1281,8 +1350,11 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         case 5: rc = build_nw<5>(idx, st); break;
         default: set_error("unsupported k");
     }
+    tm.mark("insert + sets");
     if (rc != PA_OK || defer_tiles) return rc;
-    return index_prepare(idx, st);
+    rc = index_prepare(idx, st);
+    tm.mark("tiles");
+    return rc;
 }
 
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
@@ -1399,4 +1471,14 @@ pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_
     return PA_OK;
 }
 
+}  // namespace pa
+
+namespace {
+__global__ void k_warm_index() {}
+}  // namespace
+
+namespace pa {
+// Loads this file's code object (a first launch from a module loads it): the
+// CLI's runtime-start thread calls it so that the load overlaps host work.
+void warm_index(hipStream_t st) { hipLaunchKernelGGL(k_warm_index, dim3(1), dim3(64), 0, st); }
 }  // namespace pa

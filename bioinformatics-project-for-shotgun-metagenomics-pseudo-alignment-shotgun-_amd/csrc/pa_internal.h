@@ -166,4 +166,8 @@ pa_status index_dumpref(const pa_index *idx, const uint8_t *keep, const uint32_t
                         uint64_t *desc_order, uint32_t *desc_last_genome, uint64_t *n_kmers_out, hipStream_t st);
 pa_status result_reset(pa_result *res, hipStream_t st);
 void index_release(pa_index *idx);
+void warm_index(hipStream_t st);  // one empty launch per source file: loads its code object
+void warm_align(hipStream_t st);
+void warm_fastq(hipStream_t st);
+void warm_dump(hipStream_t st);
 }  // namespace pa

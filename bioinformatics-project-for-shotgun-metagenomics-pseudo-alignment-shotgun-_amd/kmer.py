@@ -207,6 +207,8 @@ class KmerReference:
         if not isinstance(k, int):
             raise TypeError(f"k must be an int, got {type(k)}")
         self.genomes: List[Record] = list(fasta_record_container)
+        pg = getattr(fasta_record_container, "packed_genomes", None)
+        self._packed = pg(self.genomes) if pg is not None else None  # (the parser's concatenated genomes)
         self._all_genomes: Optional[List[Record]] = None  # before EXTSIM dropped any (k-mer view order)
         self._ref_kmers: Optional[Dict[str, Dict[Record, Set[int]]]] = None  # the dict of a reference-written .kdb
         self.kmer_len: int = k
@@ -220,8 +222,9 @@ class KmerReference:
     def _build(self) -> None:
         # the align-side view (tiles, neighbour bits) is made at the first align:
         # an index that EXTSIM then rebuilds from the kept genomes never needs it
+        packed, self._packed = getattr(self, "_packed", None), None  # (only for the first build)
         self._index = N.Index([g["genome"] for g in self.genomes], self.kmer_len, device=self._device,
-                              defer_tiles=True)
+                              defer_tiles=True, packed=packed)
         self._view: Optional[Dict[str, Dict[Record, Set[int]]]] = None
 
     @property
@@ -248,7 +251,7 @@ class KmerReference:
     # -- persistence ----------------------------------------------------------
 
     def __getstate__(self):
-        state = {k: v for k, v in self.__dict__.items() if k not in ("_index", "_view")}
+        state = {k: v for k, v in self.__dict__.items() if k not in ("_index", "_view", "_packed")}
         return state
 
     def __setstate__(self, state):

@@ -9,11 +9,14 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
+import time
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+_TIMING = os.environ.get("PA_CLI_TIMING") == "1"  # (diagnostic stage times on stderr)
 LIB_PATH = os.environ.get("PA_LIBRARY", os.path.join(HERE, "libpa.so"))
 
 PA_OK, PA_EINVAL, PA_ETYPE, PA_ENOMEM, PA_EDEVICE, PA_EUNSUPPORTED, PA_EINTERNAL, PA_ENOTCANON, PA_EIO = range(9)
@@ -321,10 +324,13 @@ class Index:
     """A device-resident k-mer index (pa_index)."""
 
     def __init__(self, genomes: Sequence, k: int, device: Optional[int] = None, stream=None,
-                 defer_tiles: bool = False):
+                 defer_tiles: bool = False, packed: Optional[Tuple[np.ndarray, np.ndarray]] = None):
         """defer_tiles: build the table and genome sets only (PA_BUILD_DEFER_TILES);
-        the align-side view is made by prepare() or the first align."""
-        buf, off = concat(genomes)
+        the align-side view is made by prepare() or the first align.  packed:
+        the genomes already concatenated (uint8 bytes, uint64 offsets)."""
+        t0 = time.perf_counter()
+        buf, off = packed if packed is not None else concat(genomes)
+        t1 = time.perf_counter()
         self.device = default_device() if device is None else int(device)
         self.k = int(k)
         h = P()
@@ -332,6 +338,9 @@ class Index:
         _check(lib().pa_index_build_ex(self.device, buf.ctypes.data_as(ctypes.c_char_p) if buf.size else None,
                                        _ptr(off), len(off) - 1, kk, PA_BUILD_DEFER_TILES if defer_tiles else 0,
                                        _stream(stream), ctypes.byref(h)))
+        if _TIMING:
+            print(f"[pa_index] concat {1e3 * (t1 - t0):.1f} ms, pa_index_build_ex {1e3 * (time.perf_counter() - t1):.1f} "
+                  "ms", file=sys.stderr, flush=True)
         self._h = h
         self.n_genomes = len(off) - 1
 

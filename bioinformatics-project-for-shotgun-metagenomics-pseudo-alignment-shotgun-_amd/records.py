@@ -154,11 +154,22 @@ class FASTARecordContainer(RecordContainer):
     SECTION_NAMES = ("description", "genome")
 
     def load_columns(self, cols) -> None:
-        """Records from native parser columns (pa_native.SeqColumns)."""
+        """Records from native parser columns (pa_native.SeqColumns).  The
+        concatenated genome bytes are kept (``packed``): an index of exactly
+        these records is built from them without concatenating again."""
         seq, off = cols.seq, cols.off
         for i, name in enumerate(cols.names):
             genome = seq[int(off[i]):int(off[i + 1])].tobytes().decode("ascii")
             self._records.append(Record([Section("description", name), Section("genome", genome)]))
+        self._packed = (seq, np.asarray(off, dtype=np.uint64), list(self._records))
+
+    def packed_genomes(self, records: Sequence[Record]):
+        """(bytes, offsets) of ``records`` concatenated, if they are exactly this
+        container's natively parsed records in order; else None."""
+        p = getattr(self, "_packed", None)
+        if p is None or len(records) != len(p[2]) or any(a is not b for a, b in zip(records, p[2])):
+            return None
+        return p[0], p[1]
 
     def parse_records(self, data: str) -> None:
         if not self._records:
