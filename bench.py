@@ -134,6 +134,8 @@ def traffic_pass(args, cfg, kept_path):
            "--reads-per-gpu", str(cfg["reads_per_gpu"]), "--steps", "2", "--warmup", "1"]
     if args.genome_len:
         cmd += ["--genome-len", str(args.genome_len)]
+    if args.params is not None:
+        cmd += ["--params", args.params]
     if kept_path:
         cmd += ["--kept-file", kept_path]
     env = dict(os.environ, TMPDIR="/tmp")
@@ -235,8 +237,13 @@ def main():
     ap.add_argument("--kept-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--reduce", choices=("torch", "capi"), default="torch",
                     help="N > 1: all-reduce through torch.distributed (RCCL) or libpa's pa_counters_reduce")
+    ap.add_argument("--params", default=None,
+                    help='override the filter arguments, JSON, e.g. \'{"mg": 10}\' (experiments; named in config)')
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
+    if args.params is not None:
+        cfg["params"] = json.loads(args.params)
+        cfg["name"] += f" [filters overridden: {args.params}]"
     if args.reads_per_gpu:
         cfg["reads_per_gpu"] = args.reads_per_gpu
     if args.genome_len:

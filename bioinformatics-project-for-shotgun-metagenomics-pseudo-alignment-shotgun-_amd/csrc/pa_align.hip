@@ -713,11 +713,58 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
     return PA_OK;
 }
 
-pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t base, pa_result *acc,
+// Smallest quality byte of all reads and smallest read length (grid-stride).
+__global__ void k_reads_qstats(const uint8_t *__restrict__ qual, const uint64_t *__restrict__ off, uint64_t n,
+                               uint32_t *out) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t b0 = off[0], b1 = off[n];
+    uint32_t qm = 255, lm = 0xFFFFFFFFu;
+    for (uint64_t i = b0 + tid; i < b1; i += stride) qm = min(qm, (uint32_t)qual[i]);
+    for (uint64_t r = tid; r < n; r += stride) lm = min(lm, (uint32_t)min<uint64_t>(off[r + 1] - off[r], 0xFFFFFFFFull));
+    for (int o = 32; o > 0; o >>= 1) {
+        qm = min(qm, (uint32_t)__shfl_down(qm, o));
+        lm = min(lm, (uint32_t)__shfl_down(lm, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&out[0], qm);
+        atomicMin(&out[1], lm);
+    }
+}
+
+// Quality thresholds no read can fail, dropped from the pass: every read's mean
+// and every window's mean are >= the smallest quality byte, so with
+// --min-read-quality / --min-kmer-quality <= that byte nothing is filtered
+// (src/kmer.py:420, 587: strict <) -- e.g. C3's literal 20 / 25 against
+// FASTQ qualities >= '!' (33), quirk 5.  Reads of length 0 keep the read test.
+pa_status effective_params(const pa_reads *r, const DevParams &p, DevParams &out, hipStream_t st) {
+    out = p;
+    if (!(p.flags & (F_MRQ | F_MKQ)) || !r->qual || r->n == 0 || std::getenv("PA_NO_QELIDE")) return PA_OK;
+    pa_reads *w = const_cast<pa_reads *>(r);  // (a cache of immutable data)
+    if (w->q_min < 0) {
+        uint32_t *d = nullptr, h[2] = {255, 0xFFFFFFFFu};
+        PA_HIP(hipMalloc(&d, 8));
+        PA_HIP(hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_reads_qstats, dim3(2048), dim3(256), 0, st, r->qual, r->off, r->n, d);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        hipFree(d);
+        PA_HIP(e);
+        w->q_min = (int32_t)h[0];
+        w->len_min = (int64_t)h[1];
+    }
+    if ((p.flags & F_MRQ) && w->len_min > 0 && p.mrq <= w->q_min) out.flags &= ~F_MRQ;
+    if ((p.flags & F_MKQ) && p.mkq <= w->q_min) out.flags &= ~F_MKQ;
+    return PA_OK;
+}
+
+pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_t base, pa_result *acc,
                 hipStream_t st) {
     if (r->n == 0) return PA_OK;
     PA_TRY(index_note_reads(idx, r->n, st));  // (the neighbour bits, once enough reads came)
     PA_TRY(reserve_queues(idx, r->n));
+    DevParams p;
+    PA_TRY(effective_params(r, p_in, p, st));
     AlignArgs a = make_args(idx, r, p, base);
     const uint32_t G = idx->n_genomes;
     a.stats = (unsigned long long *)acc->sum_block;

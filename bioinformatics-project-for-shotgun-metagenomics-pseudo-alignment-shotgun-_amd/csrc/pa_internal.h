@@ -122,6 +122,10 @@ struct pa_reads {
     uint8_t *seq = nullptr;
     uint8_t *qual = nullptr;
     uint64_t *off = nullptr;  // [n+1]
+    // (pa_align) the smallest quality byte and read length, once measured
+    // (-1: not yet): quality thresholds no read can fail are then not applied
+    int32_t q_min = -1;
+    int64_t len_min = -1;
 };
 
 struct pa_result {

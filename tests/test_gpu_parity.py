@@ -557,3 +557,28 @@ def test_pseudo_align_random_big_kmers_property(seed):
     qual, _ = O.concat([rec["quality_sequence"]])
     o = oix.align(seq, qual, off, m=m, p=p)
     assert int(o.types[0]) == result.value
+
+
+@pytest.mark.parametrize("mrq,mkq", [(40, None), (None, 40), (40, 40), (41, 40), (40, 41), (20, 25), (0, 0)])
+def test_quality_thresholds_no_read_can_fail(mrq, mkq, monkeypatch):
+    """pa_align drops a quality threshold at or below the batch's smallest
+    quality byte (no read or window mean can be below it, src/kmer.py:420, 587);
+    the results equal the oracle's and the un-elided pass's, at the boundary
+    (threshold == smallest byte) and one above it."""
+    gens, s, q, off = _synthetic_case(10, 20000, 5, 0.01, 31, 5000, 150, 0.01, seed=91)
+    q = np.maximum(q, 40).astype(np.uint8)  # smallest quality byte 40
+    q[5 * 150 + 7] = 40
+    index = N.Index(gens, 31)
+    oix = O.OracleIndex(gens, 31)
+    out = []
+    for elide in ("1", "0"):
+        if elide == "0":
+            monkeypatch.setenv("PA_NO_QELIDE", "1")
+        reads = N.Reads.upload(s, q, off)
+        res = N.Result(index)
+        N.align(index, reads, N.Params.make(1, 1, mrq, mkq, 10), 0, res)
+        out.append([x.tolist() for x in res.fetch()])
+    o = oix.align(s.tobytes(), q.tobytes(), off, m=1, p=1, mrq=mrq, mkq=mkq, mg=10, read_base=0, detail=False)
+    ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+    assert out[0] == out[1]
+    assert out[0] == [o.stats.tolist(), o.unique.tolist(), o.ambiguous.tolist(), ofk.tolist()]
