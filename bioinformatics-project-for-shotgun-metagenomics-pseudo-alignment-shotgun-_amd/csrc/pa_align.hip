@@ -731,6 +731,29 @@ __global__ void k_reads_qstats(const uint8_t *__restrict__ qual, const uint64_t 
     }
 }
 
+// The batch's smallest quality byte and read length (pa_reads.q_min / len_min),
+// measured when the reads are made (upload, synthesis; the FASTQ parser takes
+// them from its own pass).
+pa_status reads_measure(pa_reads *r, hipStream_t st) {
+    r->q_min = 255;
+    r->len_min = 0;
+    if (!r->qual || r->n == 0) return PA_OK;
+    uint32_t *d = nullptr, h[2] = {255, 0xFFFFFFFFu};
+    PA_HIP(hipMalloc(&d, 8));
+    hipError_t e = hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_reads_qstats, dim3(2048), dim3(256), 0, st, r->qual, r->off, r->n, d);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    hipFree(d);
+    PA_HIP(e);
+    r->q_min = (int32_t)h[0];
+    r->len_min = (int64_t)h[1];
+    return PA_OK;
+}
+
 // Quality thresholds no read can fail, dropped from the pass: every read's mean
 // and every window's mean are >= the smallest quality byte, so with
 // --min-read-quality / --min-kmer-quality <= that byte nothing is filtered
@@ -739,22 +762,9 @@ __global__ void k_reads_qstats(const uint8_t *__restrict__ qual, const uint64_t 
 pa_status effective_params(const pa_reads *r, const DevParams &p, DevParams &out, hipStream_t st) {
     out = p;
     if (!(p.flags & (F_MRQ | F_MKQ)) || !r->qual || r->n == 0 || std::getenv("PA_NO_QELIDE")) return PA_OK;
-    pa_reads *w = const_cast<pa_reads *>(r);  // (a cache of immutable data)
-    if (w->q_min < 0) {
-        uint32_t *d = nullptr, h[2] = {255, 0xFFFFFFFFu};
-        PA_HIP(hipMalloc(&d, 8));
-        PA_HIP(hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_reads_qstats, dim3(2048), dim3(256), 0, st, r->qual, r->off, r->n, d);
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        hipFree(d);
-        PA_HIP(e);
-        w->q_min = (int32_t)h[0];
-        w->len_min = (int64_t)h[1];
-    }
-    if ((p.flags & F_MRQ) && w->len_min > 0 && p.mrq <= w->q_min) out.flags &= ~F_MRQ;
-    if ((p.flags & F_MKQ) && p.mkq <= w->q_min) out.flags &= ~F_MKQ;
+    if (r->q_min < 0) PA_TRY(reads_measure(const_cast<pa_reads *>(r), st));  // (not measured at creation)
+    if ((p.flags & F_MRQ) && r->len_min > 0 && p.mrq <= r->q_min) out.flags &= ~F_MRQ;
+    if ((p.flags & F_MKQ) && p.mkq <= r->q_min) out.flags &= ~F_MKQ;
     return PA_OK;
 }
 

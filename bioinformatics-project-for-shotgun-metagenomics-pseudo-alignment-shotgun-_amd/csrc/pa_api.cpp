@@ -268,6 +268,7 @@ pa_status pa_reads_upload(int32_t device, const uint8_t *seq, const uint8_t *qua
         delete[] tmp;
         if (e != hipSuccess) return fail(e);
     }
+    if (pa::reads_measure(r, st) != PA_OK) return fail(hipErrorUnknown);
     *out = r;
     return PA_OK;
 }
@@ -285,6 +286,7 @@ pa_status pa_reads_synthesize_mix(const pa_index *idx, uint64_t n_reads, uint32_
     PA_CHECK(r != nullptr, PA_ENOMEM, "out of host memory");
     pa_status rc = pa::reads_synthesize(idx, r, n_reads, read_len, first_read, seed, sub_rate, rc_rate, foreign_rate,
                                         as_stream(stream));
+    if (rc == PA_OK) rc = pa::reads_measure(r, as_stream(stream));
     if (rc != PA_OK) {
         hipFree(r->seq); hipFree(r->qual); hipFree(r->off);
         delete r;

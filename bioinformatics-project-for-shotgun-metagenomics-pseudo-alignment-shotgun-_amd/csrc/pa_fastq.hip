@@ -65,6 +65,7 @@ struct Meta {                 // window bookkeeping, device -> host once per win
     unsigned long long end;   // first byte after the last complete record (absolute)
     unsigned long long max_len;
     unsigned long long err;
+    unsigned long long q_low;  // 255 - the smallest quality byte so far (0: none yet)
 };
 
 // Per-byte "is a line feed" bits of a dword, in [lo, hi) of absolute positions.
@@ -265,12 +266,12 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *D, uint64_t t0, 
     const uint32_t m = chunk_lf(D, c0, lo, hi);
     uint32_t total;
     const uint64_t li0 = tile_off[blockIdx.x] + block_excl_scan256(__popc(m), s_wave, total);
-    if (c0 + 16 <= lo || c0 >= hi) return;
+    uint32_t bad = 0, q_low = 0;
+    if (!(c0 + 16 <= lo || c0 >= hi)) {  // (no early return: the wave reduces q_low below)
     const uint4 v = *(const uint4 *)(D + c0);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint64_t li = li0;
     uint64_t ls = li ? (uint64_t)nl[li - 1] + 1 : lo;  // start of the line holding byte c0 (or lo)
-    uint32_t bad = 0;
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         const uint64_t p = c0 + j;
@@ -289,9 +290,13 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *D, uint64_t t0, 
         } else if (type == 3) {
             if (!id_byte(c)) bad = 1;
             else if (rec_off[r] + col < rec_off[r + 1]) qual[rec_off[r] + col] = c;
+            q_low = max(q_low, 255u - c);
         }
     }
+    }
     if (bad) atomicOr(&meta_out->err, (unsigned long long)kErrGrammar);
+    for (int o = 32; o > 0; o >>= 1) q_low = max(q_low, (uint32_t)__shfl_down(q_low, o));
+    if (lane_id() == 0 && q_low) atomicMax(&meta_out->q_low, (unsigned long long)q_low);
 }
 
 struct Source {  // plain file (positional reads on host threads) or gzip stream
@@ -457,6 +462,8 @@ pa_status parse_align_window(ParseBufs &B, const uint8_t *D, uint64_t lo, uint64
     r.seq = B.seq;
     r.qual = B.qual;
     r.off = (uint64_t *)B.rec_off;
+    r.q_min = 255 - (int32_t)B.h_meta->q_low;  // (over the file so far: <= this window's smallest byte)
+    r.len_min = 1;                              // (the grammar: a non-empty sequence)
     PA_TRY(align(idx, &r, prm, base, acc, st));
     out.records = R;
     return PA_OK;

@@ -157,6 +157,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p, uint64_t b
 pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uint8_t *type, uint32_t *qf,
                        uint32_t *hr, uint64_t *list_off, uint32_t *lists, uint64_t list_cap, uint64_t *list_total,
                        hipStream_t st);
+pa_status reads_measure(pa_reads *r, hipStream_t st);  // q_min / len_min of a batch (at its creation)
 pa_status ensure_workspace(pa_index *idx, size_t bytes);
 pa_status reserve_queues(pa_index *idx, uint64_t n);  // align queues for batches of up to n reads
 pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,

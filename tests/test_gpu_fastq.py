@@ -56,7 +56,8 @@ def both_ways(ref_obj, path, **kw):
     return a, b
 
 
-PARAMS = [dict(), dict(m=2, p=0), dict(min_read_quality=58, min_kmer_quality=60, max_genomes=2)]
+PARAMS = [dict(), dict(m=2, p=0), dict(min_read_quality=58, min_kmer_quality=60, max_genomes=2),
+          dict(min_read_quality=20, min_kmer_quality=25, max_genomes=10)]  # (C3 literal: elided thresholds)
 
 
 @pytest.mark.parametrize("window", [0, 65536])
