@@ -77,6 +77,8 @@ struct AlignArgs {
     int walk_rounds;
     int tpos_local;                 // slot.tpos genome-local (first_pos), else concatenated
     uint32_t lane_maxpend;  // lane kernel: more unwalked windows than this -> wave kernel
+    int lane_noanchor;      // lane kernel: a read without any seed in the index probes all its windows
+                            // (Bloom filter first) instead of going to the wave kernel
     int dbg_mode;  // PA_STATS / PA_DISSECT builds: stop each read after phase N (timing dissection; results invalid)
     const uint8_t *seq;
     const uint8_t *qual;
@@ -641,6 +643,8 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tpos_local = idx->tpos_local;
     a.lane_maxpend = 96;
     if (const char *e = std::getenv("PA_LANE_MAXPEND")) a.lane_maxpend = (uint32_t)std::atoi(e);
+    a.lane_noanchor = a.bloom != nullptr;  // (without the filter every window costs a table line)
+    if (const char *e = std::getenv("PA_LANE_NOANCHOR")) a.lane_noanchor = e[0] == '1';
     if (const char *e = std::getenv("PA_WALK_ROUNDS")) a.walk_rounds = std::atoi(e);
     if (const char *e = std::getenv("PA_DBG_MODE")) a.dbg_mode = std::atoi(e);
     a.seq = r->seq;

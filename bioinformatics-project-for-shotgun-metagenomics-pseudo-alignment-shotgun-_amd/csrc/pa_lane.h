@@ -38,7 +38,10 @@
 // included k-mer contains g; src/kmer.py:464-480).  Any other read -- no
 // anchor, a local repeat, a non-ACGT base, a second re-anchoring, a read longer
 // than the lane limits -- is queued whole for the wave kernel, which handles
-// every case exactly.
+// every case exactly.  A read none of whose seeds is in the index (reverse-
+// complemented, unindexed organism) lists all its windows for the cooperative
+// probes (Bloom filter first): nothing found -> UNMAPPED, only multi-genome
+// k-mers -> AMBIGUOUS, a specific one -> walked again from it.
 
 constexpr int kLaneMaxW = 128;    // windows per read on the lane path
 constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
@@ -72,7 +75,6 @@ struct __align__(16) LaneWave {
     unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 40) | position
     uint32_t flags[64];              // bit 0: specific k-mer found off the walk; bits 2..: unspecific ones found
     uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
-    uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
     uint32_t again_r[128];           // reads to walk again from a specific k-mer found off their walk,
     unsigned long long again_a[128]; //   and that anchor: (window << 40) | position
     uint32_t n_hr[64], n_qf[64];     // per-lane window counters of the settled reads (kept out of VGPRs)
@@ -444,7 +446,23 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #pragma unroll
         for (int i = 0; i < NSEED; i++)
             if (at < 0 && stp[i] != ~0ull && (pass == 1 || scls[i] < a.G)) at = i;
-    if (at < 0) return (void)LANE_HARD_WHY(3);  // no anchor
+    if (at < 0) {
+        // no seed k-mer is in the index (a read of an unindexed organism, a
+        // reverse-complemented read, or many errors): every window is probed by
+        // the wave together, the Bloom filter first (lane_probe_wave).  Nothing
+        // found -> UNMAPPED; only multi-genome k-mers -> AMBIGUOUS with an empty
+        // list (no specific k-mer, src/kmer.py:458-461); a specific one -> the
+        // read is walked again from it, like any re-anchored read
+        if (!a.lane_noanchor) return (void)LANE_HARD_WHY(3);
+        S.atp = ~0ull;  // (no anchor: lane_walk is skipped)
+        S.acls = NONE;
+        S.aw = 0;
+        S.g = 0;
+        S.P0 = (W >= 64 ? ~0ull : ((1ull << W) - 1)) & ~S.F0;
+        S.P1 = (W > 64 ? (W >= 128 ? ~0ull : ((1ull << (W - 64)) - 1)) : 0ull) & ~S.F1;
+        S.kind = LANE_WALK;
+        return;
+    }
     S.atp = stp[0];
     S.acls = scls[0];
     S.aw = sw[0];
@@ -709,6 +727,21 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     }
 }
 
+// Position of the j-th (0-based) set bit of x (j < popcount(x)).
+__device__ __forceinline__ uint32_t select64(uint64_t x, uint32_t j) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t w = 32; w > 0; w >>= 1) {
+        const uint32_t c = (uint32_t)__popcll(x & ((1ull << w) - 1));
+        if (j >= c) {
+            j -= c;
+            pos += w;
+            x >>= w;
+        }
+    }
+    return pos;
+}
+
 // Phase 3 (whole wave): probe windows (Q0, Q1) of the walking lanes; `reset`
 // clears the lanes' outcomes first (LW.flags / hr / cand accumulate otherwise).
 __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW, const LaneRead &S, uint64_t Q0,
@@ -729,37 +762,39 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
 #ifdef PA_STATS
     if (lane == 0 && total) atomicAdd(&a.dbg[14], (unsigned long long)total);
 #endif
+    wave_sync();  // the lanes' rows (written by their owners) are read by any lane below
     for (uint32_t base = 0; base < total; base += kPassEntries) {
-        // this pass's entries of the lane: global indices [max(pre, base), min(pre + c, base + 256))
-        const uint32_t lo = max(pre, base), hi = min(pre + c, base + (uint32_t)kPassEntries);
-        for (uint32_t e = lo; e < hi; e++) {
-            uint32_t w;
-            if (Q0) {
-                w = __builtin_ctzll(Q0);
-                Q0 &= Q0 - 1;
-            } else {
-                w = 64 + __builtin_ctzll(Q1);
-                Q1 &= Q1 - 1;
-            }
-            LW.list[e - base] = (uint16_t)((lane << 8) | w);
-        }
-        wave_sync();
+        // entry base + NPR * lane + i of the wave's concatenated window lists:
+        // its owner lane (the first whose inclusive count exceeds it, by a
+        // binary search over the lanes' counts) and the owner's j-th window
+        // (the j-th set bit of its mask) -- every lane finds its own entries,
+        // no lane writes a list serially
         const uint32_t cnt = min(total - base, (uint32_t)kPassEntries);
         constexpr int NPR = PA_LANE_PROBES;
         uint64_t key4[NPR];
         uint32_t tag4[NPR], act = 0;
 #pragma unroll
         for (int i = 0; i < NPR; i++) {
-            const uint32_t e = NPR * lane + i;
+            const uint32_t e = NPR * lane + i, g = base + e;
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t step = 32; step > 0; step >>= 1) {
+                const uint32_t v = (uint32_t)__shfl((int)incl, (int)(lo + step - 1));
+                lo += v <= g ? step : 0u;
+            }
+            const uint32_t owner = lo < 63u ? lo : 63u;
+            const uint32_t pre_o = (uint32_t)__shfl((int)pre, (int)owner);
+            const uint64_t q0 = shfl64(Q0, (int)owner), q1 = shfl64(Q1, (int)owner);
             key4[i] = 0;
             tag4[i] = 0;
             if (e < cnt) {
-                const uint32_t t = LW.list[e];
-                const uint64_t *row = LW.R[t >> 8];
-                const uint32_t o = 2 * (t & 255), q = o >> 6, rr = o & 63;
+                const uint32_t j = g - pre_o, n0 = (uint32_t)__popcll(q0);
+                const uint32_t w = j < n0 ? select64(q0, j) : 64u + select64(q1, j - n0);
+                const uint64_t *row = LW.R[owner];
+                const uint32_t o = 2 * w, q = o >> 6, rr = o & 63;
                 const uint64_t hi64 = row[q] << rr;
                 key4[i] = (rr ? (hi64 | (row[q + 1] >> (64 - rr))) : hi64) >> sh;
-                tag4[i] = t;
+                tag4[i] = (owner << 8) | w;
                 act |= 1u << i;
             }
         }
@@ -795,7 +830,6 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
                                                                                a.tpos_local));
             }
         }
-        wave_sync();  // the list is rewritten by the next pass
     }
 }
 
@@ -871,7 +905,7 @@ void k_align_lane(AlignArgs a) {
 #endif
 #pragma unroll 1
         for (int attempt = again_batch ? 1 : 0; attempt < 2; attempt++) {
-            if (S.kind == LANE_WALK) lane_walk<WIN_Q, MG>(a, LW.R[lane], S);
+            if (S.kind == LANE_WALK && S.atp != ~0ull) lane_walk<WIN_Q, MG>(a, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif

@@ -582,3 +582,31 @@ def test_quality_thresholds_no_read_can_fail(mrq, mkq, monkeypatch):
     ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
     assert out[0] == out[1]
     assert out[0] == [o.stats.tolist(), o.unique.tolist(), o.ambiguous.tolist(), ofk.tolist()]
+
+
+@pytest.mark.parametrize("noanchor", ["1", "0"])
+@pytest.mark.parametrize("ps", [dict(), dict(m=0, p=0), dict(mg=2), dict(mrq=58, mkq=60, mg=5), dict(p=-1)])
+def test_unanchored_reads_vs_oracle(ps, noanchor, monkeypatch):
+    """Reads with no seed in the index -- reverse-complemented reads (forward-only
+    lookups) and reads of an unindexed organism, 1.5 % substitutions -- probed
+    window by window in the lane kernel (PA_LANE_NOANCHOR=1, the default with a
+    Bloom filter) or left to the wave kernel (0): both equal the oracle."""
+    monkeypatch.setenv("PA_LANE_NOANCHOR", noanchor)
+    gens = synth.family_genomes(12, 30000, seed=61, family_size=4, sub_rate=0.01, conserved_len=800,
+                                n_rate=2e-4, n_run=8)
+    index = N.Index(gens, 31)
+    oix = O.OracleIndex(gens, 31)
+    reads = N.Reads.synthesize(index, 20000, 150, first_read=0, seed=62, sub_rate=0.015, rc_rate=0.3,
+                               foreign_rate=0.3)
+    s, q, off = reads.download()
+    full = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+    res = N.Result(index)
+    N.align(index, reads, N.Params.make(full["m"], full["p"], full["mrq"], full["mkq"], full["mg"]), 99, res)
+    stats, uq, am, fk = res.fetch()
+    o = oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"], mkq=full["mkq"],
+                  mg=full["mg"], read_base=99, detail=False)
+    assert stats.tolist() == o.stats.tolist(), ps
+    assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
+    ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+    assert fk.tolist() == ofk.tolist(), ps
+    assert o.stats[2] > 5000  # many unmapped reads: the case under test

@@ -29,8 +29,10 @@ def _stub_namespace():
     m = re.search(r"```python\n(# src/pa_gpu\.py.*?)```", text, re.S)
     assert m, "INTEGRATION.md section 2 stub not found"
     code = m.group(1).replace('"/path/to/libpa.so"', repr(LIB))
+    d = re.search(r"```python\n(_L\.pa_index_dumpref\.argtypes.*?)```", text, re.S)
+    assert d, "INTEGRATION.md dumpref snippet not found"
     ns = {}
-    exec(compile(code, "INTEGRATION.md:pa_gpu.py", "exec"), ns)
+    exec(compile(code + "\n" + d.group(1), "INTEGRATION.md:pa_gpu.py", "exec"), ns)
     return ns
 
 
@@ -87,3 +89,25 @@ def test_stub_reproduces_config1_cli():
             order[names[g]] = min(order.get(names[g], 2 ** 63), int(first[g]))
         out = {"Statistics": stats, "Summary": {n: summary[n] for n in sorted(order, key=order.get)}}
         assert json.dumps(out, indent=4) + "\n" == case["stdout"], flags
+
+
+@pytest.mark.gpu
+def test_stub_dumpref_matches_reference(tmp_path):
+    """The dumpref snippet: its "Kmers" text plus the Summary built from its
+    arrays is the reference CLI's dumpref stdout for config 1 (SHA-256)."""
+    import hashlib
+    ns = _stub_namespace()
+    names, genomes = _fasta(os.path.join(GOLD, "config1.fa"))
+    index = ns["build_index"](genomes, 21)
+    recs = [{"description": n, "genome": g} for n, g in zip(names, genomes)]
+    out = tmp_path / "dump.json"
+    with open(out, "wb") as f:
+        uniq, multi, order, last = ns["dump_kmers"](index, recs, f.fileno())
+    descs = list(dict.fromkeys(names))
+    present = sorted((d for d in range(len(descs)) if int(order[d]) != 2 ** 64 - 1), key=lambda d: int(order[d]))
+    summary = {descs[d]: {"total_bases": len(genomes[int(last[d])]), "unique_kmers": int(uniq[d]),
+                          "multi_mapping_kmers": int(multi[d])} for d in present}
+    tail = json.dumps({"Kmers": 0, "Summary": summary}, indent=4)
+    text = out.read_text() + tail[tail.index('"Kmers": 0') + len('"Kmers": 0'):] + "\n"
+    gold = json.load(open(os.path.join(GOLD, "dumpref_cases.json")))["config1"]["config1"]
+    assert hashlib.sha256(text.encode()).hexdigest() == gold["sha256"]
