@@ -516,7 +516,9 @@ void prefetch_run(pa_fastq_prefetch *pf) {
     if (e == hipSuccess) e = hipMemGetInfo(&free_b, &total_b);
     // a file that would take more than a quarter of the free device memory
     // (text + parse buffers ~ 21 B per window byte) is left to the windowed stream
-    if (e == hipSuccess && pf->size + 24 * pf->window > free_b / 4) {
+    uint64_t cap = free_b / 4;  // PA_PREFETCH_MAX_BYTES: a lower limit (tests: the windowed fallback)
+    if (const char *m = std::getenv("PA_PREFETCH_MAX_BYTES")) cap = std::min<uint64_t>(cap, std::strtoull(m, nullptr, 10));
+    if (e == hipSuccess && pf->size + 24 * pf->window > cap) {
         fail(PA_EUNSUPPORTED, "FASTQ file too large to prefetch whole");
         return;
     }

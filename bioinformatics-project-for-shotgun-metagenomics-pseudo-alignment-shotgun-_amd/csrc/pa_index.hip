@@ -1096,7 +1096,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 const char *bm = std::getenv("PA_BLOOM_MB");
                 const uint64_t cap_b = idx->force_large ? 0ull : (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 64ull) << 20;
                 uint32_t lg = 6;
-                while (lg < 28 && (1ull << lg) * 64 < idx->n_kmers * 16) lg++;
+                while (lg < 33 && (1ull << lg) * 64 < idx->n_kmers * 16) lg++;
                 while (lg > 6 && (1ull << lg) * 8 > cap_b) lg--;
                 if (cap_b > 0 && idx->n_kmers > 0 && (1ull << lg) * 64 >= idx->n_kmers * 8 && (1ull << lg) * 8 <= cap_b) {
                     B_HIP(hipMalloc(&idx->bloom, (1ull << lg) * 8));

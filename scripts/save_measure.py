@@ -26,10 +26,15 @@ def main(tag: str, name: str) -> None:
         f.write(line)
     summ = os.path.join(REPO, "profiles", "rocpd_summary.py")
     for kind, label in (("trace", "kernel_stats"), ("sq", "sq")):
+        done = os.path.join(src, f"{label}.txt" if kind == "trace" else "sq.txt")
         dbs = glob.glob(os.path.join(src, kind, "**", "*.db"), recursive=True)
-        if not dbs:
+        if os.path.exists(done):  # summarised on the GPU box (measure.sh)
+            with open(done) as f:
+                out = f.read()
+        elif dbs:
+            out = subprocess.run([sys.executable, summ, dbs[0]], capture_output=True, text=True, check=True).stdout
+        else:
             continue
-        out = subprocess.run([sys.executable, summ, dbs[0]], capture_output=True, text=True, check=True).stdout
         with open(os.path.join(dst, f"{name}_{label}.txt"), "w") as f:
             f.write(f"# bench.py --config {args}; measured at commit {head} (+ working tree)\n" + out)
     print("saved", name)

@@ -153,6 +153,22 @@ def test_prefetched_equals_exact(ref, tmp_path, monkeypatch, window, chunk, kw):
     assert json.dumps(a.get_summary(), indent=4) == json.dumps(b.get_summary(), indent=4)
 
 
+def test_prefetch_too_large_takes_the_windowed_stream(ref, tmp_path, monkeypatch):
+    """A file above the prefetch limit (a quarter of the free device memory;
+    lowered here) is aligned by the windowed stream instead, same results."""
+    gens, r = ref
+    monkeypatch.setenv("PA_PREFETCH_MAX_BYTES", "1000")
+    monkeypatch.setenv("PA_STREAM_WINDOW", "65536")
+    p = tmp_path / "reads.fq"
+    p.write_text(reads_text(gens, 2000, seed=19))
+    a = PseudoAlignment(r)
+    a.align_reads_from_file(str(p), prefetch=N.FastqPrefetch(str(p)), m=2, p=0)
+    assert getattr(a, "_streamed_records", None) == 2000
+    b = PseudoAlignment(r)
+    b.align_reads_from_container(FASTAQFile(str(p)).container, m=2, p=0)
+    assert a.get_summary() == b.get_summary()
+
+
 def test_prefetched_outside_subset_and_gz(ref, tmp_path, monkeypatch):
     gens, r = ref
     monkeypatch.setenv("PA_PREFETCH_CHUNK", "8192")
