@@ -98,6 +98,9 @@ struct AlignArgs {
     // lane kernel: reads it leaves to the wave kernel
     uint32_t *queue_hard;
     unsigned long long *queue_hard_count;
+    uint32_t *queue_na;                    // lane kernel: reads with no seed in the index (null: to the wave kernel)
+    unsigned long long *queue_na_count;
+    uint64_t na_min;                       // fewer than this: k_align_lane_na hands them to the wave kernel
     // wave kernel input: a list of read indices (null: reads 0 .. n-1)
     const uint32_t *rlist;
     const unsigned long long *rlist_count;
@@ -589,6 +592,18 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), shm, st, a);
     PA_HIP(hipGetLastError());
+    if (a.queue_na) {  // the reads without a seed in the index (count on the device)
+        auto na = win_q ? (mg ? k_align_lane_na<true, true, true> : k_align_lane_na<true, true, false>)
+                : need_q ? (mg ? k_align_lane_na<true, false, true> : k_align_lane_na<true, false, false>)
+                         : (mg ? k_align_lane_na<false, false, true> : k_align_lane_na<false, false, false>);
+        int na_cu = 0;
+        PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&na_cu, na, kBlock, 0));
+        const unsigned ngrid = (unsigned)std::max<uint64_t>(
+            1, std::min<uint64_t>(want, (uint64_t)std::max(1, na_cu) * (uint64_t)cus));
+        hipLaunchKernelGGL(na, dim3(ngrid), dim3(kBlock), 0, st, a);
+        PA_HIP(hipGetLastError());
+
+    }
     return PA_OK;
 }
 
@@ -709,10 +724,13 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
     if (idx->queue_cap >= n) return PA_OK;
     hipFree(idx->queue);
     hipFree(idx->queue_hard);
-    idx->queue = idx->queue_hard = nullptr;
+    hipFree(idx->queue_na);
+    idx->queue = idx->queue_hard = idx->queue_na = nullptr;
     idx->queue_cap = 0;
     PA_HIP(hipMalloc(&idx->queue, n * 4));
     PA_HIP(hipMalloc(&idx->queue_hard, n * 4));
+    PA_HIP(hipMalloc(&idx->queue_na, n * 4));
+    if (!idx->na_count) PA_HIP(hipMalloc(&idx->na_count, 8));
     idx->queue_cap = n;
     return PA_OK;
 }
@@ -853,6 +871,14 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.queue_hard = idx->queue_hard;
             a.queue_hard_count = (unsigned long long *)idx->counters + 3;
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));
+            // reads without a seed in the index: k_align_lane_na (with a Bloom filter; PA_LANE_NOANCHOR=0/1)
+            bool na = a.bloom != nullptr;
+            if (const char *e = std::getenv("PA_LANE_NOANCHOR")) na = e[0] == '1';
+            a.queue_na = na ? idx->queue_na : nullptr;
+            a.queue_na_count = idx->na_count;
+            a.na_min = 32768;  // (PA_NA_MIN: tests)
+            if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
+            if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 8, st));
             PA_TRY(launch_lane(a, st));
             a.rlist = idx->queue_hard;
             a.rlist_count = a.queue_hard_count;

@@ -1171,6 +1171,10 @@ void index_release(pa_index *idx) {
     hipFree(idx->ws.ptr);
     hipFree(idx->queue);
     hipFree(idx->queue_hard);
+    hipFree(idx->queue_na);
+    hipFree(idx->na_count);
+    idx->queue_na = nullptr;
+    idx->na_count = nullptr;
     hipFree(idx->counters);
     for (auto e : idx->ev_start) hipEventDestroy(e);
     for (auto e : idx->ev_stop) hipEventDestroy(e);

@@ -104,6 +104,8 @@ struct pa_index {
     pa::Workspace ws;
     uint32_t *queue = nullptr;         // read indices deferred to the exact kernel
     uint32_t *queue_hard = nullptr;    // read indices the lane kernel leaves to the wave kernel
+    uint32_t *queue_na = nullptr;      // read indices the lane kernel found no seed for (k_align_lane_na)
+    unsigned long long *na_count = nullptr;
     uint64_t queue_cap = 0;
     uint64_t *counters = nullptr;      // [0] queue length, [1] deferred total, [2] error flags, [3] hard reads,
                                        // [4..31] PA_STATS counters

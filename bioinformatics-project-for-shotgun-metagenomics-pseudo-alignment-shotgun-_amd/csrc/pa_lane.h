@@ -38,10 +38,12 @@
 // included k-mer contains g; src/kmer.py:464-480).  Any other read -- no
 // anchor, a local repeat, a non-ACGT base, a second re-anchoring, a read longer
 // than the lane limits -- is queued whole for the wave kernel, which handles
-// every case exactly.  A read none of whose seeds is in the index (reverse-
-// complemented, unindexed organism) lists all its windows for the cooperative
-// probes (Bloom filter first): nothing found -> UNMAPPED, only multi-genome
-// k-mers -> AMBIGUOUS, a specific one -> walked again from it.
+// every case exactly.  A read none of whose seeds is in the index (a reverse-
+// complemented read, a read of an unindexed organism) is queued for
+// k_align_lane_na, which checks all its windows against the Bloom filter
+// lane by lane (such reads fill whole waves there, so the per-lane loops stay
+// balanced) -- nothing found: UNMAPPED; only multi-genome k-mers: AMBIGUOUS; a
+// specific one: the wave kernel.
 
 constexpr int kLaneMaxW = 128;    // windows per read on the lane path
 constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
@@ -75,12 +77,16 @@ struct __align__(16) LaneWave {
     unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 40) | position
     uint32_t flags[64];              // bit 0: specific k-mer found off the walk; bits 2..: unspecific ones found
     uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
+    uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
     uint32_t again_r[128];           // reads to walk again from a specific k-mer found off their walk,
     unsigned long long again_a[128]; //   and that anchor: (window << 40) | position
     uint32_t n_hr[64], n_qf[64];     // per-lane window counters of the settled reads (kept out of VGPRs)
 };
 
-enum : int { LANE_UNIQUE = 0, LANE_AMB = 1, LANE_UNMAPPED = 2, LANE_DROP = 3, LANE_HARD = 4, LANE_WALK = 5, LANE_AGAIN = 6 };
+enum : int {
+    LANE_UNIQUE = 0, LANE_AMB = 1, LANE_UNMAPPED = 2, LANE_DROP = 3, LANE_HARD = 4, LANE_WALK = 5, LANE_AGAIN = 6,
+    LANE_NOANCHOR = 7  // no seed in the index: k_align_lane_na takes the read
+};
 
 // Word q of a register array by a runtime index (selects; no scratch).
 template <int N>
@@ -299,7 +305,7 @@ __device__ __forceinline__ uint32_t lane_mismatches(const AlignArgs &a, const ui
 
 // Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor (a
 // read walked again: the given anchor, cd != ~0).
-template <bool NEED_Q, bool WIN_Q>
+template <bool NEED_Q, bool WIN_Q, bool SEEDS = true>
 __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsigned long long cd, uint64_t *row,
                                           LaneRead &S) {
     S.kind = LANE_HARD;
@@ -391,6 +397,10 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         return;
     }
 #endif
+    if (!SEEDS) {  // (k_align_lane_na: the read packed, its window masks made; no seeds)
+        S.kind = LANE_WALK;
+        return;
+    }
     if (cd != ~0ull) {  // walked again: from the specific k-mer found off the first walk
         S.atp = cd & ((1ull << 40) - 1);
         S.aw = (uint32_t)(cd >> 40);
@@ -446,22 +456,9 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #pragma unroll
         for (int i = 0; i < NSEED; i++)
             if (at < 0 && stp[i] != ~0ull && (pass == 1 || scls[i] < a.G)) at = i;
-    if (at < 0) {
-        // no seed k-mer is in the index (a read of an unindexed organism, a
-        // reverse-complemented read, or many errors): every window is probed by
-        // the wave together, the Bloom filter first (lane_probe_wave).  Nothing
-        // found -> UNMAPPED; only multi-genome k-mers -> AMBIGUOUS with an empty
-        // list (no specific k-mer, src/kmer.py:458-461); a specific one -> the
-        // read is walked again from it, like any re-anchored read
-        if (!a.lane_noanchor) return (void)LANE_HARD_WHY(3);
-        S.atp = ~0ull;  // (no anchor: lane_walk is skipped)
-        S.acls = NONE;
-        S.aw = 0;
-        S.g = 0;
-        S.P0 = (W >= 64 ? ~0ull : ((1ull << W) - 1)) & ~S.F0;
-        S.P1 = (W > 64 ? (W >= 128 ? ~0ull : ((1ull << (W - 64)) - 1)) : 0ull) & ~S.F1;
-        S.kind = LANE_WALK;
-        return;
+    if (at < 0) {  // no anchor: no seed k-mer is in the index
+        if (a.queue_na) S.kind = LANE_NOANCHOR;
+        return (void)LANE_HARD_WHY(3);
     }
     S.atp = stp[0];
     S.acls = scls[0];
@@ -727,21 +724,6 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     }
 }
 
-// Position of the j-th (0-based) set bit of x (j < popcount(x)).
-__device__ __forceinline__ uint32_t select64(uint64_t x, uint32_t j) {
-    uint32_t pos = 0;
-#pragma unroll
-    for (uint32_t w = 32; w > 0; w >>= 1) {
-        const uint32_t c = (uint32_t)__popcll(x & ((1ull << w) - 1));
-        if (j >= c) {
-            j -= c;
-            pos += w;
-            x >>= w;
-        }
-    }
-    return pos;
-}
-
 // Phase 3 (whole wave): probe windows (Q0, Q1) of the walking lanes; `reset`
 // clears the lanes' outcomes first (LW.flags / hr / cand accumulate otherwise).
 __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW, const LaneRead &S, uint64_t Q0,
@@ -762,39 +744,37 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
 #ifdef PA_STATS
     if (lane == 0 && total) atomicAdd(&a.dbg[14], (unsigned long long)total);
 #endif
-    wave_sync();  // the lanes' rows (written by their owners) are read by any lane below
     for (uint32_t base = 0; base < total; base += kPassEntries) {
-        // entry base + NPR * lane + i of the wave's concatenated window lists:
-        // its owner lane (the first whose inclusive count exceeds it, by a
-        // binary search over the lanes' counts) and the owner's j-th window
-        // (the j-th set bit of its mask) -- every lane finds its own entries,
-        // no lane writes a list serially
+        // this pass's entries of the lane: global indices [max(pre, base), min(pre + c, base + 256))
+        const uint32_t lo = max(pre, base), hi = min(pre + c, base + (uint32_t)kPassEntries);
+        for (uint32_t e = lo; e < hi; e++) {
+            uint32_t w;
+            if (Q0) {
+                w = __builtin_ctzll(Q0);
+                Q0 &= Q0 - 1;
+            } else {
+                w = 64 + __builtin_ctzll(Q1);
+                Q1 &= Q1 - 1;
+            }
+            LW.list[e - base] = (uint16_t)((lane << 8) | w);
+        }
+        wave_sync();
         const uint32_t cnt = min(total - base, (uint32_t)kPassEntries);
         constexpr int NPR = PA_LANE_PROBES;
         uint64_t key4[NPR];
         uint32_t tag4[NPR], act = 0;
 #pragma unroll
         for (int i = 0; i < NPR; i++) {
-            const uint32_t e = NPR * lane + i, g = base + e;
-            uint32_t lo = 0;
-#pragma unroll
-            for (uint32_t step = 32; step > 0; step >>= 1) {
-                const uint32_t v = (uint32_t)__shfl((int)incl, (int)(lo + step - 1));
-                lo += v <= g ? step : 0u;
-            }
-            const uint32_t owner = lo < 63u ? lo : 63u;
-            const uint32_t pre_o = (uint32_t)__shfl((int)pre, (int)owner);
-            const uint64_t q0 = shfl64(Q0, (int)owner), q1 = shfl64(Q1, (int)owner);
+            const uint32_t e = NPR * lane + i;
             key4[i] = 0;
             tag4[i] = 0;
             if (e < cnt) {
-                const uint32_t j = g - pre_o, n0 = (uint32_t)__popcll(q0);
-                const uint32_t w = j < n0 ? select64(q0, j) : 64u + select64(q1, j - n0);
-                const uint64_t *row = LW.R[owner];
-                const uint32_t o = 2 * w, q = o >> 6, rr = o & 63;
+                const uint32_t t = LW.list[e];
+                const uint64_t *row = LW.R[t >> 8];
+                const uint32_t o = 2 * (t & 255), q = o >> 6, rr = o & 63;
                 const uint64_t hi64 = row[q] << rr;
                 key4[i] = (rr ? (hi64 | (row[q + 1] >> (64 - rr))) : hi64) >> sh;
-                tag4[i] = (owner << 8) | w;
+                tag4[i] = t;
                 act |= 1u << i;
             }
         }
@@ -830,6 +810,7 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
                                                                                a.tpos_local));
             }
         }
+        wave_sync();  // the list is rewritten by the next pass
     }
 }
 
@@ -905,7 +886,7 @@ void k_align_lane(AlignArgs a) {
 #endif
 #pragma unroll 1
         for (int attempt = again_batch ? 1 : 0; attempt < 2; attempt++) {
-            if (S.kind == LANE_WALK && S.atp != ~0ull) lane_walk<WIN_Q, MG>(a, LW.R[lane], S);
+            if (S.kind == LANE_WALK) lane_walk<WIN_Q, MG>(a, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif
@@ -994,6 +975,14 @@ void k_align_lane(AlignArgs a) {
             qbase = shfl64(qbase, __builtin_ctzll(hb));
             if (hard) a.queue_hard[qbase + lanes_below(hb)] = (uint32_t)r;
         }
+        const bool na = S.kind == LANE_NOANCHOR;
+        const uint64_t nab = __ballot(na);
+        if (nab) {  // one queue allocation per wave
+            uint64_t qbase = 0;
+            if (lane == __builtin_ctzll(nab)) qbase = atomicAdd(a.queue_na_count, (unsigned long long)__popcll(nab));
+            qbase = shfl64(qbase, __builtin_ctzll(nab));
+            if (na) a.queue_na[qbase + lanes_below(nab)] = (uint32_t)r;
+        }
         const bool again = S.kind == LANE_AGAIN;
         const uint64_t ab = __ballot(again);
         if (ab) {  // (at most 63 + 64 entries: a batch is taken once 64 wait)
@@ -1042,4 +1031,100 @@ void k_align_lane(AlignArgs a) {
 
 constexpr size_t lane_lds_bytes(uint32_t G) {
     return (G <= kLaneLdsGenomeCap ? ((size_t)G * 12 + 15) / 16 * 16 : 0) + (size_t)kWaves * sizeof(LaneWave);
+}
+
+// k_align_lane_na: the reads k_align_lane found no seed for, one per lane.
+// Every window of the read (but those failing --min-kmer-quality) is looked up
+// -- the Bloom filter first, eight windows in flight, then the table for the
+// few the filter lets through (src/kmer.py:410-429).  No k-mer found: UNMAPPED;
+// found ones all multi-genome (or above --max-genomes, counted as highly
+// redundant): AMBIGUOUS with an empty list (no specific k-mer,
+// src/kmer.py:458-461); a specific one: the read is queued for the wave kernel.
+template <bool NEED_Q, bool WIN_Q, bool MG>
+__global__ __launch_bounds__(kBlock) void k_align_lane_na(AlignArgs a) {
+    __shared__ uint64_t rows[kBlock][kLaneWords + 1];
+    const int lane = lane_id();
+    const int sh = 64 - 2 * a.k;
+    const uint64_t n = *a.queue_na_count;
+    // a few such reads cost a ~0.2 ms chain of dependent loads here (one lane
+    // walks ~120 windows) but next to nothing among the wave kernel's reads:
+    // below a.na_min (32 k) they are handed to it
+    const bool forward = n < a.na_min;
+    uint32_t n_amb = 0, n_unm = 0;   // wave totals (scalar)
+    uint32_t hr_sum = 0, qf_sum = 0;  // per lane
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); c0 < n;
+         c0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i = c0 + lane;
+        LaneRead S;
+        S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
+        uint32_t r = 0;
+        if (i < n) {
+            r = a.queue_na[i];
+            if (forward) S.kind = LANE_HARD;
+            else lane_prep<NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
+        }
+        if (S.kind == LANE_WALK) {
+            const uint64_t *row = rows[threadIdx.x];
+            const uint32_t W = S.W;
+            bool spec = false;
+            uint32_t noff = 0, hr = 0;
+#pragma unroll 1
+            for (uint32_t w0 = 0; w0 < W && !spec; w0 += 8) {
+                uint64_t key[8];
+                uint32_t act = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t w = w0 + j;
+                    const bool filt = WIN_Q && (((w < 64 ? S.F0 >> w : S.F1 >> (w - 64)) & 1ull) != 0);
+                    key[j] = w < W ? row_bits(row, 2 * w) >> sh : 0ull;
+                    act |= (w < W && !filt) ? 1u << j : 0u;
+                }
+                if (a.bloom) {  // keys surely absent are not looked up
+                    uint64_t bw[8], bm[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        uint64_t wi;
+                        bloom_word(key[j], a.k, a.bloom_lg, wi, bm[j]);
+                        bw[j] = bit(act, j) ? a.bloom[wi] : ~0ull;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; j++)
+                        if ((bw[j] & bm[j]) != bm[j]) act &= ~(1u << j);
+                }
+                if (!act) continue;
+                uint32_t f, cl[8], tp[8];
+                lane_probe<8>(a, key, act, f, cl, tp);
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    if (!bit(f, j)) continue;
+                    if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
+                    else if (cl[j] >= a.G) noff++;
+                    else spec = true;
+                }
+            }
+            S.kind = spec ? LANE_HARD : (noff ? LANE_AMB : LANE_UNMAPPED);
+            if (!spec) {
+                hr_sum += hr;
+                qf_sum += S.qf;
+            }
+        }
+        const bool hard = S.kind == LANE_HARD;
+        const uint64_t hb = __ballot(hard);
+        if (hb) {
+            uint64_t qbase = 0;
+            if (lane == __builtin_ctzll(hb)) qbase = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
+            qbase = shfl64(qbase, __builtin_ctzll(hb));
+            if (hard) a.queue_hard[qbase + lanes_below(hb)] = r;
+        }
+        n_amb += (uint32_t)__popcll(__ballot(S.kind == LANE_AMB));
+        n_unm += (uint32_t)__popcll(__ballot(S.kind == LANE_UNMAPPED));
+    }
+    const uint32_t hr_w = wave_sum(hr_sum);
+    const uint32_t qf_w = WIN_Q ? wave_sum(qf_sum) : 0u;
+    if (lane == 0) {
+        if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
+        if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
+        if (MG && hr_w) atomicAdd(&a.stats[5], (unsigned long long)hr_w);
+        if (WIN_Q && qf_w) atomicAdd(&a.stats[4], (unsigned long long)qf_w);
+    }
 }
