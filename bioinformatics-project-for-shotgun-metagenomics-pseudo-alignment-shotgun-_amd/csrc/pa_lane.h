@@ -1040,8 +1040,42 @@ constexpr size_t lane_lds_bytes(uint32_t G) {
 // found ones all multi-genome (or above --max-genomes, counted as highly
 // redundant): AMBIGUOUS with an empty list (no specific k-mer,
 // src/kmer.py:458-461); a specific one: the read is queued for the wave kernel.
+// bloom_word of windows w0 .. w0 + 7 of a packed read (k <= 31): the
+// minimizer of each window is the smallest hashed 15-mer among its k - 14, and
+// neighbouring windows share most of them, so the group's 15-mer hashes are
+// computed once (8 + k - 15 instead of 8 (k - 14)).
+__device__ __forceinline__ void bloom_words8(const uint64_t *row, uint32_t w0, int k, uint32_t lg,
+                                             const uint64_t (&key)[8], uint64_t (&wi)[8], uint64_t (&bm)[8]) {
+    const int mm = k < 15 ? k : 15;
+    const int S = k - mm + 1;  // 15-mers per window (<= 17)
+    uint32_t h[24];
+#pragma unroll
+    for (int p = 0; p < 24; p++) {
+        uint32_t y = 0xFFFFFFFFu;
+        if (p < 8 + S - 1) {
+            const uint32_t x = (uint32_t)(row_bits(row, 2 * (w0 + p)) >> (64 - 2 * mm));
+            y = x * 0x9E3779B1u;
+            y ^= y >> 15;
+        }
+        h[p] = y;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        uint32_t best = ~0u;
+#pragma unroll
+        for (int i = 0; i < 17; i++)
+            if (i < S) best = h[j + i] < best ? h[j + i] : best;
+        const uint64_t hk = bloom_mix(key[j]);
+        bm[j] = bloom_bits(hk);
+        wi[j] = ((bloom_mix(best) >> (64 - (lg - 3))) << 3) | (hk >> 61);
+    }
+}
+
+#ifndef PA_NA_WAVES
+#define PA_NA_WAVES 4  // (c2mix: 1.31 vs 1.26 G reads/s at 3, 28 B/lane of scratch)
+#endif
 template <bool NEED_Q, bool WIN_Q, bool MG>
-__global__ __launch_bounds__(kBlock) void k_align_lane_na(AlignArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WAVES))) void k_align_lane_na(AlignArgs a) {
     __shared__ uint64_t rows[kBlock][kLaneWords + 1];
     const int lane = lane_id();
     const int sh = 64 - 2 * a.k;
@@ -1080,13 +1114,10 @@ __global__ __launch_bounds__(kBlock) void k_align_lane_na(AlignArgs a) {
                     act |= (w < W && !filt) ? 1u << j : 0u;
                 }
                 if (a.bloom) {  // keys surely absent are not looked up
-                    uint64_t bw[8], bm[8];
+                    uint64_t bw[8], bm[8], wi[8];
+                    bloom_words8(row, w0, a.k, a.bloom_lg, key, wi, bm);
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        uint64_t wi;
-                        bloom_word(key[j], a.k, a.bloom_lg, wi, bm[j]);
-                        bw[j] = bit(act, j) ? a.bloom[wi] : ~0ull;
-                    }
+                    for (int j = 0; j < 8; j++) bw[j] = bit(act, j) ? a.bloom[wi[j]] : ~0ull;
 #pragma unroll
                     for (int j = 0; j < 8; j++)
                         if ((bw[j] & bm[j]) != bm[j]) act &= ~(1u << j);
