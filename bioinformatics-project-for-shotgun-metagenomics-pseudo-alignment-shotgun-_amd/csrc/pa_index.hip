@@ -1089,16 +1089,32 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 PA_TRY(build_nb(idx, st));
             }
             // the Bloom filter of the keys, for the lane kernel's probes of windows
-            // off the walk (almost all absent): worth it while it stays in the
-            // memory-side cache, so 16 bits per key up to PA_BLOOM_MB (default
-            // 64; 0: none), fewer down to 8 bits per key, else none
+            // off the walk (almost all absent).  In the memory-side cache: 16 bits
+            // per key up to PA_BLOOM_MB (default 64; 0: none), fewer down to 8
+            // bits per key.  A reference too large for that gets one in HBM, 16
+            // (down to 8) bits per key in at most 1/8 of the free memory
+            // (PA_BLOOM_HBM=0: none): the off-walk windows of a read cluster
+            // around its mismatches and share minimizer lines, so one Bloom line
+            // answers several table lines (C4 2.94 -> 3.30, C5 2.32 -> 2.70 G
+            // reads/s; C2 keeps the cache-sized one: 3.49 vs 3.41 with 134 MB).
+            // The large-reference layout (PA_LAYOUT=large) takes the HBM form.
             {
-                const char *bm = std::getenv("PA_BLOOM_MB");
+                const char *bm = std::getenv("PA_BLOOM_MB"), *bh = std::getenv("PA_BLOOM_HBM");
                 const uint64_t cap_b = idx->force_large ? 0ull : (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 64ull) << 20;
-                uint32_t lg = 6;
-                while (lg < 33 && (1ull << lg) * 64 < idx->n_kmers * 16) lg++;
+                uint32_t lg16 = 6;  // 16 bits per key
+                while (lg16 < 34 && (1ull << lg16) * 64 < idx->n_kmers * 16) lg16++;
+                uint32_t lg = lg16;
                 while (lg > 6 && (1ull << lg) * 8 > cap_b) lg--;
-                if (cap_b > 0 && idx->n_kmers > 0 && (1ull << lg) * 64 >= idx->n_kmers * 8 && (1ull << lg) * 8 <= cap_b) {
+                bool ok = cap_b > 0 && idx->n_kmers > 0 && (1ull << lg) * 64 >= idx->n_kmers * 8 && (1ull << lg) * 8 <= cap_b;
+                if (!ok && idx->n_kmers > 0 && !(bh && bh[0] == '0') && (!bm || idx->force_large)) {
+                    size_t fb = 0, tb = 0;
+                    if (hipMemGetInfo(&fb, &tb) == hipSuccess) {
+                        lg = lg16;  // 16 bits per key, fewer down to 8 if it must, in at most 1/8 of the free memory
+                        while (lg > 6 && (1ull << lg) * 8 > fb / 8) lg--;
+                        ok = (1ull << lg) * 64 >= idx->n_kmers * 8;
+                    }
+                }
+                if (ok) {
                     B_HIP(hipMalloc(&idx->bloom, (1ull << lg) * 8));
                     B_HIP(hipMemsetAsync(idx->bloom, 0, (1ull << lg) * 8, st));
                     hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
