@@ -15,10 +15,10 @@ cd $R
 timeout -k 10 900 python bench.py --config $CFG "$@" > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
 echo bench done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 $R/bench.py --config $CFG --no-cpu-baseline --no-traffic "$@" > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 $R/bench.py --config $CFG --no-cpu-baseline --no-traffic --no-e2e "$@" > $OUT/trace.log 2>&1 || { tail -5 $OUT/trace.log; exit 1; }
 # summarised here, the database dropped (gpurun_out/ must stay under 64 MiB)
 python3 $R/profiles/rocpd_summary.py $(find $OUT/trace -name "*.db" | head -1) > $OUT/kernel_stats.txt && rm -rf $OUT/trace
 echo trace done
-timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD -d $OUT/sq -o run -- python3 $R/bench.py --config $CFG --no-cpu-baseline --no-traffic --steps 2 --warmup 1 "$@" > $OUT/sq.log 2>&1 || { tail -5 $OUT/sq.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD -d $OUT/sq -o run -- python3 $R/bench.py --config $CFG --no-cpu-baseline --no-traffic --no-e2e --steps 2 --warmup 1 "$@" > $OUT/sq.log 2>&1 || { tail -5 $OUT/sq.log; exit 1; }
 python3 $R/profiles/rocpd_summary.py $(find $OUT/sq -name "*.db" | head -1) > $OUT/sq.txt && rm -rf $OUT/sq
 echo sq done
