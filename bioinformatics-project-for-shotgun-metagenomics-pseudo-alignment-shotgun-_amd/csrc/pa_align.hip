@@ -101,6 +101,8 @@ struct AlignArgs {
     uint32_t *queue_na;                    // lane kernel: reads with no seed in the index (null: to the wave kernel)
     unsigned long long *queue_na_count;
     uint64_t na_min;                       // fewer than this: k_align_lane_na hands them to the wave kernel
+    const uint4 *qmask;                    // (quality filters) per read: windows failing --min-kmer-quality
+    const uint8_t *qdrop;                  //   and 1 if the read fails --min-read-quality (k_quality_masks)
     // wave kernel input: a list of read indices (null: reads 0 .. n-1)
     const uint32_t *rlist;
     const unsigned long long *rlist_count;
@@ -133,6 +135,67 @@ __device__ __forceinline__ void count_genome(const AlignArgs &a, const WgCounter
 }
 
 #include "pa_fast.h"
+
+// The quality filters of the lane kernels, made for all reads up front (a
+// kernel of its own, instead of the lane kernels' tight registers): per read,
+// whether its raw-ASCII quality sum is below mrq * len (mean_quality <
+// min_read_quality, src/kmer.py:394-399, 587) and the windows whose sum is
+// below mkq * k (Read.kmer_quality < min_kmer_quality, src/kmer.py:404-408,
+// 420-423) as a 128-bit mask.  A block takes 256 consecutive reads: their
+// qualities (one contiguous span) are copied to LDS with coalesced 4-B loads,
+// then each thread runs a window sum along its read.  Reads longer than the
+// lane kernels take (176) get nothing (they go to the wave kernel).
+constexpr uint32_t kQmSpan = 256 * 176 + 16;  // LDS bytes: a block of reads of <= 176 bases
+__global__ __launch_bounds__(256) void k_quality_masks(const uint8_t *__restrict__ qual, const uint64_t *__restrict__ off,
+                                                       uint64_t n, int k, int64_t mrq, int64_t mkq, uint32_t flags,
+                                                       uint4 *__restrict__ qmask, uint8_t *__restrict__ qdrop) {
+    __shared__ uint32_t buf32[kQmSpan / 4];
+    const uint8_t *buf = (const uint8_t *)buf32;
+    const int64_t T64 = mkq * (int64_t)k;
+    const uint32_t T = T64 <= 0 ? 0u : (T64 > (1 << 24) ? (1u << 24) : (uint32_t)T64);
+    for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < n; r0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t rend = min(r0 + 256, n);
+        const uint64_t a0 = off[r0] & ~3ull, b1 = off[rend];
+        const bool staged = b1 - a0 <= kQmSpan - 4;  // (else: a long read among them; from global memory)
+        if (staged) {
+            const uint32_t nw = (uint32_t)((b1 - a0 + 3) >> 2);  // (the read buffers are padded)
+            const uint32_t *src = (const uint32_t *)(qual + a0);
+            for (uint32_t i = threadIdx.x; i < nw; i += 256) buf32[i] = src[i];
+        }
+        __syncthreads();
+        const uint64_t r = r0 + threadIdx.x;
+        if (r < rend) {
+            const uint64_t o = off[r];
+            const uint64_t L64 = off[r + 1] - o;
+            uint64_t F0 = 0, F1 = 0;
+            uint32_t total = 0;
+            if (L64 <= 176u) {
+                const uint32_t len = (uint32_t)L64;
+                const bool win = (flags & 2u) && len >= (uint32_t)k;
+                const uint8_t *q = staged ? buf + (o - a0) : qual + o;
+                uint32_t run = 0;
+#pragma unroll 4
+                for (uint32_t i = 0; i < len; i++) {
+                    const uint32_t c = q[i];
+                    total += c;
+                    run += c;
+                    if (i >= (uint32_t)k) run -= q[i - k];
+                    if (win && i + 1 >= (uint32_t)k && run < T) {
+                        const uint32_t w = i + 1 - (uint32_t)k;
+                        if (w < 64) F0 |= 1ull << w;
+                        else F1 |= 1ull << (w - 64);
+                    }
+                }
+                qdrop[r] = ((flags & 1u) && (int64_t)total < mrq * (int64_t)len) ? 1 : 0;
+            } else {
+                qdrop[r] = 0;
+            }
+            qmask[r] = make_uint4((uint32_t)F0, (uint32_t)(F0 >> 32), (uint32_t)F1, (uint32_t)(F1 >> 32));
+        }
+        __syncthreads();  // (the buffer is refilled next)
+    }
+}
+
 #include "pa_lane.h"
 
 // Plane of the windows whose genome set is larger than mg (--max-genomes,
@@ -720,6 +783,19 @@ pa_status ensure_workspace(pa_index *idx, size_t bytes) {
     return PA_OK;
 }
 
+pa_status ensure_qmask(pa_index *idx, uint64_t n) {
+    if (idx->qmask_cap >= n) return PA_OK;
+    hipFree(idx->qmask);
+    hipFree(idx->qdrop);
+    idx->qmask = nullptr;
+    idx->qdrop = nullptr;
+    idx->qmask_cap = 0;
+    PA_HIP(hipMalloc(&idx->qmask, n * sizeof(uint4)));
+    PA_HIP(hipMalloc(&idx->qdrop, n));
+    idx->qmask_cap = n;
+    return PA_OK;
+}
+
 pa_status reserve_queues(pa_index *idx, uint64_t n) {
     if (idx->queue_cap >= n) return PA_OK;
     hipFree(idx->queue);
@@ -871,6 +947,15 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.queue_hard = idx->queue_hard;
             a.queue_hard_count = (unsigned long long *)idx->counters + 3;
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));
+            if (a.prm.flags & (F_MRQ | F_MKQ)) {  // the quality filters of every read, up front
+                PA_TRY(ensure_qmask(idx, r->n));
+                hipLaunchKernelGGL(k_quality_masks, dim3((unsigned)std::min<uint64_t>((r->n + 255) / 256, 65536)),
+                                   dim3(256), 0, st, r->qual, r->off, r->n, (int)idx->k, (int64_t)a.prm.mrq,
+                                   (int64_t)a.prm.mkq, a.prm.flags & (F_MRQ | F_MKQ), idx->qmask, idx->qdrop);
+                PA_HIP(hipGetLastError());
+                a.qmask = idx->qmask;
+                a.qdrop = idx->qdrop;
+            }
             // reads without a seed in the index: k_align_lane_na (with a Bloom filter; PA_LANE_NOANCHOR=0/1)
             bool na = a.bloom != nullptr;
             if (const char *e = std::getenv("PA_LANE_NOANCHOR")) na = e[0] == '1';

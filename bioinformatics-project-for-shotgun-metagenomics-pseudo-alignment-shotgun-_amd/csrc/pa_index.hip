@@ -1189,6 +1189,11 @@ void index_release(pa_index *idx) {
     hipFree(idx->queue_hard);
     hipFree(idx->queue_na);
     hipFree(idx->na_count);
+    hipFree(idx->qmask);
+    hipFree(idx->qdrop);
+    idx->qmask = nullptr;
+    idx->qdrop = nullptr;
+    idx->qmask_cap = 0;
     idx->queue_na = nullptr;
     idx->na_count = nullptr;
     hipFree(idx->counters);

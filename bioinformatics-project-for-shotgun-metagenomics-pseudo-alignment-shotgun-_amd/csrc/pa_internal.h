@@ -105,6 +105,9 @@ struct pa_index {
     uint32_t *queue = nullptr;         // read indices deferred to the exact kernel
     uint32_t *queue_hard = nullptr;    // read indices the lane kernel leaves to the wave kernel
     uint32_t *queue_na = nullptr;      // read indices the lane kernel found no seed for (k_align_lane_na)
+    uint4 *qmask = nullptr;            // per read: windows failing --min-kmer-quality (k_quality_masks)
+    uint8_t *qdrop = nullptr;          // per read: fails --min-read-quality
+    uint64_t qmask_cap = 0;
     unsigned long long *na_count = nullptr;
     uint64_t queue_cap = 0;
     uint64_t *counters = nullptr;      // [0] queue length, [1] deferred total, [2] error flags, [3] hard reads,
@@ -162,6 +165,7 @@ pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uin
 pa_status reads_measure(pa_reads *r, hipStream_t st);  // q_min / len_min of a batch (at its creation)
 pa_status ensure_workspace(pa_index *idx, size_t bytes);
 pa_status reserve_queues(pa_index *idx, uint64_t n);  // align queues for batches of up to n reads
+pa_status ensure_qmask(pa_index *idx, uint64_t n);    // quality-filter masks for batches of up to n reads
 pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,
                            int threads, uint64_t window, hipStream_t st, uint64_t *n_reads);
 pa_status fastq_prefetch_start(const char *path, int device, int threads, uint64_t window, pa_fastq_prefetch **out);

@@ -201,60 +201,6 @@ __device__ __forceinline__ uint32_t in_read_mask(uint32_t p0, uint32_t shift, ui
     return (hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1)) & (lo >= 4 ? 0u : (0xFFFFFFFFu << (8 * lo)));
 }
 
-// Windows of the read whose raw-ASCII quality sum is below mkq * k
-// (Read.kmer_quality, src/kmer.py:404-408, gate :420-423) as a 128-bit mask.
-// A running sum over the staged 16-B chunks: byte p enters, byte p - k leaves.
-// The leaving bytes of chunk c are bytes r .. r + 15 of the chunk pair
-// (lc, lc + 1), lc = floor((16c - k) / 16), r = (16c - k) mod 16 = (-k) mod 16
-// -- the same for every chunk and every lane.
-__device__ __forceinline__ void lane_window_quality(const AlignArgs &a, const uint4 *qp, uint32_t shift, uint32_t len,
-                                                    uint32_t nch, LaneRead &S) {
-    const int k = a.k;
-    const int64_t T64 = (int64_t)a.prm.mkq * (int64_t)k;
-    const uint32_t T = T64 <= 0 ? 0u : (T64 > (1 << 24) ? (1u << 24) : (uint32_t)T64);
-    const uint32_t r = (uint32_t)(-k) & 15u, rq = r >> 2, rb = r & 3u;
-    uint64_t F0 = 0, F1 = 0;
-    uint32_t run = 0;
-#pragma unroll 1
-    for (uint32_t c = 0; c < nch; c++) {
-        const uint4 v = qp[c];
-        const uint32_t cur[4] = {v.x, v.y, v.z, v.w};
-        const int32_t lc = ((int32_t)(16 * c) - k) >> 4;  // (floor)
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        const uint4 l0 = lc >= 0 ? qp[lc] : z, l1 = lc + 1 >= 0 ? qp[lc + 1] : z;
-        const uint32_t e[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-        uint32_t lag[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t lo = rq == 0 ? e[u] : rq == 1 ? e[u + 1] : rq == 2 ? e[u + 2] : e[u + 3];
-            const uint32_t hi = rq == 0 ? e[u + 1] : rq == 1 ? e[u + 2] : rq == 2 ? e[u + 3] : e[u + 4];
-            lag[u] = __builtin_amdgcn_alignbyte(hi, lo, rb);
-        }
-        uint32_t m16 = 0;
-#pragma unroll
-        for (int t = 0; t < 16; t++) {
-            const int32_t i = (int32_t)(16 * c + t) - (int32_t)shift;  // read position of the entering byte
-            const uint32_t in = (i >= 0 && i < (int32_t)len) ? ((cur[t >> 2] >> (8 * (t & 3))) & 255u) : 0u;
-            const uint32_t out = (i - k >= 0 && i - k < (int32_t)len) ? ((lag[t >> 2] >> (8 * (t & 3))) & 255u) : 0u;
-            run += in - out;
-            m16 |= ((i >= k - 1 && i < (int32_t)len && run < T) ? 1u : 0u) << t;
-        }
-        // bit t <-> window base + t
-        const int32_t base = (int32_t)(16 * c) - (int32_t)shift - k + 1;
-        const uint64_t m = m16;
-        if (base < 0) {
-            F0 |= base > -16 ? m >> (-base) : 0ull;
-        } else if (base < 64) {
-            F0 |= m << base;
-            F1 |= base > 48 ? m >> (64 - base) : 0ull;
-        } else if (base < 128) {
-            F1 |= m << (base - 64);
-        }
-    }
-    S.F0 = F0;
-    S.F1 = F1;
-    S.qf = (uint32_t)(__popcll(F0) + __popcll(F1));
-}
 
 // The walk blocks (k_tile_walk) from position A on: the 2-bit words of the
 // read's span -- gw[i] = the genome's bases from A' = A & ~31 on, word i -- and,
@@ -319,41 +265,21 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     const uint32_t len = (uint32_t)(a.off[r + 1] - o);
     const uint64_t o0 = o & ~15ull;
     const uint32_t shift = (uint32_t)(o & 15);
-    const uint32_t nch = (shift + len + 15) >> 4;
     S.len = len;
     if (len > (uint32_t)kLaneMaxLen) return (void)LANE_HARD_WHY(0);
-    // ---- qualities: read mean (src/kmer.py:399, 587) and the k-mer filter bound
+    // ---- qualities: the read's mean test (src/kmer.py:399, 587) and the windows
+    // failing --min-kmer-quality (src/kmer.py:404-408, 420-423), made for every
+    // read up front by k_quality_masks
     if (NEED_Q) {
-        const uint4 *qp = (const uint4 *)(a.qual + o0);
-        uint32_t sum = 0, qmin = 255;
-        uint4 qc[2 * kLaneWords];  // every chunk load issued before any is used (one round trip)
-#pragma unroll
-        for (uint32_t c = 0; c < 2 * kLaneWords; c++) qc[c] = c < nch ? qp[c] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (uint32_t c = 0; c < 2 * kLaneWords; c += 2) {
-            if (c >= nch) break;
-            const uint4 v0 = qc[c], v1 = qc[c + 1];
-            const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const uint32_t inr = in_read_mask(16 * c + 4 * e, shift, len);
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const uint32_t q = (d[e] >> (8 * b)) & 255u;
-                    const bool in = (inr >> (8 * b)) & 1u;
-                    sum += in ? q : 0u;
-                    qmin = in ? min(qmin, q) : qmin;
-                }
-            }
-        }
-        if ((flags & F_MRQ) && (int64_t)sum < (int64_t)a.prm.mrq * (int64_t)len) {
+        if (a.qdrop[r]) {
             S.kind = LANE_DROP;  // dropped, not unmapped (src/kmer.py:587-589)
             return;
         }
-        // a window's mean is >= the read's minimum: if that passes, no window can fail
-        if ((flags & F_MKQ) && len >= (uint32_t)k && (int64_t)qmin < (int64_t)a.prm.mkq) {
-            if (!WIN_Q) return (void)LANE_HARD_WHY(1);
-            lane_window_quality(a, qp, shift, len, nch, S);
+        if (WIN_Q) {
+            const uint4 m = a.qmask[r];
+            S.F0 = (uint64_t)m.x | ((uint64_t)m.y << 32);
+            S.F1 = (uint64_t)m.z | ((uint64_t)m.w << 32);
+            S.qf = (uint32_t)(__popcll(S.F0) + __popcll(S.F1));
         }
     }
     if (len < (uint32_t)k) {
