@@ -353,15 +353,19 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     // bounds this kernel)
     uint32_t sfound = 0, scls[NSEED], stp32[NSEED];
     {
-        constexpr uint32_t all = (1u << NSEED) - 1, outer = 1u | (1u << (NSEED - 1));
+#ifndef PA_LANE_SEED_R1
+#define PA_LANE_SEED_R1 (1u | (1u << (NSEED - 1)))  // the first round's seeds
+#endif
+        constexpr uint32_t all = (1u << NSEED) - 1, outer = PA_LANE_SEED_R1;
         uint32_t act = PA_LANE_SEED_ROUNDS > 1 ? outer : all;
 #pragma unroll 1
         for (int round = 0; round < 2 && act; round++) {
             uint32_t f;
             lane_probe<NSEED>(a, skey, act, f, scls, stp32);
             sfound |= f;
-            const bool spec = (bit(f, 0) && scls[0] < a.G && stp32[0] != NONE) ||
-                              (bit(f, NSEED - 1) && scls[NSEED - 1] < a.G && stp32[NSEED - 1] != NONE);
+            bool spec = false;
+#pragma unroll
+            for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && scls[i] < a.G && stp32[i] != NONE;
             act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 14) act = 0;  // timing dissection: one seed round
@@ -966,35 +970,53 @@ constexpr size_t lane_lds_bytes(uint32_t G) {
 // found ones all multi-genome (or above --max-genomes, counted as highly
 // redundant): AMBIGUOUS with an empty list (no specific k-mer,
 // src/kmer.py:458-461); a specific one: the read is queued for the wave kernel.
-// bloom_word of windows w0 .. w0 + 7 of a packed read (k <= 31): the
-// minimizer of each window is the smallest hashed 15-mer among its k - 14, and
-// neighbouring windows share most of them, so the group's 15-mer hashes are
-// computed once (8 + k - 15 instead of 8 (k - 14)).
-__device__ __forceinline__ void bloom_words8(const uint64_t *row, uint32_t w0, int k, uint32_t lg,
-                                             const uint64_t (&key)[8], uint64_t (&wi)[8], uint64_t (&bm)[8]) {
+// The Bloom filter test of windows w0 .. w0 + NAG - 1 of a packed read (k <=
+// 31; bit j of act: look window w0 + j up), every word load issued before any
+// is tested.  The minimizer of each window is the smallest hashed 15-mer among
+// its k - 14, and neighbouring windows share most of them, so the group's
+// 15-mer hashes are computed once (NAG + k - 15 instead of NAG (k - 14)); the
+// bits of each key are kept as the 36 bits of its mix that bloom_bits reads
+// (32 + 4), not as a 64-bit mask.  Returns the windows the filter lets through.
+#ifndef PA_NA_GROUP
+#define PA_NA_GROUP 16
+#endif
+template <int NAG>
+__device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64_t *row, uint32_t w0, uint32_t act) {
+    const int k = a.k, sh = 64 - 2 * k;
     const int mm = k < 15 ? k : 15;
     const int S = k - mm + 1;  // 15-mers per window (<= 17)
-    uint32_t h[24];
+    uint32_t h[NAG + 16];
 #pragma unroll
-    for (int p = 0; p < 24; p++) {
+    for (int p = 0; p < NAG + 16; p++) {
         uint32_t y = 0xFFFFFFFFu;
-        if (p < 8 + S - 1) {
+        if (p < NAG + S - 1) {
             const uint32_t x = (uint32_t)(row_bits(row, 2 * (w0 + p)) >> (64 - 2 * mm));
             y = x * 0x9E3779B1u;
             y ^= y >> 15;
         }
         h[p] = y;
     }
+    uint64_t bw[NAG];
+    uint32_t lo[NAG];
+    uint64_t hi = 0;  // bits 32..35 of each key's mix, 4 per window
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < NAG; j++) {
         uint32_t best = ~0u;
 #pragma unroll
         for (int i = 0; i < 17; i++)
             if (i < S) best = h[j + i] < best ? h[j + i] : best;
-        const uint64_t hk = bloom_mix(key[j]);
-        bm[j] = bloom_bits(hk);
-        wi[j] = ((bloom_mix(best) >> (64 - (lg - 3))) << 3) | (hk >> 61);
+        const uint64_t hk = bloom_mix(row_bits(row, 2 * (w0 + j)) >> sh);
+        lo[j] = (uint32_t)hk;
+        hi |= ((hk >> 32) & 15ull) << (4 * j);
+        const uint64_t wi = ((bloom_mix(best) >> (64 - (a.bloom_lg - 3))) << 3) | (hk >> 61);
+        bw[j] = bit(act, j) ? a.bloom[wi] : ~0ull;
     }
+#pragma unroll
+    for (int j = 0; j < NAG; j++) {
+        const uint64_t bm = bloom_bits(((uint64_t)((hi >> (4 * j)) & 15ull) << 32) | lo[j]);
+        if ((bw[j] & bm) != bm) act &= ~(1u << j);
+    }
+    return act;
 }
 
 #ifndef PA_NA_WAVES
@@ -1028,35 +1050,34 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
             const uint32_t W = S.W;
             bool spec = false;
             uint32_t noff = 0, hr = 0;
+            constexpr int NAG = PA_NA_GROUP;
 #pragma unroll 1
-            for (uint32_t w0 = 0; w0 < W && !spec; w0 += 8) {
-                uint64_t key[8];
+            for (uint32_t w0 = 0; w0 < W && !spec; w0 += NAG) {
                 uint32_t act = 0;
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
+                for (int j = 0; j < NAG; j++) {
                     const uint32_t w = w0 + j;
                     const bool filt = WIN_Q && (((w < 64 ? S.F0 >> w : S.F1 >> (w - 64)) & 1ull) != 0);
-                    key[j] = w < W ? row_bits(row, 2 * w) >> sh : 0ull;
                     act |= (w < W && !filt) ? 1u << j : 0u;
                 }
-                if (a.bloom) {  // keys surely absent are not looked up
-                    uint64_t bw[8], bm[8], wi[8];
-                    bloom_words8(row, w0, a.k, a.bloom_lg, key, wi, bm);
+                if (a.bloom) act = bloom_group<NAG>(a, row, w0, act);  // keys surely absent are not looked up
+                // the rest, eight table probes in flight at a time
+#pragma unroll 1
+                for (uint32_t b = 0; b < (uint32_t)NAG && act >> b && !spec; b += 8) {
+                    const uint32_t act8 = (act >> b) & 255u;
+                    if (!act8) continue;
+                    uint64_t key[8];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) bw[j] = bit(act, j) ? a.bloom[wi[j]] : ~0ull;
+                    for (int j = 0; j < 8; j++) key[j] = bit(act8, j) ? row_bits(row, 2 * (w0 + b + j)) >> sh : 0ull;
+                    uint32_t f, cl[8], tp[8];
+                    lane_probe<8>(a, key, act8, f, cl, tp);
 #pragma unroll
-                    for (int j = 0; j < 8; j++)
-                        if ((bw[j] & bm[j]) != bm[j]) act &= ~(1u << j);
-                }
-                if (!act) continue;
-                uint32_t f, cl[8], tp[8];
-                lane_probe<8>(a, key, act, f, cl, tp);
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    if (!bit(f, j)) continue;
-                    if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
-                    else if (cl[j] >= a.G) noff++;
-                    else spec = true;
+                    for (int j = 0; j < 8; j++) {
+                        if (!bit(f, j)) continue;
+                        if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
+                        else if (cl[j] >= a.G) noff++;
+                        else spec = true;
+                    }
                 }
             }
             S.kind = spec ? LANE_HARD : (noff ? LANE_AMB : LANE_UNMAPPED);
