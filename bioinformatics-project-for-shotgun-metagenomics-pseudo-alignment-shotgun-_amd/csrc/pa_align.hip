@@ -141,58 +141,108 @@ __device__ __forceinline__ void count_genome(const AlignArgs &a, const WgCounter
 // whether its raw-ASCII quality sum is below mrq * len (mean_quality <
 // min_read_quality, src/kmer.py:394-399, 587) and the windows whose sum is
 // below mkq * k (Read.kmer_quality < min_kmer_quality, src/kmer.py:404-408,
-// 420-423) as a 128-bit mask.  A block takes 256 consecutive reads: their
-// qualities (one contiguous span) are copied to LDS with coalesced 4-B loads,
-// then each thread runs a window sum along its read.  Reads longer than the
-// lane kernels take (176) get nothing (they go to the wave kernel).
-constexpr uint32_t kQmSpan = 256 * 176 + 16;  // LDS bytes: a block of reads of <= 176 bases
+// 420-423) as a 128-bit mask.  One read per thread, all in registers: its
+// 16-B chunks loaded at once, realigned to the read's first byte (v_alignbit),
+// the bytes k earlier made by a second realignment (k >> 2 is a template
+// parameter, dispatched once per launch: every index below is a constant), a
+// running window sum per byte and the window test as a bit of a 176-bit mask
+// in end-position coordinates, shifted down by k - 1 at the end.  Reads longer
+// than the lane kernels take (176) get nothing (they go to the wave kernel).
+constexpr int kQmDwords = 44;  // 176 bytes
+template <int KQ>
+__device__ __forceinline__ void quality_read(const uint8_t *__restrict__ qual, uint64_t o, uint32_t len, int k,
+                                             uint32_t T, int64_t mrq, uint32_t flags, uint4 &mask, uint8_t &drop) {
+    const uint64_t o0 = o & ~15ull;
+    const uint32_t shift = (uint32_t)(o & 15);
+    const uint4 *sp = (const uint4 *)(qual + o0);
+    uint32_t dw[kQmDwords + 8];
+#pragma unroll
+    for (int c = 0; c < (kQmDwords + 8) / 4; c++) {
+        const uint4 v = 16u * c < shift + len ? sp[c] : make_uint4(0, 0, 0, 0);
+        dw[4 * c] = v.x, dw[4 * c + 1] = v.y, dw[4 * c + 2] = v.z, dw[4 * c + 3] = v.w;
+    }
+    // rd[j] = bytes 4j .. 4j + 3 of the read
+    const uint32_t s4 = shift >> 2, sb = 8 * (shift & 3);
+    uint32_t rd[kQmDwords];
+    {
+        uint32_t lo = s4 == 0 ? dw[0] : s4 == 1 ? dw[1] : s4 == 2 ? dw[2] : dw[3];
+#pragma unroll
+        for (int j = 0; j < kQmDwords; j++) {
+            const uint32_t hi = s4 == 0 ? dw[j + 1] : s4 == 1 ? dw[j + 2] : s4 == 2 ? dw[j + 3] : dw[j + 4];
+            rd[j] = __builtin_amdgcn_alignbit(hi, lo, sb);
+            lo = hi;
+        }
+    }
+    // total of the read's bytes: the whole dwords below len >> 2, then the rest
+    const uint32_t nfull = len >> 2, pmask = (len & 3) ? (1u << (8 * (len & 3))) - 1 : 0u;
+    uint32_t run_tot = 0, total = 0, part = 0;
+#pragma unroll
+    for (int j = 0; j < kQmDwords; j++) {
+        if ((uint32_t)j == nfull) total = run_tot, part = rd[j];
+        run_tot = __builtin_amdgcn_sad_u8(rd[j], 0u, run_tot);
+    }
+    if (nfull >= (uint32_t)kQmDwords) total = run_tot;
+    total = __builtin_amdgcn_sad_u8(part & pmask, 0u, total);
+    drop = ((flags & 1u) && (int64_t)total < mrq * (int64_t)len) ? 1 : 0;
+    mask = make_uint4(0, 0, 0, 0);
+    if (!(flags & 2u) || len < (uint32_t)k) return;
+    // E bit i: the window ending at byte i fails (its sum < T); bytes i - k
+    // from rk (0 before the read)
+    const uint32_t kb = 8 * ((uint32_t)k & 3);
+    uint32_t E[kQmDwords / 8 + 1] = {};
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < kQmDwords; j++) {
+        const uint32_t a1 = j - KQ >= 0 ? rd[j - KQ] : 0u, a0 = j - KQ - 1 >= 0 ? rd[j - KQ - 1] : 0u;
+        const uint32_t rk = kb ? __builtin_amdgcn_alignbit(a1, a0, 32 - kb) : a1;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int i = 4 * j + b;
+            run += ((rd[j] >> (8 * b)) & 255u) - ((rk >> (8 * b)) & 255u);
+            E[i >> 5] |= ((run - T) >> 31) << (i & 31);  // (run, T < 2^31)
+        }
+    }
+    // only windows inside the read (ends k - 1 .. len - 1), bit w = the window starting at w
+#pragma unroll
+    for (int d = 0; d <= kQmDwords / 8; d++) {
+        const int32_t hi = (int32_t)len - 32 * d;
+        E[d] &= hi >= 32 ? ~0u : hi <= 0 ? 0u : (1u << hi) - 1;
+    }
+    const uint32_t sh = (uint32_t)k - 1;  // < 32
+    uint32_t F[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) F[d] = __builtin_amdgcn_alignbit(E[d + 1], E[d], sh);
+    mask = make_uint4(F[0], F[1], F[2], F[3]);
+}
+
+template <int KQ>
+__device__ __forceinline__ void quality_reads(const uint8_t *__restrict__ qual, const uint64_t *__restrict__ off,
+                                              uint64_t n, int k, uint32_t T, int64_t mrq, uint32_t flags,
+                                              uint4 *__restrict__ qmask, uint8_t *__restrict__ qdrop) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = off[r], L64 = off[r + 1] - o;
+        uint4 m = make_uint4(0, 0, 0, 0);
+        uint8_t d = 0;
+        if (L64 <= 4u * kQmDwords) quality_read<KQ>(qual, o, (uint32_t)L64, k, T, mrq, flags, m, d);
+        qmask[r] = m;
+        qdrop[r] = d;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_quality_masks(const uint8_t *__restrict__ qual, const uint64_t *__restrict__ off,
                                                        uint64_t n, int k, int64_t mrq, int64_t mkq, uint32_t flags,
                                                        uint4 *__restrict__ qmask, uint8_t *__restrict__ qdrop) {
-    __shared__ uint32_t buf32[kQmSpan / 4];
-    const uint8_t *buf = (const uint8_t *)buf32;
     const int64_t T64 = mkq * (int64_t)k;
     const uint32_t T = T64 <= 0 ? 0u : (T64 > (1 << 24) ? (1u << 24) : (uint32_t)T64);
-    for (uint64_t r0 = (uint64_t)blockIdx.x * 256; r0 < n; r0 += (uint64_t)gridDim.x * 256) {
-        const uint64_t rend = min(r0 + 256, n);
-        const uint64_t a0 = off[r0] & ~3ull, b1 = off[rend];
-        const bool staged = b1 - a0 <= kQmSpan - 4;  // (else: a long read among them; from global memory)
-        if (staged) {
-            const uint32_t nw = (uint32_t)((b1 - a0 + 3) >> 2);  // (the read buffers are padded)
-            const uint32_t *src = (const uint32_t *)(qual + a0);
-            for (uint32_t i = threadIdx.x; i < nw; i += 256) buf32[i] = src[i];
-        }
-        __syncthreads();
-        const uint64_t r = r0 + threadIdx.x;
-        if (r < rend) {
-            const uint64_t o = off[r];
-            const uint64_t L64 = off[r + 1] - o;
-            uint64_t F0 = 0, F1 = 0;
-            uint32_t total = 0;
-            if (L64 <= 176u) {
-                const uint32_t len = (uint32_t)L64;
-                const bool win = (flags & 2u) && len >= (uint32_t)k;
-                const uint8_t *q = staged ? buf + (o - a0) : qual + o;
-                uint32_t run = 0;
-#pragma unroll 4
-                for (uint32_t i = 0; i < len; i++) {
-                    const uint32_t c = q[i];
-                    total += c;
-                    run += c;
-                    if (i >= (uint32_t)k) run -= q[i - k];
-                    if (win && i + 1 >= (uint32_t)k && run < T) {
-                        const uint32_t w = i + 1 - (uint32_t)k;
-                        if (w < 64) F0 |= 1ull << w;
-                        else F1 |= 1ull << (w - 64);
-                    }
-                }
-                qdrop[r] = ((flags & 1u) && (int64_t)total < mrq * (int64_t)len) ? 1 : 0;
-            } else {
-                qdrop[r] = 0;
-            }
-            qmask[r] = make_uint4((uint32_t)F0, (uint32_t)(F0 >> 32), (uint32_t)F1, (uint32_t)(F1 >> 32));
-        }
-        __syncthreads();  // (the buffer is refilled next)
+    switch (k >> 2) {  // (k <= 31 on the lane path; uniform)
+        case 0: quality_reads<0>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 1: quality_reads<1>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 2: quality_reads<2>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 3: quality_reads<3>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 4: quality_reads<4>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 5: quality_reads<5>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 6: quality_reads<6>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        default: quality_reads<7>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
     }
 }
 

@@ -129,9 +129,12 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
     uint64_t pos[NP];
 #pragma unroll
     for (int i = 0; i < NP; i++) {
-        Key<1> kk;
-        kk.w[0] = key[i];
-        pos[i] = bit(act, i) ? home_of<1>(kk, key_hash(kk), a.home) : 0;
+        pos[i] = 0;
+        if (bit(act, i)) {  // (skipped by the wave when no lane has key i)
+            Key<1> kk;
+            kk.w[0] = key[i];
+            pos[i] = home_of<1>(kk, key_hash(kk), a.home);
+        }
     }
     found = 0;
     while (act) {
@@ -228,12 +231,10 @@ __device__ __forceinline__ void lane_blocks(const AlignArgs &a, uint64_t A, uint
 }
 
 // Mismatching bases between the read (LDS row, len bases) and the genome
-// string from concatenated position A on; ~0u when the read does not fit.
-__device__ __forceinline__ uint32_t lane_mismatches(const AlignArgs &a, const uint64_t *row, uint32_t len, int64_t A) {
-    if (A < 0 || (uint64_t)A + len > a.tile_n) return ~0u;
-    const uint32_t gr = (uint32_t)(2 * (uint64_t)A & 63);
-    uint64_t gw[kLaneWords + 1], u3[3];
-    lane_blocks<false>(a, (uint64_t)A, len, gw, u3, u3);
+// words gw of the walk blocks from concatenated position A on (lane_blocks).
+__device__ __forceinline__ uint32_t lane_count_mismatches(const uint64_t *row, uint32_t len, uint64_t A,
+                                                          const uint64_t (&gw)[kLaneWords + 1]) {
+    const uint32_t gr = (uint32_t)(2 * A & 63);
     uint32_t n = 0;
     // the read's last word holds len - 32 * qlast bases: one mask (not one per word)
     const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;
@@ -247,6 +248,11 @@ __device__ __forceinline__ uint32_t lane_mismatches(const AlignArgs &a, const ui
         n += __popcll((d | (d >> 1)) & 0x5555555555555555ull);
     }
     return n;
+}
+
+// ~0u when the read does not fit the tile from A on.
+__device__ __forceinline__ bool lane_fits(const AlignArgs &a, uint32_t len, int64_t A) {
+    return A >= 0 && (uint64_t)A + len <= a.tile_n;
 }
 
 // Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor (a
@@ -295,10 +301,12 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     const uint32_t s2 = 2 * shift;
     uint32_t bad = 0;
     uint64_t prev = 0;
-    // every chunk load of the read issued before any is used (one round trip)
+    // every chunk load of the read issued before any is used (one round trip);
+    // chunks past the read read as "AAAA" (code 0, valid)
     uint4 ch[2 * kLaneWords];
 #pragma unroll
-    for (int c = 0; c < 2 * kLaneWords; c++) ch[c] = 16u * c < shift + len ? sp[c] : make_uint4(0, 0, 0, 0);
+    for (int c = 0; c < 2 * kLaneWords; c++)
+        ch[c] = 16u * c < shift + len ? sp[c] : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
 #pragma unroll
     for (int q = 0; q <= kLaneWords; q++) {
         uint64_t P = 0;
@@ -308,13 +316,34 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 const uint32_t cd = swar_codes(d[e]);
+#ifdef PA_PACK_MASKED
                 bad |= swar_bad_bytes(d[e], cd) & in_read_mask(32 * q + 4 * e, shift, len);
+#else
+                bad |= swar_bad_bytes(d[e], cd);  // (bytes of the neighbouring reads too: checked below)
+#endif
                 P |= (uint64_t)swar_pack_byte(cd) << (56 - 8 * e);
             }
         }
         if (q > 0) row[q - 1] = s2 ? ((prev << s2) | (P >> (64 - s2))) : prev;
         prev = P;
     }
+#ifndef PA_PACK_MASKED
+    // a non-ACGT byte in the staged chunks, most likely outside the read (the
+    // buffer's padding after the last read): only the read's own bytes count
+    // (the chunks loaded again: nothing stays live across the packing)
+    if (bad) {
+        bad = 0;
+#pragma unroll 1
+        for (int c = 0; c < 2 * kLaneWords; c++) {
+            if (16u * c >= shift + len) break;
+            const uint4 v = sp[c];
+            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                bad |= swar_bad_bytes(d[e], swar_codes(d[e])) & in_read_mask(16u * c + 4 * e, shift, len);
+        }
+    }
+#endif
     row[kLaneWords] = 0;
     if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
 #if defined(PA_STATS) || defined(PA_DISSECT)
@@ -426,18 +455,18 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #ifdef PA_STATS
             atomicAdd(&a.dbg[26], 1ull);
 #endif
-            uint32_t best = ~0u, bj = 0;
-#pragma unroll 1
-            for (uint32_t j = 0; j < 3; j++) {
-                const int64_t Aj = j == 0 ? e0 : (j == 1 ? e1 : e2);
-                if (Aj == INT64_MIN) break;
-                const uint32_t m = lane_mismatches(a, row, len, Aj);
-                if (m < best) {
-                    best = m;
-                    bj = j;
-                }
-                if (best == 0) break;
-            }
+            // the stretches' walk blocks loaded together (one round trip, not one per stretch)
+            const bool f0 = lane_fits(a, len, e0), f1 = lane_fits(a, len, e1), f2 = e2 != INT64_MIN && lane_fits(a, len, e2);
+            uint64_t g0[kLaneWords + 1], g1[kLaneWords + 1], g2[kLaneWords + 1], u3[3];
+            lane_blocks<false>(a, f0 ? (uint64_t)e0 : 0, len, g0, u3, u3);
+            lane_blocks<false>(a, f1 ? (uint64_t)e1 : 0, len, g1, u3, u3);
+            lane_blocks<false>(a, f2 ? (uint64_t)e2 : 0, len, g2, u3, u3);
+            const uint32_t m0 = f0 ? lane_count_mismatches(row, len, (uint64_t)e0, g0) : ~0u;
+            const uint32_t m1 = f1 ? lane_count_mismatches(row, len, (uint64_t)e1, g1) : ~0u;
+            const uint32_t m2 = f2 ? lane_count_mismatches(row, len, (uint64_t)e2, g2) : ~0u;
+            uint32_t bj = 0, best = m0;
+            if (m1 < best) best = m1, bj = 1;
+            if (m2 < best) best = m2, bj = 2;
             if (bj == 1) {
                 S.atp = t1, S.aw = w1, S.acls = c1;
             } else if (bj == 2) {
@@ -693,9 +722,11 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
         constexpr int NPR = PA_LANE_PROBES;
         uint64_t key4[NPR];
         uint32_t tag4[NPR], act = 0;
+        // entry 64 i + lane: with fewer than 64 (NPR - 1) entries the last keys
+        // of every lane are idle, and their hashing and probing is skipped
 #pragma unroll
         for (int i = 0; i < NPR; i++) {
-            const uint32_t e = NPR * lane + i;
+            const uint32_t e = 64 * i + lane;
             key4[i] = 0;
             tag4[i] = 0;
             if (e < cnt) {
@@ -712,9 +743,13 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
             uint64_t bw[NPR], bm[NPR];
 #pragma unroll
             for (int i = 0; i < NPR; i++) {
-                uint64_t wi;
-                bloom_word(key4[i], a.k, a.bloom_lg, wi, bm[i]);
-                bw[i] = bit(act, i) ? a.bloom[wi] : ~0ull;
+                bw[i] = ~0ull;
+                bm[i] = 0;
+                if (64u * i < cnt) {  // (uniform)
+                    uint64_t wi;
+                    bloom_word(key4[i], a.k, a.bloom_lg, wi, bm[i]);
+                    if (bit(act, i)) bw[i] = a.bloom[wi];
+                }
             }
 #pragma unroll
             for (int i = 0; i < NPR; i++)

@@ -614,3 +614,36 @@ def test_unanchored_reads_vs_oracle(ps, noanchor, monkeypatch):
     ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
     assert fk.tolist() == ofk.tolist(), ps
     assert o.stats[2] > 5000  # many unmapped reads: the case under test
+
+
+@pytest.mark.parametrize("k", [3, 4, 5, 8, 11, 16, 21, 28, 31])
+def test_quality_masks_every_k_vs_oracle(k):
+    """k_quality_masks (the lane kernels' --min-read-quality / --min-kmer-quality
+    pre-pass: 16-B chunks realigned to the read, the bytes k earlier by a second
+    realignment templated on k >> 2) at every k residue and read length around
+    its limits (k - 1 .. 176, and longer reads left to the wave kernel), with
+    qualities in low and high runs so that both filters fire; equal to the oracle
+    (src/kmer.py:394-408, 420-423, 587)."""
+    rng = np.random.default_rng(700 + k)
+    gens = synth.family_genomes(6, 6000, seed=k, family_size=3, sub_rate=0.01, conserved_len=300)
+    nr = 4000
+    seq, _, _ = synth.sample_reads(gens, nr, 200, seed=k + 1, err_rate=0.01)
+    lens = rng.integers(max(1, k - 2), 181, nr)
+    lens[:40] = np.arange(130, 170)[:40] + (k % 3)
+    off = np.zeros(nr + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    s = np.concatenate([seq[i, :lens[i]] for i in range(nr)])
+    q = rng.integers(45, 75, len(s)).astype(np.uint8)
+    for st in rng.integers(0, len(s) - 40, len(s) // 60):  # low-quality runs
+        q[st:st + rng.integers(3, 40)] = rng.integers(33, 45)
+    index = N.Index(gens, k)
+    oix = O.OracleIndex(gens, k)
+    reads = N.Reads.upload(s, q, off)
+    for mrq, mkq in ((55, None), (None, 54), (56, 52), (58, 60)):
+        res = N.Result(index)
+        N.align(index, reads, N.Params.make(1, 1, mrq, mkq, None), 7, res)
+        got = [x.tolist() for x in res.fetch()]
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=1, p=1, mrq=mrq, mkq=mkq, mg=None, read_base=7, detail=False)
+        ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+        assert got == [o.stats.tolist(), o.unique.tolist(), o.ambiguous.tolist(), ofk.tolist()], (mrq, mkq)
+        assert (mrq is None or o.stats[3] > 0) and (mkq is None or o.stats[4] > 0)
