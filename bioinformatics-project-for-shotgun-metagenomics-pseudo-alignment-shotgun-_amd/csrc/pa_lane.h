@@ -10,9 +10,9 @@
 // read whose windows are, almost always, one stretch of one genome.  Here each
 // lane takes a whole read and proves that case cheaply:
 //   1. lane_prep: the read is 2-bit packed (16-B loads, SWAR codes) into the
-//      lane's LDS row; with a quality filter, the read mean and -- when the
-//      read's minimum quality can fail it -- a 128-bit mask of the windows
-//      failing --min-kmer-quality (a running sum over the staged chunks);
+//      lane's LDS row; with a quality filter, the read's mean test and the
+//      128-bit mask of the windows failing --min-kmer-quality come from the
+//      k_quality_masks pre-pass;
 //   2. five seed windows (first ... last) are probed in two rounds: the first
 //      and the last, then the middle three only if neither is specific.  A
 //      found seed gives the read's position on the concatenated genomes (the
