@@ -72,7 +72,15 @@ __device__ __forceinline__ uint64_t key_hash(const Key<NW> &k) {
 }
 
 // Home slot by multiply-high range reduction (table size need not be 2^n).
-__device__ __forceinline__ uint64_t home_slot(uint64_t h, uint64_t cap) { return __umul64hi(h, cap); }
+// For cap < 2^32 (every table up to 64 GiB) the same value from three 32-bit
+// multiplies instead of seven: with h = hi 2^32 + lo, floor(h cap / 2^64) =
+// floor((hi cap + floor(lo cap / 2^32)) / 2^32).
+__device__ __forceinline__ uint64_t home_slot(uint64_t h, uint64_t cap) {
+    if (cap >> 32) return __umul64hi(h, cap);
+    const uint32_t c = (uint32_t)cap;
+    const uint64_t x = (uint64_t)(uint32_t)(h >> 32) * c + __umulhi((uint32_t)h, c);
+    return x >> 32;
+}
 
 __device__ __forceinline__ uint32_t base_code(uint32_t ch) {
     return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : ch == 'T' ? 3u : 4u;
