@@ -1000,7 +1000,7 @@ constexpr size_t lane_lds_bytes(uint32_t G) {
 
 // k_align_lane_na: the reads k_align_lane found no seed for, one per lane.
 // Every window of the read (but those failing --min-kmer-quality) is looked up
-// -- the Bloom filter first, eight windows in flight, then the table for the
+// -- the Bloom filter first, sixteen windows in flight, then the table for the
 // few the filter lets through (src/kmer.py:410-429).  No k-mer found: UNMAPPED;
 // found ones all multi-genome (or above --max-genomes, counted as highly
 // redundant): AMBIGUOUS with an empty list (no specific k-mer,
@@ -1031,15 +1031,35 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
         }
         h[p] = y;
     }
+    // each window's minimum: with S >= 16 (k >= 30) every window of the group
+    // holds 15-mer 15, so it is min(suffix minimum from j to 15, prefix minimum
+    // from 15 to j + S - 1) -- 2 NAG + 1 min ops, not NAG (S - 1)
+    uint32_t mn[NAG];
+    if (NAG == 16 && S >= 16) {  // (uniform)
+        uint32_t sfx[16], pfx[17];
+        sfx[15] = pfx[0] = h[15];
+#pragma unroll
+        for (int j = 14; j >= 0; j--) sfx[j] = min(h[j], sfx[j + 1]);
+#pragma unroll
+        for (int t = 1; t < 17; t++) pfx[t] = min(pfx[t - 1], h[15 + t]);
+#pragma unroll
+        for (int j = 0; j < NAG; j++) mn[j] = min(sfx[j], S == 17 ? pfx[j + 1] : pfx[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < NAG; j++) {
+            uint32_t best = ~0u;
+#pragma unroll
+            for (int i = 0; i < 17; i++)
+                if (i < S) best = h[j + i] < best ? h[j + i] : best;
+            mn[j] = best;
+        }
+    }
     uint64_t bw[NAG];
     uint32_t lo[NAG];
     uint64_t hi = 0;  // bits 32..35 of each key's mix, 4 per window
 #pragma unroll
     for (int j = 0; j < NAG; j++) {
-        uint32_t best = ~0u;
-#pragma unroll
-        for (int i = 0; i < 17; i++)
-            if (i < S) best = h[j + i] < best ? h[j + i] : best;
+        const uint32_t best = mn[j];
         const uint64_t hk = bloom_mix(row_bits(row, 2 * (w0 + j)) >> sh);
         lo[j] = (uint32_t)hk;
         hi |= ((hk >> 32) & 15ull) << (4 * j);
