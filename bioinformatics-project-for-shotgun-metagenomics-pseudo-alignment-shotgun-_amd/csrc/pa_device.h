@@ -228,6 +228,28 @@ __device__ __forceinline__ uint64_t bloom_mix(uint64_t x) {
     x ^= x >> 33;
     return x;
 }
+// The key's mix (bits 0..35: the six fields, bits 61..63: the word within its
+// line) and the line's mix of a minimizer hash.  One xorshift-multiply round
+// (splitmix-style: the high key bits folded in first, the fields taken from the
+// product's high bits, which depend on every key bit) and a 32 x 64 Fibonacci
+// multiply for the line (the minimum of 17 hashes is small; the product's top
+// bits spread it) -- about half the multiplies of two fmix64 rounds, for every
+// Bloom query of the align kernels and every key of the build.
+__device__ __forceinline__ uint64_t bloom_key_mix(uint64_t key) {
+#ifdef PA_BLOOM_MIX_FULL
+    return bloom_mix(key);
+#else
+    const uint64_t h = (key ^ (key >> 31) ^ 0x9E3779B97F4A7C15ull) * 0xff51afd7ed558ccdull;
+    return ((h >> 25) & ((1ull << 36) - 1)) | (h & (7ull << 61));
+#endif
+}
+__device__ __forceinline__ uint64_t bloom_line_mix(uint32_t best) {
+#ifdef PA_BLOOM_MIX_FULL
+    return bloom_mix(best);
+#else
+    return (uint64_t)best * 0x9E3779B97F4A7C15ull;
+#endif
+}
 __device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
     uint64_t m = 0;
 #pragma unroll
@@ -240,7 +262,7 @@ __device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
 // most neighbours, read the same line (+1 % on C2, C3) -- the word within the
 // line and the bits by the k-mer's own mix.
 __device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uint64_t &w, uint64_t &m) {
-    const uint64_t h = bloom_mix(key);
+    const uint64_t h = bloom_key_mix(key);
     m = bloom_bits(h);
     const int mm = k < 15 ? k : 15;
     const uint64_t mmask = (1ull << (2 * mm)) - 1;
@@ -251,7 +273,7 @@ __device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uin
         y ^= y >> 15;
         best = y < best ? y : best;
     }
-    const uint64_t line = bloom_mix(best) >> (64 - (lg - 3));
+    const uint64_t line = bloom_line_mix(best) >> (64 - (lg - 3));
     w = (line << 3) | (h >> 61);
 }
 

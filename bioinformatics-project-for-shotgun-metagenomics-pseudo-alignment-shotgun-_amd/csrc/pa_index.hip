@@ -648,7 +648,7 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
     }
 }
 
-// The Bloom filter of the table's keys (pa_device.h bloom_mix): one pass over
+// The Bloom filter of the table's keys (pa_device.h bloom_word): one pass over
 // the slots, an atomic OR per key.
 __global__ void k_bloom_build(const Slot<1> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg, int k) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;

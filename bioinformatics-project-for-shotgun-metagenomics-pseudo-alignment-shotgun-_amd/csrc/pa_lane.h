@@ -1060,10 +1060,10 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
 #pragma unroll
     for (int j = 0; j < NAG; j++) {
         const uint32_t best = mn[j];
-        const uint64_t hk = bloom_mix(row_bits(row, 2 * (w0 + j)) >> sh);
+        const uint64_t hk = bloom_key_mix(row_bits(row, 2 * (w0 + j)) >> sh);
         lo[j] = (uint32_t)hk;
         hi |= ((hk >> 32) & 15ull) << (4 * j);
-        const uint64_t wi = ((bloom_mix(best) >> (64 - (a.bloom_lg - 3))) << 3) | (hk >> 61);
+        const uint64_t wi = ((bloom_line_mix(best) >> (64 - (a.bloom_lg - 3))) << 3) | (hk >> 61);
         bw[j] = bit(act, j) ? a.bloom[wi] : ~0ull;
     }
 #pragma unroll
