@@ -1,8 +1,14 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the MI355X pseudo-alignment engine.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3raw|c2mix|c4|c5|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3raw|c2mix|c2rc|c4|c5|c1]
     torchrun --nproc-per-node N bench.py --gpus N ...            (one rank per GPU)
+
+With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset), this
+process starts the N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE and
+a 127.0.0.1 rendezvous in their environment) before anything touches the GPU,
+relays rank 0's line and exits non-zero if any rank fails.  A rank whose
+WORLD_SIZE differs from an explicit --gpus exits non-zero.
 
 Metric (BASELINE.json): reads/s pseudo-aligned, k=31, 150 bp reads, plus the
 achieved fraction of the HBM roofline.  Workload (SURVEY.md section 8d,
@@ -132,23 +138,39 @@ def random_line_roofline():
 
 
 REQ_COUNTERS = {"TCC_EA0_RDREQ_32B_sum": 32, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_EA0_RDREQ_128B_sum": 128}
+# the SQ counters of the same pass (8 SQ counters and 4 TCC fit one rocprofv3
+# pass; these count quad-cycles, so only their ratios are used)
+SQ_COUNTERS = ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")
+ALIGN_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_fast", "k_align_exact")
 
 
-def traffic_pass(args, cfg, kept_path):
-    """FETCH_SIZE of the align kernels per pass, measured now: a child process
-    repeats this workload under rocprofv3 --pmc FETCH_SIZE (2 passes after a
-    warmup).  Returns a dict, or None with a reason."""
+def kernel_short_name(mangled: str):
+    """The kernel's own identifier from its mangled name (the length prefix
+    keeps k_align_lane apart from k_align_lane_na), or None."""
+    import re
+    for m in re.finditer(r"(\d+)(k_[A-Za-z0-9_]+)", mangled):
+        name = m.group(2)[:int(m.group(1))]
+        if name in ALIGN_KERNELS:
+            return name
+    return None
+
+
+def counter_pass(args, cfg, kept_path, save_dir=None):
+    """Fabric read bytes and SQ cycle shares of the align kernels, measured now:
+    a child process repeats this workload under rocprofv3 --kernel-trace --pmc
+    (TCC_EA0_RDREQ_{32B,64B,128B} + 5 SQ counters, one pass; 2 passes of the
+    align after a warmup).  Returns ({kernel: {...}}, basis) or (None, reason).
+    With save_dir, the per-kernel summary is also written there."""
     import glob
     import shutil
     import sqlite3
-    import subprocess
     import tempfile
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None, "rocprofv3 not found"
     tmp = tempfile.mkdtemp(prefix="pa_traffic_", dir="/tmp")
-    cmd = [prof, "--kernel-trace", "--pmc", *REQ_COUNTERS, "-d", tmp, "-o", "run", "--", sys.executable,
-           os.path.abspath(__file__), "--traffic-child", "--config", args.config,
+    cmd = [prof, "--kernel-trace", "--pmc", *REQ_COUNTERS, *SQ_COUNTERS, "-d", tmp, "-o", "run", "--",
+           sys.executable, os.path.abspath(__file__), "--traffic-child", "--config", args.config,
            "--reads-per-gpu", str(cfg["reads_per_gpu"]), "--steps", "2", "--warmup", "1"]
     if args.genome_len:
         cmd += ["--genome-len", str(args.genome_len)]
@@ -157,8 +179,8 @@ def traffic_pass(args, cfg, kept_path):
     if kept_path:
         cmd += ["--kept-file", kept_path]
     env = dict(os.environ, TMPDIR="/tmp")
-    env.pop("RANK", None)
-    env.pop("WORLD_SIZE", None)
+    for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(v, None)
     try:
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                            timeout=900)
@@ -169,25 +191,60 @@ def traffic_pass(args, cfg, kept_path):
     dbs = glob.glob(os.path.join(tmp, "**", "*.db"), recursive=True)
     if not dbs:
         return None, "no rocprofv3 database written"
-    per = {}
+    raw = {}
     try:
         c = sqlite3.connect(dbs[0])
-        for name, cname, v in c.execute(
-                "select s.kernel_name, i.name, avg(e.value) from rocpd_pmc_event e "
+        for name, cname, v, n in c.execute(
+                "select s.kernel_name, i.name, avg(e.value), count(e.value) from rocpd_pmc_event e "
                 "join rocpd_info_pmc i on e.pmc_id = i.id join rocpd_event ev on e.event_id = ev.id "
                 "join rocpd_kernel_dispatch d on d.event_id = ev.id "
                 "join rocpd_info_kernel_symbol s on d.kernel_id = s.id group by s.kernel_name, i.name"):
-            for short in ("k_align_lane", "k_align_fast"):
-                if short in name and cname in REQ_COUNTERS:
-                    per[short] = per.get(short, 0.0) + float(v) * REQ_COUNTERS[cname]
+            short = kernel_short_name(name)
+            if short is not None:
+                raw.setdefault(short, {})[cname] = (float(v), int(n))
+        durs = {}
+        for name, avg_ns, n in c.execute(
+                "select s.kernel_name, avg(d.end - d.start), count(*) from rocpd_kernel_dispatch d "
+                "join rocpd_info_kernel_symbol s on d.kernel_id = s.id group by s.kernel_name"):
+            short = kernel_short_name(name)
+            if short is not None:
+                durs[short] = (float(avg_ns) / 1e6, int(n))
     except sqlite3.Error as e:
         return None, f"rocprofv3 database unreadable: {e}"
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+    per = {}
+    for k, cs in raw.items():
+        b = sum(cs[c][0] * w for c, w in REQ_COUNTERS.items() if c in cs)
+        wave = cs.get("SQ_WAVE_CYCLES", (0.0, 0))[0]
+        d = {"bytes_per_launch": b, "launches": max(x[1] for x in cs.values()),
+             "trace_avg_ms": durs.get(k, (None, 0))[0]}
+        if wave > 0:
+            d["sq_share_of_wave_cycles"] = {c[3:].lower(): cs[c][0] / wave for c in SQ_COUNTERS[1:] if c in cs}
+        per[k] = d
     if not per:
-        return None, "no align-kernel FETCH_SIZE samples"
-    return per, ("rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_{32B,64B,128B}_sum of this workload (child process, "
-                 "2 passes after a warmup, avg per dispatch): bytes = 32/64/128 x requests")
+        return None, "no align-kernel counter samples"
+    if save_dir:
+        os.makedirs(save_dir, exist_ok=True)
+        with open(os.path.join(save_dir, f"counters_{args.config}.json"), "w") as f:
+            json.dump({"command": " ".join(cmd[cmd.index("--") + 1:]), "counters": list(REQ_COUNTERS) +
+                       list(SQ_COUNTERS), "per_kernel_avg_per_dispatch": raw, "trace_avg_ms": durs}, f, indent=1)
+    return per, ("rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_{32B,64B,128B}_sum + SQ_{WAVE,BUSY}_CYCLES, "
+                 "SQ_WAIT_ANY, SQ_ACTIVE_INST_{ANY,VALU} of this workload in one pass (child process, 2 passes "
+                 "after a warmup, average per dispatch): bytes = 32/64/128 x requests (on gfx950 every L2 miss "
+                 "is a request of its size; FETCH_SIZE would count 128-B requests at 64 B, profiles/fetch_calib)")
+
+
+def bound_of(frac_hbm, sq) -> str:
+    """What limits the kernel, from its measured HBM fraction and SQ shares."""
+    if frac_hbm is not None and frac_hbm >= 0.7:
+        return "hbm"
+    if not sq:
+        return "unknown (no SQ counters)"
+    wait, valu = sq.get("wait_any", 0.0), sq.get("active_inst_valu", 0.0)
+    if wait >= 0.4:
+        return "latency+valu" if valu >= 0.15 else "latency"
+    return "valu" if valu >= 0.3 else "issue"
 
 
 def host_threads() -> int:
@@ -200,27 +257,53 @@ def host_threads() -> int:
     return max(1, min(n, 16))
 
 
-def cpu_baseline(cfg, genomes, index, reads, prm_kw, target_s: float):
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, genomes, index, reads, prm_kw, target_s: float, restricted: bool = False):
     """Time the oracle on a prefix of the reads (1 thread, then all host
-    threads over read shards); check GPU == oracle on the multi-thread sample."""
+    threads over read shards); check GPU == oracle on the multi-thread sample.
+    restricted (C5, whose full CPU index would need ~0.7 TB): the oracle index
+    holds the sample's k-mers only, each with its full genome list
+    (ora_index_build_restricted), built after the sample is chosen."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pa_oracle as O
-    t0 = time.perf_counter()
-    # one build thread: its pages sit on one NUMA node, as in round 1 (a build
-    # spread over the host's threads spreads them and slows the timed align)
-    oix = O.OracleIndex(genomes, cfg["k"], threads=1 if sum(len(g) for g in genomes) < 3e8 else host_threads())
-    build_s = time.perf_counter() - t0
     kw = dict(m=prm_kw.get("m", 1), p=prm_kw.get("p", 1), mrq=prm_kw.get("mrq"), mkq=prm_kw.get("mkq"),
               mg=prm_kw.get("mg"))
-    n1 = min(reads.n, 100000)
-    s, q, off = reads.download(0, n1)
+    threads = host_threads()
+    bases = sum(len(g) for g in genomes)
+    if restricted:
+        n = int(min(reads.n, 2_000_000))
+        s, q, off = reads.download(0, n)
+        t0 = time.perf_counter()
+        oix = O.OracleIndex.restricted(genomes, cfg["k"], (s, off), threads=threads)
+        build_s, build_threads = time.perf_counter() - t0, threads
+        n1 = min(n, 100000)
+        s1, q1, off1 = s[:int(off[n1])], q[:int(off[n1])], off[:n1 + 1]
+    else:
+        t0 = time.perf_counter()
+        # one build thread: its pages sit on one NUMA node, as in round 1 (a build
+        # spread over the host's threads spreads them and slows the timed align)
+        build_threads = 1 if bases < 3e8 else threads
+        oix = O.OracleIndex(genomes, cfg["k"], threads=build_threads)
+        build_s = time.perf_counter() - t0
+        n1 = min(reads.n, 100000)
+        s1, q1, off1 = reads.download(0, n1)
     t0 = time.perf_counter()
-    oix.align(s.tobytes(), q.tobytes(), off, detail=False, **kw)
+    oix.align(s1.tobytes(), q1.tobytes(), off1, detail=False, **kw)
     dt1 = time.perf_counter() - t0
     rate1 = n1 / max(dt1, 1e-9)
-    threads = host_threads()
-    n = int(min(reads.n, max(n1, rate1 * threads * target_s), 16_000_000))
-    s, q, off = reads.download(0, n)
+    if not restricted:
+        n = int(min(reads.n, max(n1, rate1 * threads * target_s), 16_000_000))
+        s, q, off = reads.download(0, n)
     t0 = time.perf_counter()
     o = O.align_counts_parallel(oix, s, q, off, threads, **kw)
     dt = time.perf_counter() - t0
@@ -232,17 +315,85 @@ def cpu_baseline(cfg, genomes, index, reads, prm_kw, target_s: float):
     ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
     exact = (stats.tolist() == o.stats.tolist() and uq.tolist() == o.unique.tolist()
              and am.tolist() == o.ambiguous.tolist() and fk.tolist() == ofk.tolist())
+    what = ("a RESTRICTED oracle index (the sample's k-mers with their full genome lists, streamed from the whole "
+            "reference: smaller than the full index, so this CPU rate is flattering)" if restricted else
+            "the full oracle index")
     return ({"value": n / dt, "unit": "reads/s", "cores": threads, "kind": "port",
-             "single_thread": rate1,
+             "single_thread": rate1, "cpu_model": cpu_model(),
+             "index_build": {"Mbp_per_s": bases / build_s / 1e6, "s": build_s, "threads": build_threads,
+                             "bases": bases, "restricted": restricted},
              "sample": f"first {n} of the benchmark's device-generated reads, oracle/pa_oracle.c on {threads} host "
-                       f"threads over read shards ({dt:.1f} s); 1 thread: {rate1:.0f} reads/s on the first {n1} "
-                       f"reads; oracle index build {build_s:.1f} s not included"},
-            {"reads": n, "bit_exact": bool(exact), "stats": [int(x) for x in stats]})
+                       f"threads over read shards ({dt:.1f} s) against {what}; 1 thread: {rate1:.0f} reads/s on "
+                       f"the first {n1} reads; oracle index build {build_s:.1f} s ({bases / build_s / 1e6:.1f} "
+                       f"Mbp/s on {build_threads} threads) not included"},
+            {"reads": n, "bit_exact": bool(exact), "stats": [int(x) for x in stats],
+             "oracle": "restricted" if restricted else "full"})
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, share_device: bool) -> int:
+    """--gpus N > 1 without torchrun: one child process per rank (this parent
+    never initialises the GPU), rank i on device i (share_device: all on device
+    0, the 1-GPU rehearsal).  Relays rank 0's stdout; a failed rank stops the
+    others.  Returns the exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0" if share_device else str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PA_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = []
+    import threading
+    reader = threading.Thread(target=lambda: out0.extend(procs[0].stdout.read().decode().splitlines()), daemon=True)
+    reader.start()
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            log(f"[launcher] a rank exited with {rc}: stopping the others")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    rc = rc or next((p.returncode for p in procs if p.returncode), 0)
+    for line in out0:
+        print(line, flush=True)
+    if rc == 0 and not any(x.startswith("{") for x in out0):
+        log("[launcher] rank 0 printed no result line")
+        rc = 1
+    return rc
+
+
+def counters_digest(result) -> dict:
+    """The job's counters after the last step (every rank holds them once
+    reduced): statistics plus a SHA-256 of the sum and min blocks, so a test can
+    compare an N-rank run with one process aligning the same global reads."""
+    import hashlib
+    stats, uq, am, fk = result.fetch()
+    h = hashlib.sha256()
+    for a in (stats, uq, am, fk):
+        h.update(np.ascontiguousarray(a, dtype=np.uint64).tobytes())
+    return {"stats": [int(x) for x in stats], "sha256": h.hexdigest()}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (GPUs); default WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -250,16 +401,22 @@ def main():
     ap.add_argument("--genome-len", type=int, default=None, help="override the genome length (experiments)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-traffic", action="store_true", help="skip the in-run FETCH_SIZE pass")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the in-run counter pass (traffic, SQ shares)")
+    ap.add_argument("--profile-dir", default=None, help="also write the counter pass's per-kernel summary here")
     ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--kept-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--reduce", choices=("torch", "capi"), default="torch",
                     help="N > 1: all-reduce through torch.distributed (RCCL) or libpa's pa_counters_reduce")
     ap.add_argument("--no-e2e", action="store_true",
                     help="C2 at N=1: skip the end-to-end dumpalign CLI figure (scripts/e2e_cli.py)")
+    ap.add_argument("--ranks-share-device", action="store_true", help=argparse.SUPPRESS)  # 1-GPU rehearsal
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--fail-rank", type=int, default=None, help=argparse.SUPPRESS)  # launcher test: this rank dies
     ap.add_argument("--params", default=None,
                     help='override the filter arguments, JSON, e.g. \'{"mg": 10}\' (experiments; named in config)')
     args = ap.parse_args()
+    if (args.gpus or 1) > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, args.ranks_share_device))
     cfg = dict(CONFIGS[args.config])
     if args.params is not None:
         cfg["params"] = json.loads(args.params)
@@ -271,11 +428,16 @@ def main():
         cfg["name"] += f" [genome_len overridden: {args.genome_len}]"
 
     import torch
-    rank, world, local = pa_dist.init_process_group()
+    rank, world, local = pa_dist.init_process_group(args.dist_backend)
+    if args.fail_rank == rank:
+        log(f"[rank {rank}] --fail-rank: exiting")
+        sys.exit(3)
+    if args.gpus is not None and world != args.gpus:
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    backend = torch.distributed.get_backend() if world > 1 else None
 
     t0 = time.perf_counter()
     gkw = dict(seed=1, family_size=cfg["family"], sub_rate=cfg["sub"], conserved_len=cfg["conserved"],
@@ -296,6 +458,7 @@ def main():
     index = N.Index(genomes, cfg["k"], device=local, stream=stream, defer_tiles=bool(filtering))
     torch.cuda.synchronize(dev)
     build_s = time.perf_counter() - t0
+    build_bases = sum(len(g) for g in genomes)
     extsim = None
     kept_path = None
     if args.kept_file:  # traffic child: the parent's EXTSIM outcome
@@ -320,6 +483,7 @@ def main():
             genomes = [genomes[j] for j in kept_idx]
             index = N.Index(genomes, cfg["k"], device=local, stream=stream, defer_tiles=True)
             torch.cuda.synchronize(dev)
+            build_bases += sum(len(g) for g in genomes)
         rebuild_s = time.perf_counter() - t1
         import tempfile
         fd, kept_path = tempfile.mkstemp(prefix="pa_kept_", suffix=".json", dir="/tmp")
@@ -348,6 +512,14 @@ def main():
         f"{info.n_multi_classes} multi-genome sets, table {info.table_bytes / 2**30:.2f} GiB; {npg} reads")
 
     comm = pa_dist.make_comm(local) if (world > 1 and args.reduce == "capi") else None
+    # the ranks an RCCL communicator of this job really spans (ncclCommCount);
+    # the torch path's communicator is torch's own, so one is made to ask
+    rccl_ranks = None
+    if world > 1 and backend == "nccl":
+        probe = comm if comm is not None else pa_dist.make_comm(local)
+        rccl_ranks = probe.n_ranks
+        if probe is not comm:
+            probe.close()
 
     def step():
         result.reset(stream)
@@ -380,17 +552,22 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms, launches, deferred = index.profile_read()
+    kern = index.profile_read_kernels()
     index.profile_enable(False)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
+    job_counters = counters_digest(result)
 
     total_reads = world * npg * args.steps
     value = total_reads / elapsed
-    kern_s = kern_ms / max(launches, 1) / 1e3
+    pass_s = kern_ms / max(launches, 1) / 1e3
     b_read = bytes_per_read(cfg)
-    achieved = b_read * npg / kern_s / 1e9 if kern_s > 0 else 0.0
+    alg_achieved = b_read * npg / pass_s / 1e9 if pass_s > 0 else 0.0
+    # the dominant kernel: the largest share of the timed align passes
+    dominant = max((k for k in kern if kern[k][1] > 0), key=lambda k: kern[k][0], default="k_align_lane")
+    dom_s = kern[dominant][0] / max(kern[dominant][1], 1) / 1e3
     out = {
         "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -399,14 +576,24 @@ def main():
         "config": {"workload": cfg["name"], "genomes": cfg["n_genomes"], "genome_len": cfg["genome_len"],
                    "k": cfg["k"], "reads_per_gpu": npg, "read_len": cfg["read_len"],
                    "filters": cfg["params"] or None, "parallelism": f"read-sharded x{world}, index replicated",
-                   "reduce": args.reduce if world > 1 else None,
+                   "reduce": args.reduce if world > 1 else None, "backend": backend, "rccl_ranks": rccl_ranks,
                    "read_mix": {"reverse_complement": cfg.get("rc_rate", 0.0), "foreign": cfg.get("foreign_rate", 0.0),
                                 "substitution_rate": cfg["read_err"]}},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "achieved_basis": "algorithmic bytes (SURVEY.md 8d: L + q*L + 16*(L-k+1) per read)",
-                     "kernel": "align pass: k_align_lane + k_align_fast", "kernel_ms": kern_s * 1e3, "bytes_per_read": b_read},
+        "roofline": {"bound": None, "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                     "traffic": None, "kernel": dominant, "kernel_ms": dom_s * 1e3,
+                     "achieved_basis": ("MEASURED fabric read bytes of the dominant kernel per launch (traffic, "
+                                        "counter pass) / its average duration (HIP events around each launch on "
+                                        "its stream over the timed steps) / 8 TB/s"),
+                     "algorithmic": {"bytes_per_read": b_read, "bytes_per_pass": b_read * npg,
+                                     "pass_ms": pass_s * 1e3, "achieved": alg_achieved,
+                                     "frac": alg_achieved / HBM_PEAK_GBS,
+                                     "basis": ("SURVEY.md 8d: L + q*L + 16*(L-k+1) per read over the whole align "
+                                               "pass (all align kernels); it prices one 16-B slot read per window, "
+                                               "which the lane walk mostly skips, so it can pass 1.0 and no longer "
+                                               "measures the kernel")},
+                     "kernels": {k: {"ms_avg": v[0] / v[1], "launches": v[1]} for k, v in kern.items() if v[1]}},
         "deferred_read_fraction": deferred / max(npg * args.steps, 1),
+        "job_counters": job_counters,
         "index": {"build_s": index_total_s, "first_build_s": build_s, "prepare_s": prepare_s,
                   "build_basis": ("FASTA genomes in host memory -> align-ready index: table + genome sets"
                                   + (", EXTSIM statistics and greedy pass, rebuild of the kept genomes" if extsim else "")
@@ -416,19 +603,25 @@ def main():
         "extsim": extsim,
         "cpu_baseline": None,
     }
-    if args.config == "c5" and not args.no_cpu_baseline:
-        # the oracle's index of the kept ~5 Gbp would need ~0.7 TB of host memory
-        out["cpu_baseline_note"] = ("skipped for C5 (the oracle index of the kept ~5 Gbp reference would need "
-                                    "~0.7 TB of host memory); C5's layout and EXTSIM are parity-tested in "
-                                    "tests/test_gpu_scale.py")
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # index-build roofline (B_bp = 17 B per genome base -- one
+    # base read + one 16-B slot touched -- over every build of the job)
+    bases_built = int(build_bases)
+    ib = out["index"]
+    ib["bases_built"] = bases_built
+    ib["Mbp_per_s"] = bases_built / index_total_s / 1e6 if index_total_s > 0 else None
+    ib["roofline"] = {"bytes_per_base": 17, "achieved": 17 * bases_built / index_total_s / 1e9,
+                      "frac": 17 * bases_built / index_total_s / 1e9 / HBM_PEAK_GBS, "unit": "GB/s",
+                      "basis": "17 B per genome base of every build (first build + EXTSIM rebuild) / build_s"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize(dev)
-        base, parity = cpu_baseline(cfg, genomes, index, reads, pk, args.cpu_seconds)
+        # C5: the oracle's full index of the kept ~5 Gbp would need ~0.7 TB of host memory
+        base, parity = cpu_baseline(cfg, genomes, index, reads, pk, args.cpu_seconds,
+                                    restricted=args.config == "c5")
         out["cpu_baseline"] = base
         out["parity_sample"] = parity
-    # the traffic pass last, after this process's device memory is released:
+    # the counter pass last, after this process's device memory is released:
     # its child rebuilds the same index and reads (C5's would not fit twice)
-    traffic = measured_frac = lines_per_read = line_frac = per = None
+    per = None
     line_peak, line_src = random_line_roofline()
     if rank == 0 and world == 1 and not args.no_traffic:
         result.close()
@@ -436,15 +629,32 @@ def main():
         index.close()
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
-        per, tnote = traffic_pass(args, cfg, kept_path)
-        if per is not None:
-            traffic = sum(per.values())
-            measured_frac = traffic / kern_s / 1e9 / HBM_PEAK_GBS if kern_s > 0 else None
-            line_frac = traffic / kern_s / 1e9 / line_peak if (kern_s > 0 and line_peak) else None
-            lines_per_read = traffic / 128.0 / npg
-            log(f"[rank 0] traffic: {traffic / 1e9:.2f} GB per pass ({lines_per_read:.1f} 128-B lines/read)")
+        per, tnote = counter_pass(args, cfg, kept_path, args.profile_dir)
     else:
         tnote = "not measured (--no-traffic, or a rank of a multi-GPU run)"
+    rl = out["roofline"]
+    rl["traffic_basis"] = tnote
+    rl["random_line_peak"], rl["random_line_peak_source"] = line_peak, line_src
+    if per is not None:
+        for k, d in per.items():
+            kd = rl["kernels"].setdefault(k, {})
+            kd.update(d)
+            ms = kd.get("ms_avg")
+            if ms:
+                kd["measured_GBs"] = d["bytes_per_launch"] / (ms / 1e3) / 1e9
+                kd["frac"] = kd["measured_GBs"] / HBM_PEAK_GBS
+            kd["lines_per_read"] = d["bytes_per_launch"] / 128.0 / npg
+        if dominant in per and dom_s > 0:
+            d = per[dominant]
+            rl["traffic"] = d["bytes_per_launch"]
+            rl["achieved"] = d["bytes_per_launch"] / dom_s / 1e9
+            rl["frac"] = rl["achieved"] / HBM_PEAK_GBS
+            rl["sq"] = d.get("sq_share_of_wave_cycles")
+            rl["random_line_frac"] = rl["achieved"] / line_peak if line_peak else None
+            rl["pass_lines_per_read"] = sum(x["bytes_per_launch"] for x in per.values()) / 128.0 / npg
+            log(f"[rank 0] {dominant}: {rl['traffic'] / 1e9:.2f} GB per launch in {dom_s * 1e3:.3f} ms "
+                f"= {rl['achieved']:.0f} GB/s ({rl['frac']:.3f} of HBM peak)")
+    rl["bound"] = bound_of(rl["frac"], rl.get("sq"))
     if kept_path:
         os.unlink(kept_path)
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_e2e and not args.traffic_child:
@@ -455,9 +665,6 @@ def main():
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
         out["end_to_end"] = e2e_pass()
-    out["roofline"].update({"traffic": traffic, "measured_frac": measured_frac, "lines_per_read": lines_per_read,
-                            "traffic_by_kernel": per, "traffic_basis": tnote, "random_line_frac": line_frac,
-                            "random_line_peak": line_peak, "random_line_peak_source": line_src})
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

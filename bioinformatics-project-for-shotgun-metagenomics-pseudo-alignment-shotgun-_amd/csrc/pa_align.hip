@@ -687,7 +687,26 @@ pa_status launch_fast(const AlignArgs &a, size_t shm, hipStream_t st) {
     return PA_OK;
 }
 
-pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
+// Per-kernel profile events (pa_profile_read_kernels): a pair around one
+// launch on its stream while the index's profiling is on.
+struct KernelTimer {
+    pa_index *idx;
+    hipStream_t st;
+    int slot;
+    hipEvent_t e0 = nullptr;
+    KernelTimer(pa_index *i, hipStream_t s, int sl) : idx(i), st(s), slot(sl) {
+        if (idx && idx->profile && hipEventCreate(&e0) == hipSuccess) hipEventRecord(e0, st);
+    }
+    ~KernelTimer() {
+        hipEvent_t e1 = nullptr;
+        if (e0 && hipEventCreate(&e1) == hipSuccess && hipEventRecord(e1, st) == hipSuccess)
+            idx->kev.push_back({slot, e0, e1});
+        else if (e0)
+            hipEventDestroy(e0);
+    }
+};
+
+pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
     const size_t shm = lane_lds_bytes(a.G);
     const bool win_q = (a.prm.flags & F_MKQ) != 0;
@@ -703,8 +722,11 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
     const uint64_t want = (a.n + kBlock - 1) / kBlock;
     const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)cus;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), shm, st, a);
-    PA_HIP(hipGetLastError());
+    {
+        KernelTimer kt(prof, st, PA_PROF_LANE);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), shm, st, a);
+        PA_HIP(hipGetLastError());
+    }
     if (a.queue_na) {  // the reads without a seed in the index (count on the device)
         auto na = win_q ? (mg ? k_align_lane_na<true, true, true> : k_align_lane_na<true, true, false>)
                 : need_q ? (mg ? k_align_lane_na<true, false, true> : k_align_lane_na<true, false, false>)
@@ -713,6 +735,7 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st) {
         PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&na_cu, na, kBlock, 0));
         const unsigned ngrid = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>(want, (uint64_t)std::max(1, na_cu) * (uint64_t)cus));
+        KernelTimer kt(prof, st, PA_PROF_LANE_NA);
         hipLaunchKernelGGL(na, dim3(ngrid), dim3(kBlock), 0, st, a);
         PA_HIP(hipGetLastError());
 
@@ -999,6 +1022,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));
             if (a.prm.flags & (F_MRQ | F_MKQ)) {  // the quality filters of every read, up front
                 PA_TRY(ensure_qmask(idx, r->n));
+                KernelTimer kt(idx, st, PA_PROF_QUALITY);
                 hipLaunchKernelGGL(k_quality_masks, dim3((unsigned)std::min<uint64_t>((r->n + 255) / 256, 65536)),
                                    dim3(256), 0, st, r->qual, r->off, r->n, (int)idx->k, (int64_t)a.prm.mrq,
                                    (int64_t)a.prm.mkq, a.prm.flags & (F_MRQ | F_MKQ), idx->qmask, idx->qdrop);
@@ -1014,11 +1038,14 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.na_min = 32768;  // (PA_NA_MIN: tests)
             if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
             if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 8, st));
-            PA_TRY(launch_lane(a, st));
+            PA_TRY(launch_lane(a, st, idx));
             a.rlist = idx->queue_hard;
             a.rlist_count = a.queue_hard_count;
         }
-        PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
+        {
+            KernelTimer kt(idx, st, PA_PROF_WAVE);
+            PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
+        }
         if (idx->profile) {
             PA_HIP(hipEventRecord(e1, st));
             idx->ev_start.push_back(e0);
@@ -1029,8 +1056,11 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
     } else {
         x.use_queue = 0;
     }
-    launch_exact_nw(idx->nw, x, egrid, st);
-    PA_HIP(hipGetLastError());
+    {
+        KernelTimer kt(idx, st, PA_PROF_EXACT);
+        launch_exact_nw(idx->nw, x, egrid, st);
+        PA_HIP(hipGetLastError());
+    }
 #ifdef PA_STATS
     unsigned long long d[32];
     PA_HIP(hipMemcpyAsync(d, idx->counters, 256, hipMemcpyDeviceToHost, st));

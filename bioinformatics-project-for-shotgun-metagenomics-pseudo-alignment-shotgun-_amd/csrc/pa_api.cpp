@@ -571,4 +571,29 @@ pa_status pa_profile_read(pa_index *idx, double *main_ms, uint64_t *launches, ui
     return PA_OK;
 }
 
+pa_status pa_profile_read_kernels(pa_index *idx, double *ms, uint64_t *launches) {
+    PA_CHECK(idx != nullptr && ms != nullptr && launches != nullptr, PA_EINVAL, "NULL argument");
+    PA_HIP(hipSetDevice(idx->device));
+    for (int i = 0; i < PA_PROF_KERNELS; i++) {
+        ms[i] = 0;
+        launches[i] = 0;
+    }
+    pa_status rc = PA_OK;
+    for (const auto &e : idx->kev) {
+        float t = 0;
+        hipError_t he = hipEventSynchronize(e.stop);
+        if (he == hipSuccess) he = hipEventElapsedTime(&t, e.start, e.stop);
+        if (he != hipSuccess && rc == PA_OK) {
+            pa::set_error(std::string("pa_profile_read_kernels: ") + hipGetErrorString(he));
+            rc = PA_EDEVICE;
+        }
+        ms[e.slot] += t;
+        launches[e.slot]++;
+        hipEventDestroy(e.start);
+        hipEventDestroy(e.stop);
+    }
+    idx->kev.clear();
+    return rc;
+}
+
 }  // extern "C"

@@ -119,6 +119,18 @@ pa_status pa_comm_free(void *comm) {
     return rccl_status(rccl().comm_destroy((ncclComm_t)comm), "ncclCommDestroy");
 }
 
+pa_status pa_comm_count(void *comm, int32_t *nranks) {
+    if (!comm || !nranks) {
+        pa::set_error("pa_comm_count: comm and nranks must not be NULL");
+        return PA_EINVAL;
+    }
+    PA_NEED_RCCL();
+    int n = 0;
+    PA_TRY(rccl_status(rccl().comm_count((ncclComm_t)comm, &n), "ncclCommCount"));
+    *nranks = n;
+    return PA_OK;
+}
+
 pa_status pa_counters_reduce(pa_result *res, void *comm, void *stream) {
     if (!res || !comm) {
         pa::set_error("pa_counters_reduce: res and comm must not be NULL");

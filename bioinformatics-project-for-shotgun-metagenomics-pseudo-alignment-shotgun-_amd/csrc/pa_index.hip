@@ -1199,6 +1199,11 @@ void index_release(pa_index *idx) {
     hipFree(idx->counters);
     for (auto e : idx->ev_start) hipEventDestroy(e);
     for (auto e : idx->ev_stop) hipEventDestroy(e);
+    for (auto &e : idx->kev) {
+        hipEventDestroy(e.start);
+        hipEventDestroy(e.stop);
+    }
+    idx->kev.clear();
     idx->table = nullptr;
 }
 

@@ -115,6 +115,11 @@ struct pa_index {
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> ev_start, ev_stop;
+    struct KernelEvents {
+        int slot;  // PA_PROF_* (include/pa.h)
+        hipEvent_t start, stop;
+    };
+    std::vector<KernelEvents> kev;     // one pair per kernel launch of the align pass
     double prof_ms = 0;
     uint64_t prof_launches = 0;
 };

@@ -38,8 +38,8 @@ EXPORTS = (
     "pa_result_copy_in", "pa_result_free",
     "pa_align", "pa_align_detail", "pa_align_batch", "pa_align_fastq_file",
     "pa_fastq_prefetch_start", "pa_align_fastq_prefetched", "pa_fastq_prefetch_free",
-    "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_counters_reduce",
-    "pa_profile_enable", "pa_profile_read",
+    "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_comm_count", "pa_counters_reduce",
+    "pa_profile_enable", "pa_profile_read", "pa_profile_read_kernels",
     "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free",
 )
 
@@ -142,9 +142,11 @@ def lib():
         "pa_comm_unique_id": (I32, [P]),
         "pa_comm_init": (I32, [I32, I32, I32, P, PP]),
         "pa_comm_free": (I32, [P]),
+        "pa_comm_count": (I32, [P, ctypes.POINTER(I32)]),
         "pa_counters_reduce": (I32, [P, P, P]),
         "pa_profile_enable": (I32, [P, I32]),
         "pa_profile_read": (I32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        "pa_profile_read_kernels": (I32, [P, P, P]),
         "pa_parse_text": (I32, [I32, P, U64, I32, I32, PP]),
         "pa_parse_file": (I32, [I32, ctypes.c_char_p, I32, PP]),
         "pa_seqset_sizes": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
@@ -405,6 +407,16 @@ class Index:
     def profile_enable(self, on: bool = True):
         _check(lib().pa_profile_enable(self._h, 1 if on else 0))
 
+    PROF_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_fast", "k_align_exact")
+
+    def profile_read_kernels(self) -> dict:
+        """{kernel: (summed ms, launches)} of the align passes since the last
+        call (pa_profile_read_kernels: HIP events around each launch)."""
+        ms = np.zeros(len(self.PROF_KERNELS), dtype=np.float64)
+        nl = np.zeros(len(self.PROF_KERNELS), dtype=np.uint64)
+        _check(lib().pa_profile_read_kernels(self._h, _ptr(ms), _ptr(nl)))
+        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(self.PROF_KERNELS)}
+
     def profile_read(self) -> Tuple[float, int, int]:
         ms = ctypes.c_double(0)
         nl = U64(0)
@@ -549,6 +561,13 @@ class Comm:
     @property
     def handle(self):
         return self._h
+
+    @property
+    def n_ranks(self) -> int:
+        """Ranks the communicator spans (pa_comm_count -> ncclCommCount)."""
+        n = I32(0)
+        _check(lib().pa_comm_count(self._h, ctypes.byref(n)))
+        return int(n.value)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -297,6 +297,8 @@ pa_status pa_runtime_start(int32_t device);
 pa_status pa_comm_unique_id(uint8_t *id /* [PA_COMM_ID_BYTES], rank 0; share it with the others */);
 pa_status pa_comm_init(int32_t device, int32_t nranks, int32_t rank, const uint8_t *id, void **comm);
 pa_status pa_comm_free(void *comm);
+/* ranks in the communicator (ncclCommCount): what a job's reduce really spans */
+pa_status pa_comm_count(void *comm, int32_t *nranks);
 pa_status pa_counters_reduce(pa_result *res, void *comm, void *stream);
 
 /* ---- profiling ------------------------------------------------------------------ */
@@ -307,6 +309,17 @@ pa_status pa_counters_reduce(pa_result *res, void *comm, void *stream);
  * (deferred) path since the last read. */
 pa_status pa_profile_enable(pa_index *idx, int32_t enable);
 pa_status pa_profile_read(pa_index *idx, double *main_ms, uint64_t *launches, uint64_t *deferred_reads);
+/* The same events per kernel of the align pass (each launch bracketed by its
+ * own pair on the launch stream): ms[PA_PROF_KERNELS] summed milliseconds and
+ * launches[PA_PROF_KERNELS] launch counts since the last call, indexed by
+ * PA_PROF_*.  Independent of pa_profile_read (either may be read first). */
+#define PA_PROF_QUALITY 0   /* k_quality_masks */
+#define PA_PROF_LANE 1      /* k_align_lane (the dominant kernel) */
+#define PA_PROF_LANE_NA 2   /* k_align_lane_na */
+#define PA_PROF_WAVE 3      /* k_align_fast */
+#define PA_PROF_EXACT 4     /* k_align_exact */
+#define PA_PROF_KERNELS 5
+pa_status pa_profile_read_kernels(pa_index *idx, double *ms, uint64_t *launches);
 
 /* ---- ingest (host only, no device) ---------------------------------------------- */
 

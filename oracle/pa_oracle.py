@@ -59,6 +59,9 @@ def lib():
         L.ora_index_build.argtypes = [ctypes.c_char_p, P, ctypes.c_uint32, ctypes.c_int64]
         L.ora_index_build_mt.restype = P
         L.ora_index_build_mt.argtypes = [ctypes.c_char_p, P, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int]
+        L.ora_index_build_restricted.restype = P
+        L.ora_index_build_restricted.argtypes = [P, P, ctypes.c_uint32, ctypes.c_int64, P, P, ctypes.c_uint32,
+                                                 ctypes.c_int]
         L.ora_index_free.argtypes = [P]
         L.ora_index_n_kmers.restype = U64
         L.ora_index_n_kmers.argtypes = [P]
@@ -85,6 +88,17 @@ def concat(chunks: Sequence) -> Tuple[bytes, np.ndarray]:
     off = np.zeros(len(bs) + 1, dtype=np.uint64)
     off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
     return b"".join(bs), off
+
+
+def _packed(x) -> Tuple[np.ndarray, np.ndarray]:
+    """(uint8 buffer, uint64 CSR offsets) of a sequence list, or the pair as is."""
+    if isinstance(x, tuple) and len(x) == 2 and isinstance(x[1], np.ndarray):
+        buf, off = x
+        buf = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+        return buf, np.ascontiguousarray(off, dtype=np.uint64)
+    text, off = concat(x)
+    buf = np.frombuffer(text, dtype=np.uint8) if text else np.zeros(1, dtype=np.uint8)
+    return buf, off
 
 
 @dataclass
@@ -140,8 +154,30 @@ class OracleIndex:
             lib().ora_index_free(h)
             self._h = None
 
+    @classmethod
+    def restricted(cls, genomes, k: int, seeds, threads: Optional[int] = None) -> "OracleIndex":
+        """The k-mers of ``seeds`` only, each with exactly the genome list the full
+        index gives it (ora_index_build_restricted): reads drawn from the seeds
+        align as against the full index, and for every genome in the seeds
+        ``extsim_stats`` rows are exact.  Memory scales with the seeds, so BASELINE
+        configs 4-5 (1 and 8 Gbp) get full-size parity.  ``genomes`` / ``seeds``:
+        sequences, or already concatenated ``(uint8 array, uint64 offsets)``."""
+        self = cls.__new__(cls)
+        self.k = int(k)
+        gbuf, goff = _packed(genomes)
+        sbuf, soff = _packed(seeds)
+        self.n_genomes = len(goff) - 1
+        self._off = goff
+        self._h = lib().ora_index_build_restricted(_ptr(gbuf), _ptr(goff), self.n_genomes, self.k, _ptr(sbuf),
+                                                   _ptr(soff), len(soff) - 1,
+                                                   int(threads if threads else host_threads()))
+        if not self._h:
+            raise MemoryError("oracle restricted index build failed")
+        return self
+
     @property
     def n_kmers(self) -> int:
+        """Distinct k-mers (a restricted index: those of its seeds that some genome holds)."""
         return int(lib().ora_index_n_kmers(self._h))
 
     def lookup(self, kmer: str) -> List[int]:

@@ -1,0 +1,84 @@
+"""bench.py --gpus N starts its own N ranks.
+
+The driver's scaling runs call ``python bench.py --gpus N``; without a torchrun
+environment the parent starts the N rank processes itself, before anything
+touches the GPU, and the line it prints is rank 0's, with ``n_gpus`` = the
+ranks that ran.  On the 1-GPU test box both ranks share device 0 and reduce
+over gloo (a test-only flag); the job's counters must then equal one process
+aligning the same 2 x N global reads -- weak scaling with global read indices.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+SMALL = ["--config", "c2", "--reads-per-gpu", "200000", "--genome-len", "200000", "--steps", "2", "--warmup", "1",
+         "--no-cpu-baseline", "--no-traffic", "--no-e2e"]
+
+
+def test_launcher_fails_loudly_when_a_rank_fails():
+    """A rank that dies after the rendezvous (a test flag) makes the whole job
+    exit non-zero with no result line, the other rank stopped rather than left
+    waiting in a collective -- never a silent 1-rank run.  CPU: gloo, and the
+    dying rank exits before any device call."""
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--ranks-share-device", "--dist-backend", "gloo",
+                        "--fail-rank", "1"] + SMALL, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=300)
+    assert r.returncode != 0
+    assert "--fail-rank" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_rank_world_mismatch_is_an_error():
+    """A rank started with WORLD_SIZE != --gpus refuses to run."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2"] + SMALL, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_two_ranks_launched_by_bench_equal_one_process():
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--ranks-share-device", "--dist-backend", "gloo"]
+                       + SMALL, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["backend"] == "gloo"
+    npg = line["config"]["reads_per_gpu"]
+    assert npg == 200000 and line["value"] > 0
+
+    # one process, the same index and the same 2 x npg global reads
+    sys.path.insert(0, REPO)
+    import bench
+    import pa_native as N
+    import synth
+    cfg = dict(bench.CONFIGS["c2"], genome_len=200000)
+    gens = synth.family_genomes(cfg["n_genomes"], cfg["genome_len"], seed=1, family_size=cfg["family"],
+                                sub_rate=cfg["sub"], conserved_len=cfg["conserved"], n_rate=cfg["n_rate"],
+                                n_run=cfg["n_run"])
+    index = N.Index(gens, cfg["k"], device=0)
+    res = N.Result(index)
+    for rank in range(2):
+        reads = N.Reads.synthesize(index, npg, cfg["read_len"], first_read=rank * npg, seed=2,
+                                   sub_rate=cfg["read_err"])
+        N.align(index, reads, N.Params.make(), rank * npg, res)
+        reads.close()
+    want = bench.counters_digest(res)
+    assert line["job_counters"] == want
+    assert sum(want["stats"][:4]) == 2 * npg
+    res.close()
+    index.close()
