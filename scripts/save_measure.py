@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Copy one scripts/measure.sh result into profiles/r02/: the bench line, the
-rocprofv3 kernel summary of the same workload and its SQ counter pass, each
-summarised by profiles/rocpd_summary.py, plus the git commit measured.
+"""Copy one scripts/measure.sh result into profiles/r03/: the bench line, its
+counter pass (per-kernel fabric bytes and SQ shares, JSON) and the rocprofv3
+kernel summary of the same workload, stamped with the git commit measured.
 
     python scripts/save_measure.py <tag> [name]      (name defaults to the tag)
 """
@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main(tag: str, name: str) -> None:
     src = os.path.join(REPO, "gpurun_out", f"ms_{tag}")
-    dst = os.path.join(REPO, "profiles", "r02")
+    dst = os.path.join(REPO, "profiles", "r03")
     os.makedirs(dst, exist_ok=True)
     head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True, text=True).stdout.strip()
     with open(os.path.join(src, "args")) as f:
@@ -24,6 +24,11 @@ def main(tag: str, name: str) -> None:
         line = f.read()
     with open(os.path.join(dst, f"bench_{name}.json"), "w") as f:
         f.write(line)
+    for cj in glob.glob(os.path.join(src, "counters_*.json")):
+        with open(cj) as f:
+            body = f.read()
+        with open(os.path.join(dst, f"{name}_counters.json"), "w") as f:
+            f.write(body)
     summ = os.path.join(REPO, "profiles", "rocpd_summary.py")
     for kind, label in (("trace", "kernel_stats"), ("sq", "sq")):
         done = os.path.join(src, f"{label}.txt" if kind == "trace" else "sq.txt")
