@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void k_nl_write(const uint8_t *D, uint64_t t0,
     while (m) {
         const int j = __builtin_ctz(m);
         m &= m - 1;
-        nl[o++] = (uint32_t)(c0 + j);
+        nl[o++] = (uint32_t)(c0 + j - t0);  // relative to the window's first tile: < 2^32 for any file size
     }
 }
 
@@ -186,18 +186,18 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint32_t *in, uint64_t
 // Complete records of the window: the last window may end without a line
 // feed (one optional final line break); any other window ends at the line
 // feed of its last complete record, the rest is carried.
-__global__ void k_window_meta(const uint8_t *D, uint64_t lo, uint64_t hi, int last, uint32_t *nl,
+__global__ void k_window_meta(const uint8_t *D, uint64_t t0, uint64_t lo, uint64_t hi, int last, uint32_t *nl,
                               const unsigned long long *n_nl, Meta *meta) {
     if (threadIdx.x || blockIdx.x) return;
     uint64_t lines = *n_nl;
     meta->n_nl = lines;
     uint64_t end = lo;
     if (last) {
-        if (hi > lo && D[hi - 1] != '\n') nl[lines++] = (uint32_t)hi;  // the final line, no line feed
+        if (hi > lo && D[hi - 1] != '\n') nl[lines++] = (uint32_t)(hi - t0);  // the final line, no line feed
         if (lines % 4) meta->err |= kErrGrammar;
         end = hi;
     } else if (lines >= 4) {
-        end = (uint64_t)nl[(lines / 4) * 4 - 1] + 1;
+        end = t0 + (uint64_t)nl[(lines / 4) * 4 - 1] + 1;
     }
     meta->n_rec = lines / 4;
     meta->end = end;
@@ -206,14 +206,14 @@ __global__ void k_window_meta(const uint8_t *D, uint64_t lo, uint64_t hi, int la
 __device__ __forceinline__ bool id_byte(uint8_t c) { return c >= 0x21 && c <= 0x7E; }
 
 // One record per thread: header, "+" line, lengths, the id's hash.
-__global__ void k_records(const uint8_t *D, uint64_t lo, const uint32_t *nl, const Meta *meta, uint32_t *len,
+__global__ void k_records(const uint8_t *D, uint64_t t0, uint64_t lo, const uint32_t *nl, const Meta *meta, uint32_t *len,
                           unsigned long long *ids, uint64_t ids_cap, Meta *meta_out) {
     const uint64_t R = meta->n_rec;
     uint32_t bad = 0, mx = 0;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t hs = r ? (uint64_t)nl[4 * r - 1] + 1 : lo, he = nl[4 * r];
-        const uint64_t ss = he + 1, se = nl[4 * r + 1], ps = se + 1, pe = nl[4 * r + 2], qs = pe + 1,
-                       qe = nl[4 * r + 3];
+        const uint64_t hs = r ? t0 + nl[4 * r - 1] + 1 : lo, he = t0 + nl[4 * r];
+        const uint64_t ss = he + 1, se = t0 + nl[4 * r + 1], ps = se + 1, pe = t0 + nl[4 * r + 2], qs = pe + 1,
+                       qe = t0 + nl[4 * r + 3];
         const uint64_t n = se - ss;
         bool ok = he >= hs + 2 && D[hs] == '@' && id_byte(D[hs + 1]) && id_byte(D[he - 1]);
         ok = ok && n >= 1 && pe == ps + 1 && D[ps] == '+' && qe - qs == n && n < (1ull << 31);
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *D, uint64_t t0, 
     const uint4 v = *(const uint4 *)(D + c0);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint64_t li = li0;
-    uint64_t ls = li ? (uint64_t)nl[li - 1] + 1 : lo;  // start of the line holding byte c0 (or lo)
+    uint64_t ls = li ? t0 + nl[li - 1] + 1 : lo;  // start of the line holding byte c0 (or lo)
 #pragma unroll
     for (int j = 0; j < 16; j++) {
         const uint64_t p = c0 + j;
@@ -424,7 +424,7 @@ pa_status parse_align_window(ParseBufs &B, const uint8_t *D, uint64_t lo, uint64
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, B.bsum, (uint64_t)sgrid, B.tot);
     hipLaunchKernelGGL(k_scan_apply, dim3(sgrid), dim3(256), 0, st, B.tile_cnt, ntiles, B.bsum, B.tile_off);
     hipLaunchKernelGGL(k_nl_write, dim3((unsigned)ntiles), dim3(256), 0, st, D, t0, lo, hi, B.tile_off, B.nl);
-    hipLaunchKernelGGL(k_window_meta, dim3(1), dim3(1), 0, st, D, lo, hi, last ? 1 : 0, B.nl, B.tot, B.meta);
+    hipLaunchKernelGGL(k_window_meta, dim3(1), dim3(1), 0, st, D, t0, lo, hi, last ? 1 : 0, B.nl, B.tot, B.meta);
     PA_HIP(hipGetLastError());
     PA_HIP(hipMemcpyAsync(B.h_meta, B.meta, sizeof(Meta), hipMemcpyDeviceToHost, st));
     auto tw = now();
@@ -439,7 +439,7 @@ pa_status parse_align_window(ParseBufs &B, const uint8_t *D, uint64_t lo, uint64
     if (R == 0) return PA_OK;
     const unsigned rgrid = (unsigned)std::min<uint64_t>((R + 255) / 256, 65536);
     const unsigned lgrid = (unsigned)((R + kScanBlock - 1) / kScanBlock);
-    hipLaunchKernelGGL(k_records, dim3(rgrid), dim3(256), 0, st, D, lo, B.nl, B.meta, B.len, B.ids, B.ids_cap, B.meta);
+    hipLaunchKernelGGL(k_records, dim3(rgrid), dim3(256), 0, st, D, t0, lo, B.nl, B.meta, B.len, B.ids, B.ids_cap, B.meta);
     hipLaunchKernelGGL(k_scan_sums, dim3(lgrid), dim3(256), 0, st, B.len, R, B.bsum);
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, B.bsum, (uint64_t)lgrid, B.tot);
     hipLaunchKernelGGL(k_scan_apply, dim3(lgrid), dim3(256), 0, st, B.len, R, B.bsum, B.rec_off);
@@ -655,7 +655,8 @@ pa_status fastq_prefetch_start(const char *path, int device, int threads, uint64
     pf->device = device;
     pf->path = path;
     pf->size = (uint64_t)sb.st_size;
-    pf->window = std::max<uint64_t>(window, 1 << 16) & ~(uint64_t)(kTile - 1);
+    // (<= 2 GiB: line-feed offsets are kept relative to a window's first tile as uint32)
+    pf->window = std::min<uint64_t>(std::max<uint64_t>(window, 1 << 16), 1ull << 31) & ~(uint64_t)(kTile - 1);
     pf->threads = std::max(1, threads);
     pf->th = std::thread(prefetch_run, pf);
     *out = pf;
@@ -767,6 +768,11 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
                 return PA_EIO;
             }
             gzbuffer(src.gz, 1 << 20);
+            if (gzdirect(src.gz)) {  // not gzip data: the exact path raises the reference's BadGzipFile
+                gzclose(src.gz);
+                set_error(std::string("not a gzip file: ") + path);
+                return PA_ENOTCANON;
+            }
         } else {
             src.fd = open(path, O_RDONLY);
             struct stat sb;
@@ -778,7 +784,7 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
             src.size = (uint64_t)sb.st_size;
         }
     }
-    const uint64_t W = std::max<uint64_t>(window, 1 << 16) & ~(uint64_t)(kTile - 1);
+    const uint64_t W = std::min<uint64_t>(std::max<uint64_t>(window, 1 << 16), 1ull << 31) & ~(uint64_t)(kTile - 1);
     const uint64_t dbytes = kCarryMax + W + 2 * kTile;       // one device text buffer
     const uint64_t est_rec = src.gz ? (1ull << 24) : src.size / 16 + 1024;
 
@@ -836,10 +842,11 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
     tw = now();
     reader.join();
     t_wait_read += ms(tw, now());
-    if (!read_ok) {
+    if (!read_ok) {  // (a corrupt .gz: the exact path raises the reference's error)
         set_error(std::string("read error in ") + path);
+        const bool gz = src.gz != nullptr;
         cleanup();
-        return PA_EIO;
+        return gz ? PA_ENOTCANON : PA_EIO;
     }
     uint64_t carry = 0, records = 0, prev_end = 0;
     int cur = 0;
@@ -881,9 +888,9 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
             tw = now();
             reader.join();
             t_wait_read += ms(tw, now());
-            if (!read_ok) {
+            if (!read_ok) {  // a corrupt .gz: the exact path (Python gzip) raises the reference's error
                 set_error(std::string("read error in ") + path);
-                rc = PA_EIO;
+                rc = src.gz ? PA_ENOTCANON : PA_EIO;
                 break;
             }
             got = got_next;

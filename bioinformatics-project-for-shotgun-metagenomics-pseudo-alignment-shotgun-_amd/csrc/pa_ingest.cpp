@@ -461,6 +461,11 @@ pa_status pa_parse_file(int32_t kind, const char *path, int32_t threads, pa_seqs
             return PA_EIO;
         }
         gzbuffer(f, 1 << 20);
+        if (gzdirect(f)) {  // not gzip data: the exact path raises the reference's BadGzipFile
+            gzclose(f);
+            pa::set_error(std::string("not a gzip file: ") + path);
+            return PA_ENOTCANON;
+        }
         vector<uint8_t> buf;
         size_t n = 0;
         buf.resize(64 << 20);

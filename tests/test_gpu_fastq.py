@@ -192,3 +192,60 @@ def test_prefetched_outside_subset_and_gz(ref, tmp_path, monkeypatch):
         f.write(reads_text(gens, 10, seed=18))
     with pytest.raises(N.PaUnsupported):
         N.FastqPrefetch(str(g))
+
+
+@pytest.mark.parametrize("kind", ["plain_text_named_gz", "crc_corrupt_gz", "truncated_gz"])
+def test_bad_gzip_takes_the_reference_error(ref, tmp_path, kind):
+    """A ".fq.gz" that is not gzip data, or a damaged one, gives the exact path's
+    verdict (src/data_file.py:117-128: gzip.open(...).read()), not a libpa error."""
+    gens, r = ref
+    text = reads_text(gens, 400, seed=20).encode()
+    p = tmp_path / "reads.fq.gz"
+    if kind == "plain_text_named_gz":
+        p.write_bytes(text)
+    else:
+        blob = bytearray(gzip.compress(text))
+        if kind == "crc_corrupt_gz":
+            blob[-8] ^= 0xFF  # the CRC-32 of the trailer
+        else:
+            blob = blob[:len(blob) * 2 // 3]
+        p.write_bytes(bytes(blob))
+    with pytest.raises(Exception) as want:
+        FASTAQFile(str(p))
+    with pytest.raises(type(want.value)):
+        PseudoAlignment(r).align_reads_from_file(str(p))
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+def test_file_past_4_gib(ref, tmp_path):
+    """A FASTQ file larger than 2^32 bytes through the device parse (prefetched
+    and windowed): line-feed offsets stay window-relative, so records past 4 GiB
+    parse like the rest.  The file is K copies of one block of records (ids made
+    unique per copy), so its summary is K times the block's, key order equal."""
+    gens, r = ref
+    block_text = reads_text(gens, 4000, seed=21, lens=(150, 100, 176))
+    lines = block_text.split("\n")
+    K = (2 ** 32 + 2 ** 27) // len(block_text) + 1
+    p = tmp_path / "big.fq"
+    with open(p, "w") as f:
+        for j in range(K):
+            out = list(lines)
+            for i in range(0, len(out) - 1, 4):
+                out[i] = "@b" + str(j) + "_" + out[i][1:]
+            f.write("\n".join(out))
+    assert os.path.getsize(p) > 2 ** 32
+    one = tmp_path / "block.fq"
+    one.write_text(block_text)
+    b = PseudoAlignment(r)
+    b.align_reads_from_container(FASTAQFile(str(one)).container)
+    want = b.get_summary()
+    for prefetch in (True, False):
+        a = PseudoAlignment(r)
+        a.align_reads_from_file(str(p), prefetch=N.FastqPrefetch(str(p)) if prefetch else None)
+        assert getattr(a, "_streamed_records", None) == 4000 * K
+        got = a.get_summary()
+        assert list(got["Summary"]) == list(want["Summary"])
+        assert got["Statistics"] == {k: v * K for k, v in want["Statistics"].items()}
+        assert got["Summary"] == {g: {k: v * K for k, v in c.items()} for g, c in want["Summary"].items()}
+    os.unlink(p)
