@@ -242,7 +242,8 @@ __global__ __launch_bounds__(256) void k_quality_masks(const uint8_t *__restrict
         case 4: quality_reads<4>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 5: quality_reads<5>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 6: quality_reads<6>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
-        default: quality_reads<7>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 7: quality_reads<7>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        default: break;  // (unreachable: the launch requires k <= 31)
     }
 }
 
@@ -1021,6 +1022,10 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.queue_hard_count = (unsigned long long *)idx->counters + 3;
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));
             if (a.prm.flags & (F_MRQ | F_MKQ)) {  // the quality filters of every read, up front
+                if (idx->k > 31) {  // (k_quality_masks realigns by k >> 2 <= 7: lane_ok implies k <= 31)
+                    set_error("internal: quality pre-pass for k > 31");
+                    return PA_EINTERNAL;
+                }
                 PA_TRY(ensure_qmask(idx, r->n));
                 KernelTimer kt(idx, st, PA_PROF_QUALITY);
                 hipLaunchKernelGGL(k_quality_masks, dim3((unsigned)std::min<uint64_t>((r->n + 255) / 256, 65536)),

@@ -216,7 +216,8 @@ __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, c
 
 // Word-blocked Bloom filter of the table's single-word keys (the lane
 // kernel's prefilter for the windows it must probe): 2^lg 64-bit words, one
-// word per key (the top lg bits of a 64-bit mix, lg <= 28) and six bits in it
+// word per key (lg <= 34: up to 128 GiB, 64-bit word index; C2 takes lg = 23,
+// C4 / C5 the HBM form up to 1/8 of free memory) and six bits in it
 // (six 6-bit fields of the low 36).  No false negatives: a key whose bits are
 // not all set is not in the table.
 __device__ __forceinline__ uint64_t bloom_mix(uint64_t x) {

@@ -122,15 +122,22 @@ def _prefetch_reads(reads_file: str):
 
 def create_alignment_from_reference(kmer_reference: KmerReference, reads_file: str, m: int, p: int,
                                     min_read_quality, min_kmer_quality, max_genomes,
-                                    prefetch=None) -> PseudoAlignment:
+                                    prefetch=None, per_read: bool = False) -> PseudoAlignment:
     # the FASTQ file goes straight to the device (parsed there, aligned in
     # windows); a file outside that subset of the grammar is parsed the exact
-    # way (FASTAQFile), which also raises the reference's errors
+    # way (FASTAQFile), which also raises the reference's errors.  per_read
+    # (task 'align': the .aln file holds every read's result): the host parse,
+    # whose records the per-read results are made from -- the device parse
+    # would only have to be repeated on the host for them
     FASTAQFile.check_extension(reads_file)
     _stage("reference built")
     alignment = PseudoAlignment(kmer_reference)
-    alignment.align_reads_from_file(reads_file, m, p, min_read_quality, min_kmer_quality, max_genomes,
-                                    prefetch=prefetch)
+    if per_read:
+        alignment.align_reads_from_container(FASTAQFile(reads_file).container, m, p, min_read_quality,
+                                             min_kmer_quality, max_genomes)
+    else:
+        alignment.align_reads_from_file(reads_file, m, p, min_read_quality, min_kmer_quality, max_genomes,
+                                        prefetch=prefetch)
     _stage("reads aligned")
     return alignment
 
@@ -197,15 +204,13 @@ def _run(args: argparse.Namespace) -> None:
         validate_file_writable(args.alignfile, "Alignment output")
         if args.referencefile and args.reads and args.alignfile:
             validate_file_readable(args.referencefile, "Reference database")
-            pf = _prefetch_reads(args.reads)
             ref = _load_reference(args.referencefile)
         else:
             validate_file_readable(args.genomefile, "Genome FASTA")
-            pf = _prefetch_reads(args.reads)
             ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
             if args.referencefile:
                 ref.save(args.referencefile)
-        create_alignment_from_reference(ref, args.reads, *filt, prefetch=pf).save(args.alignfile)
+        create_alignment_from_reference(ref, args.reads, *filt, per_read=True).save(args.alignfile)
     elif args.task == "dumpalign":
         if args.referencefile and args.reads:
             validate_file_readable(args.reads, "FASTQ reads")
