@@ -153,10 +153,13 @@ def kernel_short_name(mangled: str):
     """The kernel's own identifier from its mangled name (the length prefix
     keeps k_align_lane apart from k_align_lane_na), or None."""
     import re
+    # (the digits may run into a preceding name: "_GLOBAL__N_1" + "12k_align_lane")
     for m in re.finditer(r"(\d+)(k_[A-Za-z0-9_]+)", mangled):
-        name = m.group(2)[:int(m.group(1))]
-        if name in ALIGN_KERNELS:
-            return name
+        digits, rest = m.group(1), m.group(2)
+        for i in range(len(digits)):
+            n = int(digits[i:])
+            if n <= len(rest) and rest[:n] in ALIGN_KERNELS:
+                return rest[:n]
     return None
 
 

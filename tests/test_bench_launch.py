@@ -82,3 +82,20 @@ def test_two_ranks_launched_by_bench_equal_one_process():
     assert sum(want["stats"][:4]) == 2 * npg
     res.close()
     index.close()
+
+
+def test_kernel_short_names():
+    """Counter rows are matched to kernels by their own mangled names (the
+    length prefix keeps k_align_lane apart from k_align_lane_na)."""
+    sys.path.insert(0, REPO)
+    import bench
+    names = {
+        "_ZN12_GLOBAL__N_112k_align_laneILb0ELb0ELb0EEEvNS_9AlignArgsE.kd": "k_align_lane",
+        "_ZN12_GLOBAL__N_115k_align_lane_naILb0ELb0ELb0EEEvNS_9AlignArgsE.kd": "k_align_lane_na",
+        "_ZN12_GLOBAL__N_112k_align_fastILi1ELi2ELb1EEEvNS_9AlignArgsE.kd": "k_align_fast",
+        "_ZN12_GLOBAL__N_113k_align_exactILi1EEEvNS_9ExactArgsE.kd": "k_align_exact",
+        "_ZN2pa15k_quality_masksEPKhPKmmilljP15HIP_vector_typeIjLj4EEPh.kd": "k_quality_masks",
+        "_ZN12_GLOBAL__N_110k_nb_buildEPKmPKjmiPKN3pad4SlotILi1EEENS4_7HomeCfgE": None,
+    }
+    for mangled, want in names.items():
+        assert bench.kernel_short_name(mangled) == want, mangled
