@@ -124,8 +124,8 @@ __global__ void k_fill_u64(uint64_t *p, uint64_t n, uint64_t v) {
 // Insert (or find) a key; returns its slot.  Slots only go EMPTY -> key, so a
 // stale plain load can only show EMPTY, which the CAS then corrects.
 template <int NW>
-__device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, uint64_t home,
-                                 unsigned long long *n_kmers, uint32_t *err) {
+__device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, uint64_t home, uint32_t &fresh,
+                                 uint32_t *err) {
     uint64_t pos = home;
     if constexpr (NW == 1) {
         for (uint64_t it = 0; it < cap; it++) {
@@ -134,7 +134,7 @@ __device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, ui
             if (cur == EMPTY) {
                 uint64_t old = atomicCAS((unsigned long long *)&t[pos].key[0], EMPTY, k.w[0]);
                 if (old == EMPTY) {
-                    atomicAdd(n_kmers, 1ull);
+                    fresh++;
                     return pos;
                 }
                 if (old == k.w[0]) return pos;
@@ -157,7 +157,7 @@ __device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, ui
 #pragma unroll
                     for (int j = 1; j < NW; j++) st_agent(&t[pos].key[j], k.w[j]);
                     __hip_atomic_store(&t[pos].key[0], k.w[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    atomicAdd(n_kmers, 1ull);
+                    fresh++;
                     return pos;
                 }
                 continue;  // someone claimed it: look again
@@ -176,39 +176,52 @@ __device__ uint64_t table_insert(Slot<NW> *t, uint64_t cap, const Key<NW> &k, ui
     return ~0ull;
 }
 
-// Pass 1 over one genome: insert windows, count distinct genomes per slot.
+// Build bookkeeping lives in the slot itself until the slots are final
+// (one random line per window instead of four arrays): during pass 1
+//   slot.cls  = ~(last genome + 1)   (0xFFFFFFFF: none yet; atomicMin keeps the latest)
+//   slot.tpos = ~(genomes so far)    (deg, counted down)
+// Genomes are inserted one launch each in FASTA order, so within a launch all
+// windows carry the same g and the thread whose atomicMin lowers cls is the
+// only one to count g for that slot; a singleton's genome is its last one.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    return v;
+}
+
+// Pass 1 over one genome: insert windows, count distinct genomes per slot;
+// new keys are counted per wave (one atomic per wave, not per key).
 template <int NW>
 __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
-                               uint64_t mask0, uint32_t g, Slot<NW> *table, HomeCfg hc, uint32_t *deg,
-                               uint32_t *last_g, uint32_t *first_g, unsigned long long *n_kmers, uint32_t *err,
-                               int tile, int wpt) {
+                               uint64_t mask0, uint32_t g, Slot<NW> *table, HomeCfg hc, unsigned long long *n_kmers,
+                               uint32_t *err, int wpt) {
     const uint64_t cap = hc.cap;
-    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
-    if (w0 >= nwin) return;
-    uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
-    const uint8_t *s = codes + gstart + w0;
-    Key<NW> key;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
+    uint32_t fresh = 0;
+    if (w0 < nwin) {
+        const uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
+        const uint8_t *s = codes + gstart + w0;
+        Key<NW> key;
 #pragma unroll
-    for (int j = 0; j < NW; j++) key.w[j] = 0;
-    int run = 0;
-    for (int i = 0; i < k - 1; i++) {
-        uint32_t c = s[i];
-        run = c > 3 ? 0 : run + 1;
-        key_push(key, c & 3, mask0);
-    }
-    for (uint64_t w = w0; w < w1; w++) {
-        uint32_t c = s[w - w0 + k - 1];
-        run = c > 3 ? 0 : run + 1;
-        key_push(key, c & 3, mask0);
-        if (run < k) continue;  // window contains a non-ACGT base (src/kmer.py:145)
-        uint64_t slot = table_insert<NW>(table, cap, key, home_of(key, key_hash(key), hc), n_kmers, err);
-        if (slot == ~0ull) return;
-        uint32_t old = atomicMax(&last_g[slot], g + 1);
-        if (old < g + 1) {
-            uint32_t d = atomicAdd(&deg[slot], 1u);
-            if (d == 0) first_g[slot] = g;
+        for (int j = 0; j < NW; j++) key.w[j] = 0;
+        int run = 0;
+        for (int i = 0; i < k - 1; i++) {
+            uint32_t c = s[i];
+            run = c > 3 ? 0 : run + 1;
+            key_push(key, c & 3, mask0);
+        }
+        const uint32_t mark = ~(g + 1);
+        for (uint64_t w = w0; w < w1; w++) {
+            uint32_t c = s[w - w0 + k - 1];
+            run = c > 3 ? 0 : run + 1;
+            key_push(key, c & 3, mask0);
+            if (run < k) continue;  // window contains a non-ACGT base (src/kmer.py:145)
+            const uint64_t slot = table_insert<NW>(table, cap, key, home_of(key, key_hash(key), hc), fresh, err);
+            if (slot == ~0ull) break;
+            if (atomicMin(&table[slot].cls, mark) > mark) atomicSub(&table[slot].tpos, 1u);
         }
     }
+    fresh = wave_sum_u32(fresh);
+    if (lane_id() == 0 && fresh) atomicAdd(n_kmers, (unsigned long long)fresh);
 }
 
 // Distinct k-mer estimate (HyperLogLog, 2^16 registers, ~0.4 % error) of one
@@ -248,10 +261,12 @@ __global__ void k_hll(const uint8_t *__restrict__ codes, uint64_t gstart, uint64
 // multi slots and takes its storage with ONE atomic (a bump per wave made
 // ~10^7 same-address atomics on C5 and cost 144 ms on C2), then hands out
 // offsets inside the range by block-wide scans.
+// Singletons -> final slot values (cls = the genome, tpos reset); multi slots
+// -> list storage, cls and tpos reset for pass 2 (tpos then counts the list
+// down again, so it holds ~deg once the lists are full).
 template <int NW>
-__global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t cap, const uint32_t *deg, uint32_t *aux,
-                                                    uint64_t *off, unsigned long long *bump,
-                                                    unsigned long long *n_multi) {
+__global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t cap, uint64_t *off,
+                                                    unsigned long long *bump, unsigned long long *n_multi) {
     __shared__ unsigned long long s_red[2][4];
     __shared__ unsigned long long s_base;
     __shared__ uint32_t s_wave[4];
@@ -259,10 +274,10 @@ __global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t ca
     const uint64_t per = ((cap + gridDim.x - 1) / gridDim.x + 255) & ~255ull;
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(cap, lo + per);
     if (lo >= hi) return;
-    // phase A: this range's list storage and multi slots (deg is 0 at empty slots)
+    // phase A: this range's list storage and multi slots (deg is 0 at empty slots: tpos = ~0)
     unsigned long long tot = 0, nm = 0;
     for (uint64_t s = lo + threadIdx.x; s < hi; s += 256) {
-        const uint32_t d = deg[s];
+        const uint32_t d = ~table[s].tpos;
         if (d >= 2) tot += d, nm++;
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -284,9 +299,10 @@ __global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t ca
         const uint64_t s = b + threadIdx.x;
         uint32_t d = 0;
         if (s < hi && table[s].key[0] != EMPTY) {
-            d = deg[s];
+            d = ~table[s].tpos;
             if (d == 1) {
-                table[s].cls = aux[s];
+                table[s].cls = ~table[s].cls - 1;  // the only genome = the last one
+                table[s].tpos = 0xFFFFFFFFu;
                 d = 0;
             }
         }
@@ -301,18 +317,21 @@ __global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t ca
         }
         if (d >= 2) {
             off[s] = run + before + incl - d;
-            aux[s] = 0;
+            table[s].cls = 0xFFFFFFFFu;
+            table[s].tpos = 0xFFFFFFFFu;
         }
         run += total;
         __syncthreads();  // s_wave is rewritten by the next chunk
     }
 }
 
-// Pass 2 over one genome: append g to the genome list of every multi slot.
+// Pass 2 over one genome: append g to the genome list of every multi slot
+// (singletons already hold their genome, cls < G; multi slots hold ~(last
+// genome + 1) >= 2^32 - 2^20 > G while their lists fill).
 template <int NW>
 __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k,
-                             uint64_t mask0, uint32_t g, const Slot<NW> *table, HomeCfg hc, const uint32_t *deg,
-                             uint32_t *last_g, uint32_t *fill, const uint64_t *off, uint32_t *lists, int wpt) {
+                             uint64_t mask0, uint32_t g, Slot<NW> *table, HomeCfg hc, uint32_t G,
+                             const uint64_t *off, uint32_t *lists, int wpt) {
     const uint64_t cap = hc.cap;
     uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
     if (w0 >= nwin) return;
@@ -327,6 +346,7 @@ __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart,
         run = c > 3 ? 0 : run + 1;
         key_push(key, c & 3, mask0);
     }
+    const uint32_t mark = ~(g + 1);
     for (uint64_t w = w0; w < w1; w++) {
         uint32_t c = s[w - w0 + k - 1];
         run = c > 3 ? 0 : run + 1;
@@ -335,10 +355,9 @@ __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart,
         uint64_t slot;
         uint32_t cls, tpos;
         if (!table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) continue;
-        if (deg[slot] < 2) continue;
-        uint32_t old = atomicMax(&last_g[slot], g + 1);
-        if (old < g + 1) {
-            uint32_t p = atomicAdd(&fill[slot], 1u);
+        if (cls < G) continue;  // a singleton
+        if (atomicMin(&table[slot].cls, mark) > mark) {
+            const uint32_t p = ~atomicSub(&table[slot].tpos, 1u);  // genomes listed before g
             lists[off[slot] + p] = g;
         }
     }
@@ -350,15 +369,16 @@ __device__ __forceinline__ uint64_t list_hash(const uint32_t *l, uint32_t n) {
     return h >> 1;  // < 2^63: never EMPTY
 }
 
+// (after pass 2: a multi slot has cls >= G and tpos = ~deg)
 template <int NW>
-__global__ void k_class_insert(const Slot<NW> *table, uint64_t cap, const uint32_t *deg, const uint64_t *off,
+__global__ void k_class_insert(const Slot<NW> *table, uint64_t cap, uint32_t G, const uint64_t *off,
                                const uint32_t *lists, uint64_t *cs_key, uint64_t *cs_rep, uint64_t cs_cap,
                                uint32_t *err) {
     uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; s < cap; s += stride) {
-        if (table[s].key[0] == EMPTY || deg[s] < 2) continue;
-        uint64_t h = list_hash(lists + off[s], deg[s]);
+        if (table[s].key[0] == EMPTY || table[s].cls < G) continue;
+        uint64_t h = list_hash(lists + off[s], ~table[s].tpos);
         uint64_t pos = home_slot(fmix64(h), cs_cap);
         uint64_t it = 0;
         for (; it < cs_cap; it++) {
@@ -374,8 +394,9 @@ __global__ void k_class_insert(const Slot<NW> *table, uint64_t cap, const uint32
     }
 }
 
+template <int NW>
 __global__ void k_class_number(const uint64_t *cs_key, const uint64_t *cs_rep, uint32_t *cs_id, uint64_t cs_cap,
-                               const uint32_t *deg, uint32_t *class_size, uint64_t *class_off, uint64_t *rep_of,
+                               const Slot<NW> *table, uint32_t *class_size, uint64_t *class_off, uint64_t *rep_of,
                                unsigned long long *n_cls, unsigned long long *bump) {
     uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -383,7 +404,7 @@ __global__ void k_class_number(const uint64_t *cs_key, const uint64_t *cs_rep, u
         if (cs_key[e] == EMPTY) continue;
         uint64_t id = atomicAdd(n_cls, 1ull);
         uint64_t rep = cs_rep[e];
-        uint32_t d = deg[rep];
+        uint32_t d = ~table[rep].tpos;
         cs_id[e] = (uint32_t)id;
         class_size[id] = d;
         class_off[id] = atomicAdd(bump, (unsigned long long)d + 1);  // record = [size, genomes...]
@@ -415,27 +436,31 @@ __global__ void k_class_masks(uint64_t n_cls, const uint64_t *class_off, const u
     }
 }
 
+// (every thread reads and writes its own slot only; the representative's
+// size comes from class_size, its list from `lists`)
 template <int NW>
-__global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint32_t *deg, const uint64_t *off,
-                               const uint32_t *lists, const uint64_t *cs_key, const uint64_t *cs_rep,
-                               const uint32_t *cs_id, uint64_t cs_cap, const uint64_t *class_off,
-                               uint32_t n_genomes, uint32_t *err) {
+__global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint64_t *off, const uint32_t *lists,
+                               const uint64_t *cs_key, const uint64_t *cs_rep, const uint32_t *cs_id, uint64_t cs_cap,
+                               const uint32_t *class_size, const uint64_t *class_off, uint32_t n_genomes,
+                               uint32_t *err) {
     uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; s < cap; s += stride) {
-        if (table[s].key[0] == EMPTY || deg[s] < 2) continue;
-        uint32_t d = deg[s];
+        if (table[s].key[0] == EMPTY || table[s].cls < n_genomes) continue;
+        const uint32_t d = ~table[s].tpos;
         const uint32_t *l = lists + off[s];
         uint64_t h = list_hash(l, d);
         uint64_t pos = home_slot(fmix64(h), cs_cap);
         while (cs_key[pos] != h) pos = (pos + 1 == cs_cap) ? 0 : pos + 1;
         uint64_t rep = cs_rep[pos];
-        bool same = deg[rep] == d;
+        const uint32_t id = cs_id[pos];
+        bool same = class_size[id] == d;
         const uint32_t *rl = lists + off[rep];
         for (uint32_t i = 0; same && i < d; i++) same = (rl[i] == l[i]);
         if (!same) atomicOr(err, 2u);  // 63-bit list-hash collision: refuse, never merge
         // a multi-genome class id is G + the word offset of its [size, genomes...] record
-        table[s].cls = n_genomes + (uint32_t)class_off[cs_id[pos]];
+        table[s].cls = n_genomes + (uint32_t)class_off[id];
+        table[s].tpos = 0xFFFFFFFFu;  // (the first occurrence, set by the tiles)
     }
 }
 
@@ -821,12 +846,12 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
     const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
     const uint64_t cap = idx->cap;
     Slot<NW> *table = (Slot<NW> *)idx->table;
-    uint32_t *deg = nullptr, *last_g = nullptr, *aux = nullptr, *lists = nullptr, *cs_id = nullptr, *err = nullptr;
+    uint32_t *lists = nullptr, *cs_id = nullptr, *err = nullptr;
     uint64_t *off = nullptr, *cs_key = nullptr, *cs_rep = nullptr, *rep_of = nullptr;
     unsigned long long *cnt = nullptr;  // [0] n_kmers [1] bump [2] n_multi [3] n_cls [4] bump2
     pa_status rc = PA_OK;
     auto cleanup = [&]() {
-        hipFree(deg); hipFree(last_g); hipFree(aux); hipFree(off); hipFree(lists);
+        hipFree(off); hipFree(lists);
         hipFree(cs_key); hipFree(cs_rep); hipFree(cs_id); hipFree(rep_of); hipFree(cnt); hipFree(err);
     };
 #define B_HIP(call)                                                                                 \
@@ -838,14 +863,9 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             return e_ == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;                              \
         }                                                                                           \
     } while (0)
-    B_HIP(hipMalloc(&deg, cap * 4));
-    B_HIP(hipMalloc(&last_g, cap * 4));
-    B_HIP(hipMalloc(&aux, cap * 4));
     B_HIP(hipMalloc(&off, cap * 8));
     B_HIP(hipMalloc(&cnt, 8 * 8));
     B_HIP(hipMalloc(&err, 4));
-    B_HIP(hipMemsetAsync(deg, 0, cap * 4, st));
-    B_HIP(hipMemsetAsync(last_g, 0, cap * 4, st));
     B_HIP(hipMemsetAsync(cnt, 0, 8 * 8, st));
     B_HIP(hipMemsetAsync(err, 0, 4, st));
     // pass 1
@@ -854,12 +874,11 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         if (k <= 0 || (uint64_t)k > len) continue;
         uint64_t nwin = len - k + 1;
         hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
-                           idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, deg, last_g, aux, cnt + 0,
-                           err, idx->tile_n > 0 ? 1 : 0, wpt);
+                           idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, cnt + 0, err, wpt);
     }
     B_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_build_prep<NW>, dim3(grid_for(cap, kBlock) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0,
-                       st, table, cap, deg, aux, off, cnt + 1, cnt + 2);
+                       st, table, cap, off, cnt + 1, cnt + 2);
     B_HIP(hipGetLastError());
     unsigned long long h_cnt[8];
     uint32_t h_err = 0;
@@ -876,14 +895,13 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
     idx->n_multi = 0;
     if (n_multi > 0) {
         B_HIP(hipMalloc(&lists, list_total * 4));
-        B_HIP(hipMemsetAsync(last_g, 0, cap * 4, st));
         for (uint32_t g = 0; g < G; g++) {
             uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
             if ((uint64_t)k > len) continue;
             uint64_t nwin = len - k + 1;
             hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
-                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, deg, last_g, aux,
-                               off, lists, wpt);
+                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, G, off, lists,
+                               wpt);
         }
         B_HIP(hipGetLastError());
         // distinct genome sets: a hash over the multi slots' genome lists.  A
@@ -898,7 +916,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             B_HIP(hipMalloc(&cs_rep, cs_cap * 8));
             hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0,
                                st, cs_key, cs_cap, EMPTY);
-            hipLaunchKernelGGL(k_class_insert<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists,
+            hipLaunchKernelGGL(k_class_insert<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, G, off, lists,
                                cs_key, cs_rep, cs_cap, err);
             B_HIP(hipGetLastError());
             B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
@@ -921,9 +939,9 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         B_HIP(hipMalloc(&idx->class_size, max_cls * 4));
         B_HIP(hipMalloc(&idx->class_off, max_cls * 8));
         B_HIP(hipMalloc(&rep_of, max_cls * 8));
-        hipLaunchKernelGGL(k_class_number, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0,
-                           st, cs_key, cs_rep, cs_id, cs_cap, deg, idx->class_size, idx->class_off, rep_of, cnt + 3,
-                           cnt + 4);
+        hipLaunchKernelGGL(k_class_number<NW>, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock),
+                           0, st, cs_key, cs_rep, cs_id, cs_cap, (const Slot<NW> *)table, idx->class_size,
+                           idx->class_off, rep_of, cnt + 3, cnt + 4);
         B_HIP(hipGetLastError());
         B_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
         B_HIP(hipStreamSynchronize(st));
@@ -941,8 +959,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_class_masks, dim3((unsigned)std::min<uint64_t>((n_cls + kBlock - 1) / kBlock, 4096)),
                                dim3(kBlock), 0, st, n_cls, idx->class_off, idx->class_genomes, idx->class_mask);
         }
-        hipLaunchKernelGGL(k_class_assign<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, deg, off, lists, cs_key,
-                           cs_rep, cs_id, cs_cap, idx->class_off, G, err);
+        hipLaunchKernelGGL(k_class_assign<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, off, lists, cs_key,
+                           cs_rep, cs_id, cs_cap, idx->class_size, idx->class_off, G, err);
         B_HIP(hipGetLastError());
         B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
         B_HIP(hipStreamSynchronize(st));
@@ -999,7 +1017,7 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
             uint32_t bb_lg = 6;
             const char *nbb = std::getenv("PA_NB_BLOOM");
             if (!(nbb && nbb[0] == '0') && idx->n_kmers > 0) {
-                while (bb_lg < 36 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;
+                while (bb_lg < 33 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;  // (bloom_block: lg <= 33)
                 size_t fb = 0, tb = 0;
                 if (hipMemGetInfo(&fb, &tb) != hipSuccess) fb = 0;
                 while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
@@ -1102,7 +1120,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 const char *bm = std::getenv("PA_BLOOM_MB"), *bh = std::getenv("PA_BLOOM_HBM");
                 const uint64_t cap_b = idx->force_large ? 0ull : (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 64ull) << 20;
                 uint32_t lg16 = 6;  // 16 bits per key
-                while (lg16 < 34 && (1ull << lg16) * 64 < idx->n_kmers * 16) lg16++;
+                while (lg16 < 33 && (1ull << lg16) * 64 < idx->n_kmers * 16) lg16++;  // (bloom_block: lg <= 33)
                 uint32_t lg = lg16;
                 while (lg > 6 && (1ull << lg) * 8 > cap_b) lg--;
                 bool ok = cap_b > 0 && idx->n_kmers > 0 && (1ull << lg) * 64 >= idx->n_kmers * 8 && (1ull << lg) * 8 <= cap_b;
@@ -1294,8 +1312,10 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     // 4), else 1/2 of the windows if table + build scratch fit; a reference
     // too large for either is sized on its distinct k-mers (HyperLogLog
     // estimate + 3 %): 4, 2 or 1.43 slots per distinct k-mer, the largest that
-    // fits.  The build needs 20 B of scratch per slot and at most 4 B per
-    // genome window for the genome lists.
+    // fits.  The build needs 8 B of scratch per slot (list offsets; the rest
+    // of its bookkeeping lives in the slots) and at most 4 B per genome window
+    // for the genome lists; the sizing still counts 20 B per slot, which
+    // leaves the align-side view (tiles, neighbour bits) its room.
     const int sb = slot_bytes(idx->nw);
     const uint64_t per_slot = (uint64_t)sb + 20;
     size_t free_b = 0, total_b = 0;

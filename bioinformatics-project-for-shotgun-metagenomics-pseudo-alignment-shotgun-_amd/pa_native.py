@@ -313,6 +313,10 @@ def parse_text(kind: int, text, threads: Optional[int] = None, universal_newline
 
 def concat(chunks: Sequence) -> Tuple[np.ndarray, np.ndarray]:
     """Concatenate str/bytes/uint8 chunks into (uint8 array, uint64 CSR offsets)."""
+    if chunks and all(isinstance(c, np.ndarray) and c.dtype == np.uint8 and c.ndim == 1 for c in chunks):
+        off = np.zeros(len(chunks) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([c.size for c in chunks], dtype=np.uint64)
+        return np.concatenate(chunks), off  # (one copy: multi-Gbp references, BASELINE config 5)
     bs = [c.encode() if isinstance(c, str) else (c.tobytes() if isinstance(c, np.ndarray) else bytes(c))
           for c in chunks]
     off = np.zeros(len(bs) + 1, dtype=np.uint64)
