@@ -214,12 +214,11 @@ __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, c
     return found;
 }
 
-// Word-blocked Bloom filter of the table's single-word keys (the lane
-// kernel's prefilter for the windows it must probe): 2^lg 64-bit words, one
-// word per key (lg <= 34: up to 128 GiB, 64-bit word index; C2 takes lg = 23,
-// C4 / C5 the HBM form up to 1/8 of free memory) and six bits in it
-// (six 6-bit fields of the low 36).  No false negatives: a key whose bits are
-// not all set is not in the table.
+// Bloom filter of the table's single-word keys (the lane kernels' prefilter
+// for the windows they must look up): 2^lg 64-bit words (lg <= 33: up to
+// 64 GiB; C2 takes lg = 23, C4 / C5 the HBM form up to 1/8 of free memory),
+// one word per key and six bits in it (six 6-bit fields of the key's mix).
+// No false negatives: a key whose bits are not all set is not in the table.
 __device__ __forceinline__ uint64_t bloom_mix(uint64_t x) {
     x ^= 0x9E3779B97F4A7C15ull;
     x ^= x >> 33;
@@ -229,26 +228,16 @@ __device__ __forceinline__ uint64_t bloom_mix(uint64_t x) {
     x ^= x >> 33;
     return x;
 }
-// The key's mix (bits 0..35: the six fields, bits 61..63: the word within its
-// line) and the line's mix of a minimizer hash.  One xorshift-multiply round
-// (splitmix-style: the high key bits folded in first, the fields taken from the
-// product's high bits, which depend on every key bit) and a 32 x 64 Fibonacci
-// multiply for the line (the minimum of 17 hashes is small; the product's top
-// bits spread it) -- about half the multiplies of two fmix64 rounds, for every
-// Bloom query of the align kernels and every key of the build.
+// The key's mix (bits 0..35: the six fields, bit 63: the word within its
+// block): one xorshift-multiply round (splitmix-style: the high key bits
+// folded in first, the fields taken from the product's high bits, which
+// depend on every key bit).
 __device__ __forceinline__ uint64_t bloom_key_mix(uint64_t key) {
 #ifdef PA_BLOOM_MIX_FULL
     return bloom_mix(key);
 #else
     const uint64_t h = (key ^ (key >> 31) ^ 0x9E3779B97F4A7C15ull) * 0xff51afd7ed558ccdull;
-    return ((h >> 25) & ((1ull << 36) - 1)) | (h & (7ull << 61));
-#endif
-}
-__device__ __forceinline__ uint64_t bloom_line_mix(uint32_t best) {
-#ifdef PA_BLOOM_MIX_FULL
-    return bloom_mix(best);
-#else
-    return (uint64_t)best * 0x9E3779B97F4A7C15ull;
+    return ((h >> 25) & ((1ull << 36) - 1)) | (h & (3ull << 62));
 #endif
 }
 __device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
@@ -258,24 +247,56 @@ __device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
     return m;
 }
 
-// The Bloom word of a k-mer (k <= 31) and its bits: the 64-B line is chosen by
-// the k-mer's minimizer (15-mers, hashed) -- windows of one read that share it,
-// most neighbours, read the same line (+1 % on C2, C3) -- the word within the
-// line and the bits by the k-mer's own mix.
-__device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uint64_t &w, uint64_t &m) {
-    const uint64_t h = bloom_key_mix(key);
-    m = bloom_bits(h);
+// Minimizer-blocked layout: the filter's words group into BLOCKS of
+// kBloomBW words (16 or 32 B); the block of a k-mer (k <= 31) is chosen by its
+// minimizer -- the 15-mer (the whole k-mer below 15) of smallest order among
+// its k - 14 -- so that the windows of a read that share a minimizer (runs of
+// ~9 on random sequence) share one block, which k_align_lane_na loads once per
+// run; the word within the block (the top bits of the key's mix) and the six
+// bits by the key's own mix.  The minimizer order is two full-rate ops on the
+// 15-mer (a 24-bit multiply, no 32-bit one), the block the top bits of one
+// multiply of the minimum.
+#ifndef PA_BLOOM_BW
+#define PA_BLOOM_BW 2
+#endif
+constexpr int kBloomBW = PA_BLOOM_BW;  // 64-bit words per block
+constexpr int kBloomLgBW = kBloomBW == 4 ? 2 : 1;
+static_assert(kBloomBW == 2 || kBloomBW == 4, "Bloom blocks of 16 or 32 B");
+struct BloomBlock {  // (v1 unused for 16-B blocks)
+    uint4 v0, v1;
+};
+__device__ __forceinline__ uint32_t mm_order(uint32_t x) {
+    return __umul24(x ^ (x >> 15), 0xB5297Bu) ^ (x >> 9);
+}
+__device__ __forceinline__ uint64_t bloom_block(uint32_t mn, uint32_t lg) {  // (lg - kBloomLgBW bits; lg <= 33)
+    return (uint64_t)((mn * 0x9E3779B1u) >> (32 + kBloomLgBW - lg));
+}
+__device__ __forceinline__ uint32_t key_minimizer(uint64_t key, int k) {
     const int mm = k < 15 ? k : 15;
     const uint64_t mmask = (1ull << (2 * mm)) - 1;
     uint32_t best = ~0u;
-    for (int i = 0; i + mm <= k; i++) {
-        const uint32_t x = (uint32_t)((key >> (2 * i)) & mmask);
-        uint32_t y = x * 0x9E3779B1u;  // (odd multiplier: a bijection on 32 bits)
-        y ^= y >> 15;
-        best = y < best ? y : best;
+    for (int i = 0; i + mm <= k; i++) best = min(best, mm_order((uint32_t)((key >> (2 * i)) & mmask)));
+    return best;
+}
+// The Bloom word of a key and its six bits.
+__device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uint64_t &w, uint64_t &m) {
+    const uint64_t h = bloom_key_mix(key);
+    m = bloom_bits(h);
+    w = (bloom_block(key_minimizer(key, k), lg) << kBloomLgBW) | (h >> (64 - kBloomLgBW));
+}
+// A key's test against its (loaded) block.
+__device__ __forceinline__ bool bloom_block_has(const BloomBlock &b, uint64_t h) {
+    const uint32_t wi = (uint32_t)(h >> (64 - kBloomLgBW));
+    uint32_t lo = b.v0.x, hi = b.v0.y;
+    lo = wi == 1 ? b.v0.z : lo;
+    hi = wi == 1 ? b.v0.w : hi;
+    if (kBloomBW == 4) {
+        lo = wi == 2 ? b.v1.x : (wi == 3 ? b.v1.z : lo);
+        hi = wi == 2 ? b.v1.y : (wi == 3 ? b.v1.w : hi);
     }
-    const uint64_t line = bloom_line_mix(best) >> (64 - (lg - 3));
-    w = (line << 3) | (h >> 61);
+    const uint64_t wv = ((uint64_t)hi << 32) | lo;
+    const uint64_t bm = bloom_bits(h);
+    return (wv & bm) == bm;
 }
 
 // ---- wavefront (64-lane) helpers ------------------------------------------

@@ -48,6 +48,7 @@
 #include <vector>
 
 #include "pa_device.h"
+#include "pa_gz.h"
 #include "pa_internal.h"
 
 using namespace pad;
@@ -299,9 +300,9 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *D, uint64_t t0, 
     if (lane_id() == 0 && q_low) atomicMax(&meta_out->q_low, (unsigned long long)q_low);
 }
 
-struct Source {  // plain file (positional reads on host threads) or gzip stream
+struct Source {  // plain file (positional reads on host threads) or gzip (pa_gz.cpp: BGZF on all threads)
     int fd = -1;
-    gzFile gz = nullptr;
+    pa::Gz *gz = nullptr;
     uint64_t size = 0, pos = 0;
     bool eof = false;
     int threads = 8;
@@ -309,19 +310,7 @@ struct Source {  // plain file (positional reads on host threads) or gzip stream
     // Read up to n bytes into dst; returns the count, sets eof at the end.
     bool read(uint8_t *dst, uint64_t n, uint64_t &got) {
         got = 0;
-        if (gz) {
-            while (got < n) {
-                const int r = gzread(gz, dst + got, (unsigned)std::min<uint64_t>(n - got, 1u << 30));
-                if (r < 0) return false;
-                if (r == 0) {
-                    eof = true;
-                    break;
-                }
-                got += (uint64_t)r;
-            }
-            if (!eof && gzeof(gz)) eof = true;
-            return true;
-        }
+        if (gz) return pa::gz_read(gz, dst, n, &got, &eof) == PA_OK;
         const uint64_t want = std::min<uint64_t>(n, size - pos);
         const int nt = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, want >> 22));
         std::vector<std::thread> th;
@@ -762,17 +751,7 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         const size_t pl = strlen(path);
         const bool gz = pl >= 3 && strcmp(path + pl - 3, ".gz") == 0;
         if (gz) {
-            src.gz = gzopen(path, "rb");
-            if (!src.gz) {
-                set_error(std::string("cannot open ") + path);
-                return PA_EIO;
-            }
-            gzbuffer(src.gz, 1 << 20);
-            if (gzdirect(src.gz)) {  // not gzip data: the exact path raises the reference's BadGzipFile
-                gzclose(src.gz);
-                set_error(std::string("not a gzip file: ") + path);
-                return PA_ENOTCANON;
-            }
+            PA_TRY(pa::gz_open(path, src.threads, &src.gz));  // (not gzip data: PA_ENOTCANON, the exact path)
         } else {
             src.fd = open(path, O_RDONLY);
             struct stat sb;
@@ -786,7 +765,8 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
     }
     const uint64_t W = std::min<uint64_t>(std::max<uint64_t>(window, 1 << 16), 1ull << 31) & ~(uint64_t)(kTile - 1);
     const uint64_t dbytes = kCarryMax + W + 2 * kTile;       // one device text buffer
-    const uint64_t est_rec = src.gz ? (1ull << 24) : src.size / 16 + 1024;
+    const uint64_t est_rec = src.gz ? std::max<uint64_t>(1ull << 24, pa::gz_text_size(src.gz) / 16 + 1024)
+                                    : src.size / 16 + 1024;
 
     uint8_t *H[2] = {nullptr, nullptr}, *D[2] = {nullptr, nullptr};
     ParseBufs B;
@@ -806,7 +786,7 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         }
         B.release();
         if (cs) hipStreamDestroy(cs);
-        if (src.gz) gzclose(src.gz);
+        if (src.gz) pa::gz_close(src.gz);
         if (src.fd >= 0) close(src.fd);
     };
 #define F_HIP(call)                                                                                      \

@@ -1108,7 +1108,10 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             }
             // the Bloom filter of the keys, for the lane kernel's probes of windows
             // off the walk (almost all absent).  In the memory-side cache: 16 bits
-            // per key up to PA_BLOOM_MB (default 64; 0: none), fewer down to 8
+            // per key up to PA_BLOOM_MB (default 128: with minimizer blocks of 16 B
+            // a run of ~9 keys shares one block, so the filter needs the room --
+            // at 64 MB c2rc's k_align_lane_na took 3.78 ms, at 128 MB 3.24; 0: none),
+            // fewer down to 8
             // bits per key.  A reference too large for that gets one in HBM, 16
             // (down to 8) bits per key in at most 1/8 of the free memory
             // (PA_BLOOM_HBM=0: none): the off-walk windows of a read cluster
@@ -1118,7 +1121,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             // The large-reference layout (PA_LAYOUT=large) takes the HBM form.
             {
                 const char *bm = std::getenv("PA_BLOOM_MB"), *bh = std::getenv("PA_BLOOM_HBM");
-                const uint64_t cap_b = idx->force_large ? 0ull : (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 64ull) << 20;
+                const uint64_t cap_b = idx->force_large ? 0ull : (bm ? (uint64_t)std::strtoull(bm, nullptr, 10) : 128ull) << 20;
                 uint32_t lg16 = 6;  // 16 bits per key
                 while (lg16 < 33 && (1ull << lg16) * 64 < idx->n_kmers * 16) lg16++;  // (bloom_block: lg <= 33)
                 uint32_t lg = lg16;

@@ -49,6 +49,7 @@
 #include <thread>
 #include <vector>
 
+#include "pa_gz.h"
 #include "pa_internal.h"
 
 namespace {
@@ -454,33 +455,26 @@ pa_status pa_parse_file(int32_t kind, const char *path, int32_t threads, pa_seqs
     }
     const size_t pl = strlen(path);
     const bool gz = pl >= 3 && strcmp(path + pl - 3, ".gz") == 0;
-    if (gz) {
-        gzFile f = gzopen(path, "rb");
-        if (!f) {
-            pa::set_error(std::string("cannot open ") + path);
-            return PA_EIO;
-        }
-        gzbuffer(f, 1 << 20);
-        if (gzdirect(f)) {  // not gzip data: the exact path raises the reference's BadGzipFile
-            gzclose(f);
-            pa::set_error(std::string("not a gzip file: ") + path);
-            return PA_ENOTCANON;
-        }
+    if (gz) {  // (pa_gz.cpp: a BGZF file is inflated on all threads; not gzip data: PA_ENOTCANON)
+        pa::Gz *f = nullptr;
+        const pa_status os = pa::gz_open(path, threads, &f);
+        if (os != PA_OK) return os;
         vector<uint8_t> buf;
         size_t n = 0;
-        buf.resize(64 << 20);
-        for (;;) {
+        buf.resize(std::max<uint64_t>(64ull << 20, pa::gz_text_size(f)));
+        bool eof = false;
+        while (!eof) {
             if (buf.size() - n < (16 << 20)) buf.resize(buf.size() * 2);
-            const int got = gzread(f, buf.data() + n, (unsigned)std::min<size_t>(buf.size() - n, 1u << 30));
-            if (got < 0) {
-                gzclose(f);
-                pa::set_error(std::string("gzip read error in ") + path);
-                return PA_EIO;
+            uint64_t got = 0;
+            const pa_status rs = pa::gz_read(f, buf.data() + n, buf.size() - n, &got, &eof);
+            if (rs != PA_OK) {
+                pa::gz_close(f);
+                return rs == PA_ENOTCANON ? PA_EIO : rs;  // (the Python layer takes the exact path on PA_EIO)
             }
-            if (got == 0) break;
             n += (size_t)got;
+            if (got == 0 && !eof) break;
         }
-        gzclose(f);
+        pa::gz_close(f);
         return parse(kind, buf.data(), n, threads, true, out);
     }
     const int fd = open(path, O_RDONLY);

@@ -59,6 +59,9 @@ constexpr uint32_t kLaneMaxMis = PA_LANE_MAXMIS;  // mismatching bases against t
 #ifndef PA_LANE_SEEDS
 #define PA_LANE_SEEDS 5   // seed windows probed per read (first ... last, evenly spread)
 #endif
+#ifndef PA_LANE_RANK_WORDS
+#define PA_LANE_RANK_WORDS 6  // 2-bit words of the read its candidate stretches are ranked on (6: all)
+#endif
 #ifndef PA_LANE_SLOTS
 #define PA_LANE_SLOTS 1   // table slots per probe step in the cooperative passes
 #endif
@@ -210,13 +213,13 @@ __device__ __forceinline__ uint32_t in_read_mask(uint32_t p0, uint32_t shift, ui
 // with PLANES, the flag planes of blocks A >> 6 .. +2.  Three 32-B blocks, a
 // fourth only when the read reaches into it (every load issued before any is
 // used): 1.6 128-B lines per read on average.
-template <bool PLANES>
-__device__ __forceinline__ void lane_blocks(const AlignArgs &a, uint64_t A, uint32_t len, uint64_t (&gw)[kLaneWords + 1],
+template <bool PLANES, int NWD = kLaneWords>
+__device__ __forceinline__ void lane_blocks(const AlignArgs &a, uint64_t A, uint32_t len, uint64_t (&gw)[NWD + 1],
                                             uint64_t (&pa3)[3], uint64_t (&pb3)[3]) {
     const uint64_t *lb = a.tile_lw + 4 * (A >> 6);
     const uint32_t r0 = (uint32_t)(A & 63), o = r0 >> 5, last = r0 + len - 1;
 #pragma unroll
-    for (int i = 0; i <= kLaneWords; i++) {  // only the words holding bases of the read
+    for (int i = 0; i <= NWD; i++) {  // only the words holding bases of the read
         const uint32_t w = o + (uint32_t)i;
         gw[i] = 32 * w <= last ? lb[4 * (w >> 1) + (w & 1)] : 0ull;
     }
@@ -232,15 +235,16 @@ __device__ __forceinline__ void lane_blocks(const AlignArgs &a, uint64_t A, uint
 
 // Mismatching bases between the read (LDS row, len bases) and the genome
 // words gw of the walk blocks from concatenated position A on (lane_blocks).
+template <int NWD = kLaneWords>
 __device__ __forceinline__ uint32_t lane_count_mismatches(const uint64_t *row, uint32_t len, uint64_t A,
-                                                          const uint64_t (&gw)[kLaneWords + 1]) {
+                                                          const uint64_t (&gw)[NWD + 1]) {
     const uint32_t gr = (uint32_t)(2 * A & 63);
     uint32_t n = 0;
     // the read's last word holds len - 32 * qlast bases: one mask (not one per word)
     const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;
     const uint64_t tail = rl >= 32 ? ~0ull : ~0ull << (64 - 2 * rl);
 #pragma unroll
-    for (int i = 0; i < kLaneWords; i++) {
+    for (int i = 0; i < NWD; i++) {
         if (32 * i >= (int)len) break;
         const uint64_t gwi = gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i];
         uint64_t d = row[i] ^ gwi;
@@ -396,6 +400,25 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #pragma unroll
             for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && scls[i] < a.G && stp32[i] != NONE;
             act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
+#ifdef PA_SEED_BLOOM  // (A/B r3: c2rc +0 %, C2 -7 % -- it pushed the kernel's spills from 20 to 44 B/lane)
+            // neither outer seed in the index (a reverse-strand read, an
+            // unindexed organism -- or sequencing errors at both ends): the
+            // middle seeds go through the Bloom filter first, and only those it
+            // lets through cost a table line
+            if (act && !sfound && a.bloom) {
+                uint64_t bw[NSEED], bm[NSEED];
+#pragma unroll
+                for (int i = 0; i < NSEED; i++) {
+                    uint64_t wi = 0;
+                    bm[i] = 0;
+                    if (bit(act, i)) bloom_word(skey[i], k, a.bloom_lg, wi, bm[i]);
+                    bw[i] = a.bloom[wi];  // (outside the branch: the loads issue together; word 0 for the others)
+                }
+#pragma unroll
+                for (int i = 0; i < NSEED; i++)
+                    if ((bw[i] & bm[i]) != bm[i]) act &= ~(1u << i);
+            }
+#endif
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 14) act = 0;  // timing dissection: one seed round
 #endif
@@ -455,15 +478,21 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #ifdef PA_STATS
             atomicAdd(&a.dbg[26], 1ull);
 #endif
-            // the stretches' walk blocks loaded together (one round trip, not one per stretch)
+            // the stretches' walk blocks loaded together (one round trip, not one
+            // per stretch), ranked on the read's first kRankWords x 32 bases:
+            // the choice only steers the walk (any stretch gives the exact
+            // result), and the genome words of three whole reads in flight
+            // made the kernel spill
+            constexpr int NR = PA_LANE_RANK_WORDS;
+            const uint32_t rlen = len < 32u * NR ? len : 32u * NR;
             const bool f0 = lane_fits(a, len, e0), f1 = lane_fits(a, len, e1), f2 = e2 != INT64_MIN && lane_fits(a, len, e2);
-            uint64_t g0[kLaneWords + 1], g1[kLaneWords + 1], g2[kLaneWords + 1], u3[3];
-            lane_blocks<false>(a, f0 ? (uint64_t)e0 : 0, len, g0, u3, u3);
-            lane_blocks<false>(a, f1 ? (uint64_t)e1 : 0, len, g1, u3, u3);
-            lane_blocks<false>(a, f2 ? (uint64_t)e2 : 0, len, g2, u3, u3);
-            const uint32_t m0 = f0 ? lane_count_mismatches(row, len, (uint64_t)e0, g0) : ~0u;
-            const uint32_t m1 = f1 ? lane_count_mismatches(row, len, (uint64_t)e1, g1) : ~0u;
-            const uint32_t m2 = f2 ? lane_count_mismatches(row, len, (uint64_t)e2, g2) : ~0u;
+            uint64_t g0[NR + 1], g1[NR + 1], g2[NR + 1], u3[3];
+            lane_blocks<false, NR>(a, f0 ? (uint64_t)e0 : 0, rlen, g0, u3, u3);
+            lane_blocks<false, NR>(a, f1 ? (uint64_t)e1 : 0, rlen, g1, u3, u3);
+            lane_blocks<false, NR>(a, f2 ? (uint64_t)e2 : 0, rlen, g2, u3, u3);
+            const uint32_t m0 = f0 ? lane_count_mismatches<NR>(row, rlen, (uint64_t)e0, g0) : ~0u;
+            const uint32_t m1 = f1 ? lane_count_mismatches<NR>(row, rlen, (uint64_t)e1, g1) : ~0u;
+            const uint32_t m2 = f2 ? lane_count_mismatches<NR>(row, rlen, (uint64_t)e2, g2) : ~0u;
             uint32_t bj = 0, best = m0;
             if (m1 < best) best = m1, bj = 1;
             if (m2 < best) best = m2, bj = 2;
@@ -577,8 +606,17 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             const uint32_t q = b0 + u < nnb ? b0 + u : b0;  // (a repeated load past the last)
             const uint32_t e = (uint32_t)(epk >> (8 * q)) & 255u, c = (cpk >> (2 * q)) & 3u;
             const uint64_t ni = 3 * ((uint64_t)A + e) + c;
-            nv[u] = a.nb_spec ? ((const uint64_t *)a.tile_nb)[ni] : (uint64_t)((const uint32_t *)a.tile_nb)[ni];
-            ng[u] = MG && a.tile_nbbig ? a.tile_nbbig[ni] : 0u;  // --max-genomes >= 2: present with a set > mg
+            // (one 8-B load either way, 4-B aligned, no branch: the 12-B form's
+            // 32-bit words loaded under a branch waited one by one)
+            uint64_t v8;
+            __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
+            nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
+            if (MG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
+                const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
+                ng[u] = a.tile_nbbig ? gv : 0u;
+            } else {
+                ng[u] = 0u;
+            }
             sf[u] = b0 + u < nnb ? (int32_t)e - k + 1 : 1000;  // bit q of the word <-> window e - k + 1 + q
         }
 #pragma unroll
@@ -748,7 +786,8 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
                 if (64u * i < cnt) {  // (uniform)
                     uint64_t wi;
                     bloom_word(key4[i], a.k, a.bloom_lg, wi, bm[i]);
-                    if (bit(act, i)) bw[i] = a.bloom[wi];
+                    bw[i] = a.bloom[bit(act, i) ? wi : 0ull];  // (no branch around the load: they issue together)
+                    if (!bit(act, i)) bm[i] = 0;
                 }
             }
 #pragma unroll
@@ -1000,50 +1039,67 @@ constexpr size_t lane_lds_bytes(uint32_t G) {
 
 // k_align_lane_na: the reads k_align_lane found no seed for, one per lane.
 // Every window of the read (but those failing --min-kmer-quality) is looked up
-// -- the Bloom filter first, sixteen windows in flight, then the table for the
-// few the filter lets through (src/kmer.py:410-429).  No k-mer found: UNMAPPED;
-// found ones all multi-genome (or above --max-genomes, counted as highly
-// redundant): AMBIGUOUS with an empty list (no specific k-mer,
-// src/kmer.py:458-461); a specific one: the read is queued for the wave kernel.
-// The Bloom filter test of windows w0 .. w0 + NAG - 1 of a packed read (k <=
-// 31; bit j of act: look window w0 + j up), every word load issued before any
-// is tested.  The minimizer of each window is the smallest hashed 15-mer among
-// its k - 14, and neighbouring windows share most of them, so the group's
-// 15-mer hashes are computed once (NAG + k - 15 instead of NAG (k - 14)); the
-// bits of each key are kept as the 36 bits of its mix that bloom_bits reads
-// (32 + 4), not as a 64-bit mask.  Returns the windows the filter lets through.
+// -- the Bloom filter first, then the table for the few it lets through
+// (src/kmer.py:410-429).  No k-mer found: UNMAPPED; found ones all
+// multi-genome (or above --max-genomes, counted as highly redundant):
+// AMBIGUOUS with an empty list (no specific k-mer, src/kmer.py:458-461); a
+// specific one: the read is queued for the wave kernel.
+//
+// The Bloom test of windows w0 .. w0 + NAG - 1 (w0 a multiple of 16, k <= 31;
+// bit j of act: look window w0 + j up).  The group's bases are 128 bits of
+// the lane's LDS row, realigned once (a multiple of 32 bits), so every
+// window's key and every 15-mer is a shift by a constant; the group's 15-mer
+// orders are computed once (NAG + k - 15 of them) and each window's minimizer
+// is a sliding minimum.  A window's block is the minimizer's
+// (pa_device.h), so the windows of one minimizer run read ONE 16-B block,
+// loaded where the run starts (~14 loads per 150-bp read instead of one per
+// window) and carried in `cur` to the next group.  Returns the windows the
+// filter lets through.
 #ifndef PA_NA_GROUP
-#define PA_NA_GROUP 16
+#define PA_NA_GROUP 8
 #endif
-template <int NAG>
-__device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64_t *row, uint32_t w0, uint32_t act) {
-    const int k = a.k, sh = 64 - 2 * k;
+#ifndef PA_NA_PROBES
+#define PA_NA_PROBES 4
+#endif
+__device__ __forceinline__ uint64_t bits128(uint64_t x0, uint64_t x1, int s) {  // (s constant after unrolling)
+    return s == 0 ? x0 : ((x0 << s) | (x1 >> (64 - s)));
+}
+template <int NAG, int KC>  // KC: k known at compile time (31, the benchmark k), else 0
+__device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64_t *row, uint32_t w0, uint32_t act,
+                                                uint32_t &prev_blk, BloomBlock &cur) {
+    static_assert(NAG == 8, "a group's bases are 128 bits from a multiple of 16");
+    const int k = KC ? KC : a.k, sh = 64 - 2 * k;
     const int mm = k < 15 ? k : 15;
     const int S = k - mm + 1;  // 15-mers per window (<= 17)
+    // the group's bases from window w0 on (bits 2 w0 .. 2 w0 + 127 of the row;
+    // 2 w0 is a multiple of 16, the same in every lane of the wave)
+    const uint32_t o = 2 * w0, q = o >> 6, r = o & 63;
+    uint64_t X0 = row[q], X1 = row[q + 1];
+    if (r) {
+        const uint64_t X2 = row[q + 2];
+        X0 = (X0 << r) | (X1 >> (64 - r));
+        X1 = (X1 << r) | (X2 >> (64 - r));
+    }
+    // (every h[p] computed: the ones past the group's last 15-mer are never
+    // selected below, and branching on them cost more than computing them)
     uint32_t h[NAG + 16];
 #pragma unroll
-    for (int p = 0; p < NAG + 16; p++) {
-        uint32_t y = 0xFFFFFFFFu;
-        if (p < NAG + S - 1) {
-            const uint32_t x = (uint32_t)(row_bits(row, 2 * (w0 + p)) >> (64 - 2 * mm));
-            y = x * 0x9E3779B1u;
-            y ^= y >> 15;
-        }
-        h[p] = y;
-    }
-    // each window's minimum: with S >= 16 (k >= 30) every window of the group
-    // holds 15-mer 15, so it is min(suffix minimum from j to 15, prefix minimum
-    // from 15 to j + S - 1) -- 2 NAG + 1 min ops, not NAG (S - 1)
+    for (int p = 0; p < NAG + 16; p++) h[p] = mm_order((uint32_t)(bits128(X0, X1, 2 * p) >> (64 - 2 * mm)));
+    // each window's minimum: with S >= 9 every window j < 8 holds 15-mers 7
+    // and 8 .. j + S - 1, so it is min(suffix minimum from j to 7, prefix
+    // minimum from 7 to j + S - 1)
     uint32_t mn[NAG];
-    if (NAG == 16 && S >= 16) {  // (uniform)
-        uint32_t sfx[16], pfx[17];
-        sfx[15] = pfx[0] = h[15];
+    if (KC && S >= NAG + 1) {  // (k = 31: S = 17; any other k takes the direct minimum below)
+        uint32_t sfx[NAG], pfx[17];
+        sfx[NAG - 1] = pfx[0] = h[NAG - 1];
 #pragma unroll
-        for (int j = 14; j >= 0; j--) sfx[j] = min(h[j], sfx[j + 1]);
+        for (int j = NAG - 2; j >= 0; j--) sfx[j] = min(h[j], sfx[j + 1]);
 #pragma unroll
-        for (int t = 1; t < 17; t++) pfx[t] = min(pfx[t - 1], h[15 + t]);
+        for (int t = 1; t < 17; t++) pfx[t] = min(pfx[t - 1], h[NAG - 1 + t]);
 #pragma unroll
-        for (int j = 0; j < NAG; j++) mn[j] = min(sfx[j], S == 17 ? pfx[j + 1] : pfx[j]);
+        for (int j = 0; j < NAG; j++) {
+            mn[j] = min(sfx[j], pfx[j + S - NAG]);
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < NAG; j++) {
@@ -1054,22 +1110,48 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
             mn[j] = best;
         }
     }
-    uint64_t bw[NAG];
-    uint32_t lo[NAG];
-    uint64_t hi = 0;  // bits 32..35 of each key's mix, 4 per window
+    (void)k;
+    // run starts (a new block) and their loads, all issued before any is used
+    const uint4 *blocks = (const uint4 *)a.bloom;  // (kBloomBW / 2 uint4 per block)
+    uint32_t blk[NAG], news = 0;
 #pragma unroll
     for (int j = 0; j < NAG; j++) {
-        const uint32_t best = mn[j];
-        const uint64_t hk = bloom_key_mix(row_bits(row, 2 * (w0 + j)) >> sh);
-        lo[j] = (uint32_t)hk;
-        hi |= ((hk >> 32) & 15ull) << (4 * j);
-        const uint64_t wi = ((bloom_line_mix(best) >> (64 - (a.bloom_lg - 3))) << 3) | (hk >> 61);
-        bw[j] = bit(act, j) ? a.bloom[wi] : ~0ull;
+        blk[j] = (uint32_t)bloom_block(mn[j], a.bloom_lg);
+        const uint32_t before = j ? blk[j - 1] : prev_blk;
+        news |= (blk[j] != before || (j == 0 && w0 == 0)) ? 1u << j : 0u;
+    }
+    // (no load for a run none of whose windows is looked up; the group's last
+    // run may go on in the next group, which then tests against `cur`)
+    uint32_t need = 0;
+    {
+        bool any = true;
+#pragma unroll
+        for (int j = NAG - 1; j >= 0; j--) {
+            any = any || bit(act, j);
+            if (bit(news, j)) {
+                need |= any ? 1u << j : 0u;
+                any = false;
+            }
+        }
+    }
+    prev_blk = blk[NAG - 1];
+    // (a run without a load has no window to test: it ends inside the group).
+    // Every slot loads -- the unneeded ones block 0, an L1 hit -- so that the
+    // loads issue back to back with one wait (a load under a branch waits
+    // inside it)
+    BloomBlock V[NAG];
+#pragma unroll
+    for (int j = 0; j < NAG; j++) {
+        const uint4 *p = blocks + (uint64_t)(bit(need, j) ? blk[j] : 0u) * (kBloomBW / 2);
+        V[j].v0 = p[0];
+        V[j].v1 = kBloomBW == 4 ? p[1] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < NAG; j++) {
-        const uint64_t bm = bloom_bits(((uint64_t)((hi >> (4 * j)) & 15ull) << 32) | lo[j]);
-        if ((bw[j] & bm) != bm) act &= ~(1u << j);
+        if (bit(need, j)) cur = V[j];
+        if (!bit(act, j)) continue;
+        const uint64_t hk = bloom_key_mix(bits128(X0, X1, 2 * j) >> sh);
+        if (!bloom_block_has(cur, hk)) act &= ~(1u << j);
     }
     return act;
 }
@@ -1106,6 +1188,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
             bool spec = false;
             uint32_t noff = 0, hr = 0;
             constexpr int NAG = PA_NA_GROUP;
+            uint32_t prev_blk = 0;
+            BloomBlock cur{};
 #pragma unroll 1
             for (uint32_t w0 = 0; w0 < W && !spec; w0 += NAG) {
                 uint32_t act = 0;
@@ -1115,19 +1199,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
                     const bool filt = WIN_Q && (((w < 64 ? S.F0 >> w : S.F1 >> (w - 64)) & 1ull) != 0);
                     act |= (w < W && !filt) ? 1u << j : 0u;
                 }
-                if (a.bloom) act = bloom_group<NAG>(a, row, w0, act);  // keys surely absent are not looked up
-                // the rest, eight table probes in flight at a time
+                if (a.bloom)  // keys surely absent are not looked up
+                    act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, prev_blk, cur)
+                                    : bloom_group<NAG, 0>(a, row, w0, act, prev_blk, cur);
+                // the rest (Bloom false positives, the rare present k-mer), four
+                // table probes in flight at a time
+                constexpr int NPB = PA_NA_PROBES;
 #pragma unroll 1
-                for (uint32_t b = 0; b < (uint32_t)NAG && act >> b && !spec; b += 8) {
-                    const uint32_t act8 = (act >> b) & 255u;
+                for (uint32_t b = 0; b < (uint32_t)NAG && act >> b && !spec; b += NPB) {
+                    const uint32_t act8 = (act >> b) & ((1u << NPB) - 1);
                     if (!act8) continue;
-                    uint64_t key[8];
+                    uint64_t key[NPB];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) key[j] = bit(act8, j) ? row_bits(row, 2 * (w0 + b + j)) >> sh : 0ull;
-                    uint32_t f, cl[8], tp[8];
-                    lane_probe<8>(a, key, act8, f, cl, tp);
+                    for (int j = 0; j < NPB; j++) key[j] = bit(act8, j) ? row_bits(row, 2 * (w0 + b + j)) >> sh : 0ull;
+                    uint32_t f, cl[NPB], tp[NPB];
+                    lane_probe<NPB>(a, key, act8, f, cl, tp);
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
+                    for (int j = 0; j < NPB; j++) {
                         if (!bit(f, j)) continue;
                         if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
                         else if (cl[j] >= a.G) noff++;

@@ -151,3 +151,48 @@ def fastq_text(ids: Sequence[str], seq: np.ndarray, qual: np.ndarray) -> str:
     for i, rid in enumerate(ids):
         parts.append(f"@{rid}\n{bytes(seq[i]).decode('ascii')}\n+\n{bytes(qual[i]).decode('ascii')}\n")
     return "".join(parts)
+
+
+def bgzf_bytes(data: bytes, level: int = 6, block: int = 65280) -> bytes:
+    """``data`` as a BGZF file (what ``bgzip`` writes: gzip members of at most
+    64 KiB of text, each recording its compressed size in a "BC" extra field,
+    then the empty end-of-file member).  Python's gzip reads it as any
+    multi-member gzip file; libpa inflates its members in parallel."""
+    import struct
+    import zlib
+    out = []
+
+    def member(chunk: bytes) -> bytes:
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        comp = c.compress(chunk) + c.flush()
+        bsize = 12 + 6 + len(comp) + 8  # header + BC subfield + data + trailer
+        hdr = struct.pack("<4BIBBH", 0x1F, 0x8B, 8, 4, 0, 0, 0xFF, 6) + struct.pack("<BBHH", 66, 67, 2, bsize - 1)
+        return hdr + comp + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk) & 0xFFFFFFFF)
+
+    for i in range(0, len(data), block):
+        out.append(member(data[i:i + block]))
+    out.append(member(b""))
+    return b"".join(out)
+
+
+def write_bgzf(path: str, data: bytes, level: int = 6, workers: int = 1) -> None:
+    """Write ``data`` as BGZF (bgzf_bytes), compressing slices on ``workers``
+    processes for multi-GB files."""
+    if workers <= 1 or len(data) < (64 << 20):
+        with open(path, "wb") as f:
+            f.write(bgzf_bytes(data, level))
+        return
+    from concurrent.futures import ProcessPoolExecutor
+    step = 65280 * 1024
+    pieces = [data[i:i + step] for i in range(0, len(data), step)]
+    with ProcessPoolExecutor(max_workers=workers) as ex, open(path, "wb") as f:
+        parts = list(ex.map(_bgzf_piece, [(p, level) for p in pieces]))
+        for p in parts:
+            f.write(p)
+        f.write(bgzf_bytes(b"", level))
+
+
+def _bgzf_piece(args) -> bytes:
+    data, level = args
+    full = bgzf_bytes(data, level)
+    return full[:-28]  # (without the end-of-file member: 28 bytes)

@@ -329,3 +329,37 @@ def test_reference_written_kdb_and_aln_load(monkeypatch, tmp_path):
         f.write(b"cos\ngetcwd\n(tR.")
     with pytest.raises(pickle.UnpicklingError):
         kmer.KmerReference.load(str(bad))
+
+
+def test_native_parse_file_bgzf(tmp_path):
+    """BGZF ``.fq.gz`` / ``.fa.gz`` (bgzip's multi-member gzip, read by
+    src/data_file.py:117-128 through gzip.open like any gzip file) inflated
+    member-parallel by pa_gz.cpp: the same columns as the plain text; a member
+    with a bad CRC-32, a truncated file or plain text named .gz fall back to the
+    exact path (None), which raises the reference's own error."""
+    import synth
+    from data_file import FASTAQFile
+    gens = synth.family_genomes(3, 200000, seed=9, family_size=3, n_rate=1e-3, n_run=4)
+    seq, qual, _ = synth.sample_reads(gens, 30000, 120, seed=10)
+    fq = synth.fastq_text([f"r{i}" for i in range(len(seq))], seq, qual).encode()
+    fa = synth.fasta_text(["g0", "g1 x", "g2"], gens, width=70).encode()
+    (tmp_path / "r.fq.gz").write_bytes(synth.bgzf_bytes(fq))
+    (tmp_path / "g.fa.gz").write_bytes(synth.bgzf_bytes(fa, level=1))
+    assert gzip.decompress((tmp_path / "r.fq.gz").read_bytes()) == fq
+    for threads in (1, 3, 16):
+        cols = N.parse_file(N.PA_FASTQ, str(tmp_path / "r.fq.gz"), threads=threads)
+        assert cols is not None and len(cols.names) == len(seq)
+        assert np.array_equal(cols.seq, seq.reshape(-1)) and np.array_equal(cols.qual, qual.reshape(-1))
+    cols = N.parse_file(N.PA_FASTA, str(tmp_path / "g.fa.gz"), threads=4)
+    for i, g in enumerate(gens):
+        assert np.array_equal(cols.seq[int(cols.off[i]):int(cols.off[i + 1])], g)
+    # damaged files: the exact path's verdict
+    blob = bytearray(synth.bgzf_bytes(fq))
+    blob[5000] ^= 0x55  # inside a member's deflate data (or its header): inflate or CRC fails
+    (tmp_path / "bad.fq.gz").write_bytes(bytes(blob))
+    (tmp_path / "cut.fq.gz").write_bytes(synth.bgzf_bytes(fq)[:100000])
+    (tmp_path / "txt.fq.gz").write_bytes(fq)
+    for name in ("bad.fq.gz", "cut.fq.gz", "txt.fq.gz"):
+        assert N.parse_file(N.PA_FASTQ, str(tmp_path / name)) is None, name
+        with pytest.raises(Exception):
+            FASTAQFile(str(tmp_path / name))
