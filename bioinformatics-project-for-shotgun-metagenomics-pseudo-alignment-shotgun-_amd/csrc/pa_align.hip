@@ -943,6 +943,10 @@ pa_status effective_params(const pa_reads *r, const DevParams &p, DevParams &out
 pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_t base, pa_result *acc,
                 hipStream_t st) {
     if (r->n == 0) return PA_OK;
+    if (r->n >= 0xFFFFFFFFull) {  // (read indices of a batch are 32-bit in the queues and lane kernels)
+        set_error("pa_align: a batch holds at most 2^32 - 2 reads (split it; read_index_base keeps the order)");
+        return PA_EUNSUPPORTED;
+    }
     PA_TRY(index_note_reads(idx, r->n, st));  // (the neighbour bits, once enough reads came)
     PA_TRY(reserve_queues(idx, r->n));
     DevParams p;

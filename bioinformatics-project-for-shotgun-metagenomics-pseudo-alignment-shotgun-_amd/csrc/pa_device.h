@@ -216,55 +216,46 @@ __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, c
 
 // Bloom filter of the table's single-word keys (the lane kernels' prefilter
 // for the windows they must look up): 2^lg 64-bit words (lg <= 33: up to
-// 64 GiB; C2 takes lg = 23, C4 / C5 the HBM form up to 1/8 of free memory),
-// one word per key and six bits in it (six 6-bit fields of the key's mix).
-// No false negatives: a key whose bits are not all set is not in the table.
-__device__ __forceinline__ uint64_t bloom_mix(uint64_t x) {
-    x ^= 0x9E3779B97F4A7C15ull;
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdull;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ull;
-    x ^= x >> 33;
-    return x;
-}
-// The key's mix (bits 0..35: the six fields, bit 63: the word within its
-// block): one xorshift-multiply round (splitmix-style: the high key bits
-// folded in first, the fields taken from the product's high bits, which
-// depend on every key bit).
-__device__ __forceinline__ uint64_t bloom_key_mix(uint64_t key) {
-#ifdef PA_BLOOM_MIX_FULL
-    return bloom_mix(key);
-#else
-    const uint64_t h = (key ^ (key >> 31) ^ 0x9E3779B97F4A7C15ull) * 0xff51afd7ed558ccdull;
-    return ((h >> 25) & ((1ull << 36) - 1)) | (h & (3ull << 62));
+// 64 GiB; C2 takes lg = 24, C4 / C5 the HBM form up to 1/8 of free memory),
+// one word per key and kBloomK bits in it (kBloomK 6-bit fields of the key's
+// 32-bit mix).  No false negatives: a key whose bits are not all set is not in
+// the table.  Four bits per key: with a run of ~9 keys sharing a block (below)
+// the blocks' load varies so much that more bits per key stopped paying --
+// modelled on C2: 0.98 false positives per 120 windows with 4, 1.04 with 6.
+#ifndef PA_BLOOM_K
+#define PA_BLOOM_K 4
 #endif
+constexpr int kBloomK = PA_BLOOM_K;
+static_assert(kBloomK >= 1 && kBloomK <= 5, "the fields and the block-word bits share 32 bits");
+// The key's mix: bits 0 .. 6 kBloomK - 1 the fields, the top bits the word
+// within its block.  The high word multiplied into the low one, then one
+// xorshift-multiply round (two 32-bit multiplies; the 64-bit mix it replaced
+// took three 64-bit ones.  The high half of a single multiply, tried in r3, is
+// monotone in its input: the fields correlate, c2rc's na kernel 2.63 -> 3.0 ms).
+__device__ __forceinline__ uint32_t bloom_key_mix(uint64_t key) {
+    uint32_t h = ((uint32_t)(key >> 32) * 0x9E3779B1u) ^ (uint32_t)key;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    return h;
 }
-__device__ __forceinline__ uint64_t bloom_bits(uint64_t h) {
+__device__ __forceinline__ uint64_t bloom_bits(uint32_t h) {
     uint64_t m = 0;
 #pragma unroll
-    for (int i = 0; i < 6; i++) m |= 1ull << ((h >> (6 * i)) & 63);
+    for (int i = 0; i < kBloomK; i++) m |= 1ull << ((h >> (6 * i)) & 63);
     return m;
 }
 
-// Minimizer-blocked layout: the filter's words group into BLOCKS of
-// kBloomBW words (16 or 32 B); the block of a k-mer (k <= 31) is chosen by its
+// Minimizer-blocked layout: the filter's words pair up into 16-B BLOCKS; the block of a k-mer (k <= 31) is chosen by its
 // minimizer -- the 15-mer (the whole k-mer below 15) of smallest order among
 // its k - 14 -- so that the windows of a read that share a minimizer (runs of
 // ~9 on random sequence) share one block, which k_align_lane_na loads once per
-// run; the word within the block (the top bits of the key's mix) and the six
-// bits by the key's own mix.  The minimizer order is two full-rate ops on the
+// run; the word within the block (the top bits of the key's mix) and the
+// kBloomK bits by the key's own mix.  The minimizer order is two full-rate ops on the
 // 15-mer (a 24-bit multiply, no 32-bit one), the block the top bits of one
 // multiply of the minimum.
-#ifndef PA_BLOOM_BW
-#define PA_BLOOM_BW 2
-#endif
-constexpr int kBloomBW = PA_BLOOM_BW;  // 64-bit words per block
-constexpr int kBloomLgBW = kBloomBW == 4 ? 2 : 1;
-static_assert(kBloomBW == 2 || kBloomBW == 4, "Bloom blocks of 16 or 32 B");
-struct BloomBlock {  // (v1 unused for 16-B blocks)
-    uint4 v0, v1;
-};
+constexpr int kBloomBW = 2;  // 64-bit words per block (32-B blocks: A/B r3, slower -- they spilled)
+constexpr int kBloomLgBW = 1;
 __device__ __forceinline__ uint32_t mm_order(uint32_t x) {
     return __umul24(x ^ (x >> 15), 0xB5297Bu) ^ (x >> 9);
 }
@@ -278,23 +269,16 @@ __device__ __forceinline__ uint32_t key_minimizer(uint64_t key, int k) {
     for (int i = 0; i + mm <= k; i++) best = min(best, mm_order((uint32_t)((key >> (2 * i)) & mmask)));
     return best;
 }
-// The Bloom word of a key and its six bits.
+// The Bloom word of a key and its bits.
 __device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uint64_t &w, uint64_t &m) {
-    const uint64_t h = bloom_key_mix(key);
+    const uint32_t h = bloom_key_mix(key);
     m = bloom_bits(h);
-    w = (bloom_block(key_minimizer(key, k), lg) << kBloomLgBW) | (h >> (64 - kBloomLgBW));
+    w = (bloom_block(key_minimizer(key, k), lg) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
 }
-// A key's test against its (loaded) block.
-__device__ __forceinline__ bool bloom_block_has(const BloomBlock &b, uint64_t h) {
-    const uint32_t wi = (uint32_t)(h >> (64 - kBloomLgBW));
-    uint32_t lo = b.v0.x, hi = b.v0.y;
-    lo = wi == 1 ? b.v0.z : lo;
-    hi = wi == 1 ? b.v0.w : hi;
-    if (kBloomBW == 4) {
-        lo = wi == 2 ? b.v1.x : (wi == 3 ? b.v1.z : lo);
-        hi = wi == 2 ? b.v1.y : (wi == 3 ? b.v1.w : hi);
-    }
-    const uint64_t wv = ((uint64_t)hi << 32) | lo;
+// A key's test against its (loaded) 16-B block.
+__device__ __forceinline__ bool bloom_block_has(const uint4 &b, uint32_t h) {
+    const bool w1 = (h >> 31) != 0;
+    const uint64_t wv = w1 ? (((uint64_t)b.w << 32) | b.z) : (((uint64_t)b.y << 32) | b.x);
     const uint64_t bm = bloom_bits(h);
     return (wv & bm) == bm;
 }

@@ -371,13 +371,11 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     // ---- seeds: NSEED windows spread evenly from the first to the last; a
     // specific one (its genome is the read's) is preferred as the anchor
     constexpr int NSEED = PA_LANE_SEEDS;
-    uint32_t sw[NSEED];
+    // (seed i's window, recomputed where needed rather than kept in registers)
+    auto sw = [W](int i) { return (uint32_t)(((uint64_t)(W - 1) * (uint32_t)i) / (NSEED - 1)); };
     uint64_t skey[NSEED];
 #pragma unroll
-    for (int i = 0; i < NSEED; i++) {
-        sw[i] = (uint32_t)(((uint64_t)(W - 1) * i) / (NSEED - 1));
-        skey[i] = row_bits(row, 2 * sw[i]) >> sh;
-    }
+    for (int i = 0; i < NSEED; i++) skey[i] = row_bits(row, 2 * sw(i)) >> sh;
 #ifndef PA_LANE_SEED_ROUNDS
 #define PA_LANE_SEED_ROUNDS 2
 #endif
@@ -444,13 +442,13 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     }
     S.atp = stp[0];
     S.acls = scls[0];
-    S.aw = sw[0];
+    S.aw = sw(0);
 #pragma unroll
     for (int i = 1; i < NSEED; i++)
         if (at == i) {
             S.atp = stp[i];
             S.acls = scls[i];
-            S.aw = sw[i];
+            S.aw = sw(i);
         }
     // no specific seed: the first occurrence of a multi-genome seed k-mer may
     // lie in a sibling of the read's genome (a family member), whose variants
@@ -464,14 +462,14 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         uint32_t w1 = 0, c1 = 0, w2 = 0, c2 = 0;
 #pragma unroll
         for (int i = 0; i < NSEED; i++) {
-            const int64_t Ai = (int64_t)stp[i] - sw[i];
+            const int64_t Ai = (int64_t)stp[i] - sw(i);
             if (stp[i] == ~0ull || Ai == e0 || Ai == e1 || e2 != INT64_MIN) continue;
             if (e1 == INT64_MIN) {
                 e1 = Ai;
-                t1 = stp[i], w1 = sw[i], c1 = scls[i];
+                t1 = stp[i], w1 = sw(i), c1 = scls[i];
             } else {
                 e2 = Ai;
-                t2 = stp[i], w2 = sw[i], c2 = scls[i];
+                t2 = stp[i], w2 = sw(i), c2 = scls[i];
             }
         }
         if (e1 != INT64_MIN) {
@@ -863,7 +861,7 @@ void k_align_lane(AlignArgs a) {
     uint64_t chunk = (uint64_t)blockIdx.x * kWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t n_again = 0;  // entries in LW.again_r / again_a
     while (true) {
-        uint64_t r = ~0ull;
+        uint32_t r = ~0u;  // (a batch holds < 2^32 reads: pa::align)
         unsigned long long cd = ~0ull;
         bool again_batch = false;
         if (n_again >= 64 || (chunk >= n_chunks && n_again > 0)) {
@@ -875,8 +873,7 @@ void k_align_lane(AlignArgs a) {
             n_again -= take;
             again_batch = true;
         } else if (chunk < n_chunks) {
-            r = chunk * 64 + lane;
-            if (r >= a.n) r = ~0ull;
+            r = chunk * 64 + lane < a.n ? (uint32_t)(chunk * 64 + lane) : ~0u;
             chunk += wave_stride;
         } else {
             break;
@@ -884,7 +881,7 @@ void k_align_lane(AlignArgs a) {
         LaneRead S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows (and the taken list entries) are done with
-        if (r != ~0ull) lane_prep<NEED_Q, WIN_Q>(a, r, cd, LW.R[lane], S);
+        if (r != ~0u) lane_prep<NEED_Q, WIN_Q>(a, r, cd, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
@@ -977,7 +974,7 @@ void k_align_lane(AlignArgs a) {
             uint64_t qbase = 0;
             if (lane == __builtin_ctzll(hb)) qbase = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
             qbase = shfl64(qbase, __builtin_ctzll(hb));
-            if (hard) a.queue_hard[qbase + lanes_below(hb)] = (uint32_t)r;
+            if (hard) a.queue_hard[qbase + lanes_below(hb)] = r;
         }
         const bool na = S.kind == LANE_NOANCHOR;
         const uint64_t nab = __ballot(na);
@@ -985,13 +982,13 @@ void k_align_lane(AlignArgs a) {
             uint64_t qbase = 0;
             if (lane == __builtin_ctzll(nab)) qbase = atomicAdd(a.queue_na_count, (unsigned long long)__popcll(nab));
             qbase = shfl64(qbase, __builtin_ctzll(nab));
-            if (na) a.queue_na[qbase + lanes_below(nab)] = (uint32_t)r;
+            if (na) a.queue_na[qbase + lanes_below(nab)] = r;
         }
         const bool again = S.kind == LANE_AGAIN;
         const uint64_t ab = __ballot(again);
         if (ab) {  // (at most 63 + 64 entries: a batch is taken once 64 wait)
             if (again) {
-                LW.again_r[n_again + lanes_below(ab)] = (uint32_t)r;
+                LW.again_r[n_again + lanes_below(ab)] = r;
                 LW.again_a[n_again + lanes_below(ab)] = LW.cand[lane];
             }
             n_again += (uint32_t)__popcll(ab);
@@ -1066,13 +1063,13 @@ __device__ __forceinline__ uint64_t bits128(uint64_t x0, uint64_t x1, int s) {  
 }
 template <int NAG, int KC>  // KC: k known at compile time (31, the benchmark k), else 0
 __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64_t *row, uint32_t w0, uint32_t act,
-                                                uint32_t &prev_blk, BloomBlock &cur) {
-    static_assert(NAG == 8, "a group's bases are 128 bits from a multiple of 16");
+                                                uint32_t &prev_blk, uint4 &cur, uint4 (*hc)[kBlock]) {
+    static_assert(NAG == 8 || NAG == 16, "a group's bases are 128 bits from a multiple of 16");
     const int k = KC ? KC : a.k, sh = 64 - 2 * k;
     const int mm = k < 15 ? k : 15;
     const int S = k - mm + 1;  // 15-mers per window (<= 17)
     // the group's bases from window w0 on (bits 2 w0 .. 2 w0 + 127 of the row;
-    // 2 w0 is a multiple of 16, the same in every lane of the wave)
+    // 2 w0 is a multiple of 2 NAG, the same in every lane of the wave)
     const uint32_t o = 2 * w0, q = o >> 6, r = o & 63;
     uint64_t X0 = row[q], X1 = row[q + 1];
     if (r) {
@@ -1081,10 +1078,22 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
         X1 = (X1 << r) | (X2 >> (64 - r));
     }
     // (every h[p] computed: the ones past the group's last 15-mer are never
-    // selected below, and branching on them cost more than computing them)
+    // selected below, and branching on them cost more than computing them).
+    // The previous group's last sixteen are this group's first sixteen (hc),
+    // so a group after the first computes NAG of them, one per window.
+    // (hc: the lane's sixteen in LDS, [i][thread]: no bank conflicts)
     uint32_t h[NAG + 16];
+    const uint32_t t = threadIdx.x;
 #pragma unroll
-    for (int p = 0; p < NAG + 16; p++) h[p] = mm_order((uint32_t)(bits128(X0, X1, 2 * p) >> (64 - 2 * mm)));
+    for (int i = 0; i < 4; i++) {  // (the caller stores a read's first sixteen before its first group)
+        const uint4 v = hc[i][t];
+        h[4 * i] = v.x, h[4 * i + 1] = v.y, h[4 * i + 2] = v.z, h[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int p = 16; p < NAG + 16; p++) h[p] = mm_order((uint32_t)(bits128(X0, X1, 2 * p) >> (64 - 2 * mm)));
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        hc[i][t] = make_uint4(h[NAG + 4 * i], h[NAG + 4 * i + 1], h[NAG + 4 * i + 2], h[NAG + 4 * i + 3]);
     // each window's minimum: with S >= 9 every window j < 8 holds 15-mers 7
     // and 8 .. j + S - 1, so it is min(suffix minimum from j to 7, prefix
     // minimum from 7 to j + S - 1)
@@ -1112,7 +1121,7 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
     }
     (void)k;
     // run starts (a new block) and their loads, all issued before any is used
-    const uint4 *blocks = (const uint4 *)a.bloom;  // (kBloomBW / 2 uint4 per block)
+    const uint4 *blocks = (const uint4 *)a.bloom;
     uint32_t blk[NAG], news = 0;
 #pragma unroll
     for (int j = 0; j < NAG; j++) {
@@ -1138,20 +1147,19 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
     // (a run without a load has no window to test: it ends inside the group).
     // Every slot loads -- the unneeded ones block 0, an L1 hit -- so that the
     // loads issue back to back with one wait (a load under a branch waits
-    // inside it)
-    BloomBlock V[NAG];
+    // inside it); eight at a time (eight blocks in registers, not sixteen)
 #pragma unroll
-    for (int j = 0; j < NAG; j++) {
-        const uint4 *p = blocks + (uint64_t)(bit(need, j) ? blk[j] : 0u) * (kBloomBW / 2);
-        V[j].v0 = p[0];
-        V[j].v1 = kBloomBW == 4 ? p[1] : make_uint4(0, 0, 0, 0);
-    }
+    for (int b0 = 0; b0 < NAG; b0 += 8) {
+        uint4 V[8];
 #pragma unroll
-    for (int j = 0; j < NAG; j++) {
-        if (bit(need, j)) cur = V[j];
-        if (!bit(act, j)) continue;
-        const uint64_t hk = bloom_key_mix(bits128(X0, X1, 2 * j) >> sh);
-        if (!bloom_block_has(cur, hk)) act &= ~(1u << j);
+        for (int j = 0; j < 8; j++) V[j] = blocks[bit(need, b0 + j) ? blk[b0 + j] : 0u];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (bit(need, b0 + j)) cur = V[j];
+            if (!bit(act, b0 + j)) continue;
+            const uint32_t hk = bloom_key_mix(bits128(X0, X1, 2 * (b0 + j)) >> sh);
+            if (!bloom_block_has(cur, hk)) act &= ~(1u << (b0 + j));
+        }
     }
     return act;
 }
@@ -1162,6 +1170,7 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
 template <bool NEED_Q, bool WIN_Q, bool MG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WAVES))) void k_align_lane_na(AlignArgs a) {
     __shared__ uint64_t rows[kBlock][kLaneWords + 1];
+    __shared__ uint4 hcarry[4][kBlock];  // per lane: the last Bloom group's last sixteen 15-mer orders
     const int lane = lane_id();
     const int sh = 64 - 2 * a.k;
     const uint64_t n = *a.queue_na_count;
@@ -1189,7 +1198,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
             uint32_t noff = 0, hr = 0;
             constexpr int NAG = PA_NA_GROUP;
             uint32_t prev_blk = 0;
-            BloomBlock cur{};
+            uint4 cur = make_uint4(0, 0, 0, 0);
+            if (a.bloom) {  // the read's first sixteen 15-mer orders, for its first Bloom group
+                const int mm = a.k < 15 ? a.k : 15;
+                const uint64_t X0 = row[0], X1 = row[1];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    uint32_t v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        v[e] = mm_order((uint32_t)(bits128(X0, X1, 2 * (4 * i + e)) >> (64 - 2 * mm)));
+                    hcarry[i][threadIdx.x] = make_uint4(v[0], v[1], v[2], v[3]);
+                }
+            }
 #pragma unroll 1
             for (uint32_t w0 = 0; w0 < W && !spec; w0 += NAG) {
                 uint32_t act = 0;
@@ -1200,8 +1221,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
                     act |= (w < W && !filt) ? 1u << j : 0u;
                 }
                 if (a.bloom)  // keys surely absent are not looked up
-                    act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, prev_blk, cur)
-                                    : bloom_group<NAG, 0>(a, row, w0, act, prev_blk, cur);
+                    act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, prev_blk, cur, hcarry)
+                                    : bloom_group<NAG, 0>(a, row, w0, act, prev_blk, cur, hcarry);
                 // the rest (Bloom false positives, the rare present k-mer), four
                 // table probes in flight at a time
                 constexpr int NPB = PA_NA_PROBES;

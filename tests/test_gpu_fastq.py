@@ -249,3 +249,19 @@ def test_file_past_4_gib(ref, tmp_path):
         assert got["Statistics"] == {k: v * K for k, v in want["Statistics"].items()}
         assert got["Summary"] == {g: {k: v * K for k, v in c.items()} for g, c in want["Summary"].items()}
     os.unlink(p)
+
+
+@pytest.mark.parametrize("window", [0, 65536, 200000])
+def test_streamed_bgzf_equals_exact(ref, tmp_path, monkeypatch, window):
+    """A BGZF .fq.gz (bgzip's format: src/data_file.py:117-128 reads it as any
+    gzip file) through the device stream, its members inflated on host threads
+    (pa_gz.cpp) window by window: the summary equals the exact path's."""
+    gens, r = ref
+    monkeypatch.setenv("PA_STREAM_WINDOW", str(window))
+    text = reads_text(gens, 4000, seed=23, lens=(150, 100, 31, 176)).encode()
+    p = tmp_path / "reads.fq.gz"
+    p.write_bytes(synth.bgzf_bytes(text, level=1))
+    for kw in (dict(), dict(m=2, p=0, min_read_quality=58, min_kmer_quality=60, max_genomes=2)):
+        a, b = both_ways(r, str(p), **kw)
+        assert getattr(a, "_streamed_records", None) == 4000
+        assert json.dumps(a.get_summary(), indent=4) == json.dumps(b.get_summary(), indent=4)
