@@ -1211,8 +1211,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
                     hcarry[i][threadIdx.x] = make_uint4(v[0], v[1], v[2], v[3]);
                 }
             }
+            // the windows to look up (bit w of pm0 | pm1 << 64): every window
+            // (W <= kLaneMaxW = 128) but those failing --min-kmer-quality, less
+            // those the Bloom filter shows absent
+            uint64_t pm0 = 0, pm1 = 0;
 #pragma unroll 1
-            for (uint32_t w0 = 0; w0 < W && !spec; w0 += NAG) {
+            for (uint32_t w0 = 0; w0 < W; w0 += NAG) {
                 uint32_t act = 0;
 #pragma unroll
                 for (int j = 0; j < NAG; j++) {
@@ -1223,25 +1227,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
                 if (a.bloom)  // keys surely absent are not looked up
                     act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, prev_blk, cur, hcarry)
                                     : bloom_group<NAG, 0>(a, row, w0, act, prev_blk, cur, hcarry);
-                // the rest (Bloom false positives, the rare present k-mer), four
-                // table probes in flight at a time
-                constexpr int NPB = PA_NA_PROBES;
+                if (w0 < 64) pm0 |= (uint64_t)act << w0;
+                else pm1 |= (uint64_t)act << (w0 - 64);
+            }
+            // then the table for the rest (Bloom false positives, the rare
+            // present k-mer): each lane its own next NPB windows, so a wave
+            // probes as often as its lane with the most (~1.3 rounds on c2rc,
+            // where probing per group took ~30: some lane has a false positive
+            // in almost every group)
+            constexpr int NPB = PA_NA_PROBES;
 #pragma unroll 1
-                for (uint32_t b = 0; b < (uint32_t)NAG && act >> b && !spec; b += NPB) {
-                    const uint32_t act8 = (act >> b) & ((1u << NPB) - 1);
-                    if (!act8) continue;
-                    uint64_t key[NPB];
+            while ((pm0 | pm1) && !spec) {
+                uint64_t key[NPB];
+                uint32_t act8 = 0;
 #pragma unroll
-                    for (int j = 0; j < NPB; j++) key[j] = bit(act8, j) ? row_bits(row, 2 * (w0 + b + j)) >> sh : 0ull;
-                    uint32_t f, cl[NPB], tp[NPB];
-                    lane_probe<NPB>(a, key, act8, f, cl, tp);
+                for (int j = 0; j < NPB; j++) {
+                    const bool lo = pm0 != 0;
+                    const uint64_t m = lo ? pm0 : pm1;
+                    const uint32_t w = (lo ? 0u : 64u) + (uint32_t)__builtin_ctzll(m | (1ull << 63));
+                    act8 |= m ? 1u << j : 0u;
+                    key[j] = m ? row_bits(row, 2 * w) >> sh : 0ull;
+                    if (lo) pm0 &= pm0 - 1;
+                    else pm1 &= pm1 - 1;
+                }
+                uint32_t f, cl[NPB], tp[NPB];
+                lane_probe<NPB>(a, key, act8, f, cl, tp);
 #pragma unroll
-                    for (int j = 0; j < NPB; j++) {
-                        if (!bit(f, j)) continue;
-                        if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
-                        else if (cl[j] >= a.G) noff++;
-                        else spec = true;
-                    }
+                for (int j = 0; j < NPB; j++) {
+                    if (!bit(f, j)) continue;
+                    if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
+                    else if (cl[j] >= a.G) noff++;
+                    else spec = true;
                 }
             }
             S.kind = spec ? LANE_HARD : (noff ? LANE_AMB : LANE_UNMAPPED);
