@@ -269,11 +269,27 @@ __device__ __forceinline__ uint32_t key_minimizer(uint64_t key, int k) {
     for (int i = 0; i + mm <= k; i++) best = min(best, mm_order((uint32_t)((key >> (2 * i)) & mmask)));
     return best;
 }
+// The same for a k known at compile time (15 <= K <= 31), unrolled: each
+// 15-mer one funnel shift of the key's two halves (the rolled loop above
+// costs ~14 VALU per 15-mer, this ~6)
+template <int K>
+__device__ __forceinline__ uint32_t key_minimizer_c(uint64_t key) {
+    static_assert(K >= 15 && K <= 31, "15-mers inside a single-word key");
+    const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+    uint32_t best = ~0u;
+#pragma unroll
+    for (int i = 0; i + 15 <= K; i++) {
+        const uint32_t x = (2 * i < 32 ? __builtin_amdgcn_alignbit(hi, lo, 2 * i) : hi >> (2 * i - 32)) & 0x3FFFFFFFu;
+        best = min(best, mm_order(x));
+    }
+    return best;
+}
 // The Bloom word of a key and its bits.
 __device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uint64_t &w, uint64_t &m) {
     const uint32_t h = bloom_key_mix(key);
     m = bloom_bits(h);
-    w = (bloom_block(key_minimizer(key, k), lg) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
+    const uint32_t mn = k == 31 ? key_minimizer_c<31>(key) : key_minimizer(key, k);
+    w = (bloom_block(mn, lg) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
 }
 // A key's test against its (loaded) 16-B block.
 __device__ __forceinline__ bool bloom_block_has(const uint4 &b, uint32_t h) {
