@@ -845,10 +845,10 @@ pa_status result_reset(pa_result *res, hipStream_t st) {
 
 pa_status ensure_workspace(pa_index *idx, size_t bytes) {
     if (idx->ws.bytes >= bytes) return PA_OK;
-    hipFree(idx->ws.ptr);
+    pa::dev_free(idx->ws.ptr);
     idx->ws.ptr = nullptr;
     idx->ws.bytes = 0;
-    hipError_t e = hipMalloc(&idx->ws.ptr, bytes);
+    hipError_t e = pa::dev_malloc(&idx->ws.ptr, bytes);
     if (e != hipSuccess) {
         set_error(std::string("workspace allocation failed: ") + hipGetErrorString(e));
         return PA_ENOMEM;
@@ -859,28 +859,28 @@ pa_status ensure_workspace(pa_index *idx, size_t bytes) {
 
 pa_status ensure_qmask(pa_index *idx, uint64_t n) {
     if (idx->qmask_cap >= n) return PA_OK;
-    hipFree(idx->qmask);
-    hipFree(idx->qdrop);
+    pa::dev_free(idx->qmask);
+    pa::dev_free(idx->qdrop);
     idx->qmask = nullptr;
     idx->qdrop = nullptr;
     idx->qmask_cap = 0;
-    PA_HIP(hipMalloc(&idx->qmask, n * sizeof(uint4)));
-    PA_HIP(hipMalloc(&idx->qdrop, n));
+    PA_HIP(pa::dev_malloc(&idx->qmask, n * sizeof(uint4)));
+    PA_HIP(pa::dev_malloc(&idx->qdrop, n));
     idx->qmask_cap = n;
     return PA_OK;
 }
 
 pa_status reserve_queues(pa_index *idx, uint64_t n) {
     if (idx->queue_cap >= n) return PA_OK;
-    hipFree(idx->queue);
-    hipFree(idx->queue_hard);
-    hipFree(idx->queue_na);
+    pa::dev_free(idx->queue);
+    pa::dev_free(idx->queue_hard);
+    pa::dev_free(idx->queue_na);
     idx->queue = idx->queue_hard = idx->queue_na = nullptr;
     idx->queue_cap = 0;
-    PA_HIP(hipMalloc(&idx->queue, n * 4));
-    PA_HIP(hipMalloc(&idx->queue_hard, n * 4));
-    PA_HIP(hipMalloc(&idx->queue_na, n * 4));
-    if (!idx->na_count) PA_HIP(hipMalloc(&idx->na_count, 8));
+    PA_HIP(pa::dev_malloc(&idx->queue, n * 4));
+    PA_HIP(pa::dev_malloc(&idx->queue_hard, n * 4));
+    PA_HIP(pa::dev_malloc(&idx->queue_na, n * 4));
+    if (!idx->na_count) PA_HIP(pa::dev_malloc(&idx->na_count, 8));
     idx->queue_cap = n;
     return PA_OK;
 }
@@ -911,7 +911,7 @@ pa_status reads_measure(pa_reads *r, hipStream_t st) {
     r->len_min = 0;
     if (!r->qual || r->n == 0) return PA_OK;
     uint32_t *d = nullptr, h[2] = {255, 0xFFFFFFFFu};
-    PA_HIP(hipMalloc(&d, 8));
+    PA_HIP(pa::dev_malloc(&d, 8));
     hipError_t e = hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_reads_qstats, dim3(2048), dim3(256), 0, st, r->qual, r->off, r->n, d);
@@ -919,7 +919,7 @@ pa_status reads_measure(pa_reads *r, hipStream_t st) {
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    hipFree(d);
+    pa::dev_free(d);
     PA_HIP(e);
     r->q_min = (int32_t)h[0];
     r->len_min = (int64_t)h[1];
@@ -986,7 +986,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
         if (lane_ok) {
             if ((a.prm.flags & F_MG) && a.prm.mg >= 2) {
                 const uint64_t n_words = a.tile_n / 64 + 4;
-                if (!idx->tile_big) PA_HIP(hipMalloc(&idx->tile_big, n_words * 8));
+                if (!idx->tile_big) PA_HIP(pa::dev_malloc(&idx->tile_big, n_words * 8));
                 if (idx->tile_big_mg != a.prm.mg) {
                     hipLaunchKernelGGL(k_tile_big, dim3((unsigned)std::min<uint64_t>((n_words + 3) / 4, 1u << 20)),
                                        dim3(256), 0, st, idx->tile_cls, a.tile_n, a.G, idx->class_genomes,
@@ -1001,8 +1001,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
                     const uint64_t nw = 3 * a.tile_n;
                     if (!idx->tile_nbbig) {
                         size_t free_b = 0, total_b = 0;
-                        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && nw * 4 + (8ull << 30) < free_b &&
-                            hipMalloc(&idx->tile_nbbig, nw * 4 + 64) == hipSuccess)
+                        if (pa::dev_mem_info(&free_b, &total_b) == hipSuccess && nw * 4 + (8ull << 30) < free_b &&
+                            pa::dev_malloc(&idx->tile_nbbig, nw * 4 + 64) == hipSuccess)
                             idx->tile_nbbig_mg = -1;
                         else
                             idx->tile_nbbig = nullptr;
@@ -1103,10 +1103,10 @@ pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uin
     uint8_t *d_type = nullptr;
     uint32_t *d_qf = nullptr, *d_hr = nullptr, *d_len = nullptr, *d_lists = nullptr;
     uint64_t *d_off = nullptr;
-    PA_HIP(hipMalloc(&d_type, n));
-    PA_HIP(hipMalloc(&d_qf, n * 4));
-    PA_HIP(hipMalloc(&d_hr, n * 4));
-    PA_HIP(hipMalloc(&d_len, n * 4));
+    PA_HIP(pa::dev_malloc(&d_type, n));
+    PA_HIP(pa::dev_malloc(&d_qf, n * 4));
+    PA_HIP(pa::dev_malloc(&d_hr, n * 4));
+    PA_HIP(pa::dev_malloc(&d_len, n * 4));
     x.type_out = d_type;
     x.qf_out = d_qf;
     x.hr_out = d_hr;
@@ -1131,8 +1131,8 @@ pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uin
             set_error("pa_align_detail: list_cap smaller than the required list length");
             rc = PA_EINVAL;
         } else {
-            PA_HIP(hipMalloc(&d_off, (n + 1) * 8));
-            PA_HIP(hipMalloc(&d_lists, total * 4));
+            PA_HIP(pa::dev_malloc(&d_off, (n + 1) * 8));
+            PA_HIP(pa::dev_malloc(&d_lists, total * 4));
             PA_HIP(hipMemcpyAsync(d_off, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
             x.detail = 2;
             x.list_off = d_off;
@@ -1143,7 +1143,7 @@ pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uin
             PA_HIP(hipStreamSynchronize(st));
         }
     }
-    hipFree(d_type); hipFree(d_qf); hipFree(d_hr); hipFree(d_len); hipFree(d_off); hipFree(d_lists);
+    pa::dev_free(d_type); pa::dev_free(d_qf); pa::dev_free(d_hr); pa::dev_free(d_len); pa::dev_free(d_off); pa::dev_free(d_lists);
     return rc;
 }
 

@@ -78,7 +78,7 @@ pa_status pa_runtime_start(int32_t device) {
     if (g_runtime_starter.th.joinable()) return PA_OK;
     g_runtime_starter.th = std::thread([device] {
         const auto t0 = std::chrono::steady_clock::now();
-        if (hipSetDevice(device) == hipSuccess && hipFree(nullptr) == hipSuccess) {
+        if (hipSetDevice(device) == hipSuccess && pa::dev_free(nullptr) == hipSuccess) {
             pa::warm_index(nullptr);  // the code objects too, not at the first real launch
             pa::warm_align(nullptr);
             pa::warm_fastq(nullptr);
@@ -243,14 +243,14 @@ pa_status pa_reads_upload(int32_t device, const uint8_t *seq, const uint8_t *qua
     hipStream_t st = as_stream(stream);
     auto fail = [&](hipError_t e) {
         set_error(std::string("pa_reads_upload: ") + hipGetErrorString(e));
-        hipFree(r->seq); hipFree(r->qual); hipFree(r->off);
+        pa::dev_free(r->seq); pa::dev_free(r->qual); pa::dev_free(r->off);
         delete r;
         return e == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;
     };
     hipError_t e;
-    if ((e = hipMalloc(&r->seq, nb + pa::kReadPad)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&r->qual, nb + pa::kReadPad)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&r->off, (n_reads + 1) * 8)) != hipSuccess) return fail(e);
+    if ((e = pa::dev_malloc(&r->seq, nb + pa::kReadPad)) != hipSuccess) return fail(e);
+    if ((e = pa::dev_malloc(&r->qual, nb + pa::kReadPad)) != hipSuccess) return fail(e);
+    if ((e = pa::dev_malloc(&r->off, (n_reads + 1) * 8)) != hipSuccess) return fail(e);
     if (nb) {
         if ((e = hipMemcpyAsync(r->seq, seq + read_off[0], nb, hipMemcpyHostToDevice, st)) != hipSuccess) return fail(e);
         if ((e = hipMemcpyAsync(r->qual, qual + read_off[0], nb, hipMemcpyHostToDevice, st)) != hipSuccess) return fail(e);
@@ -288,7 +288,7 @@ pa_status pa_reads_synthesize_mix(const pa_index *idx, uint64_t n_reads, uint32_
                                         as_stream(stream));
     if (rc == PA_OK) rc = pa::reads_measure(r, as_stream(stream));
     if (rc != PA_OK) {
-        hipFree(r->seq); hipFree(r->qual); hipFree(r->off);
+        pa::dev_free(r->seq); pa::dev_free(r->qual); pa::dev_free(r->off);
         delete r;
         return rc;
     }
@@ -330,9 +330,9 @@ pa_status pa_reads_download(const pa_reads *reads, uint64_t first, uint64_t coun
 void pa_reads_free(pa_reads *reads) {
     if (!reads) return;
     hipSetDevice(reads->device);
-    hipFree(reads->seq);
-    hipFree(reads->qual);
-    hipFree(reads->off);
+    pa::dev_free(reads->seq);
+    pa::dev_free(reads->qual);
+    pa::dev_free(reads->off);
     delete reads;
 }
 
@@ -345,9 +345,9 @@ pa_status pa_result_create(const pa_index *idx, pa_result **out) {
     r->device = idx->device;
     r->n_genomes = idx->n_genomes;
     const uint64_t G = idx->n_genomes;
-    if (hipMalloc(&r->sum_block, (6 + 2 * G) * 8) != hipSuccess ||
-        hipMalloc(&r->min_block, std::max<uint64_t>(G, 1) * 8) != hipSuccess) {
-        hipFree(r->sum_block);
+    if (pa::dev_malloc(&r->sum_block, (6 + 2 * G) * 8) != hipSuccess ||
+        pa::dev_malloc(&r->min_block, std::max<uint64_t>(G, 1) * 8) != hipSuccess) {
+        pa::dev_free(r->sum_block);
         delete r;
         set_error("pa_result_create: device allocation failed");
         return PA_ENOMEM;
@@ -416,8 +416,8 @@ pa_status pa_result_device_view(pa_result *res, uint64_t **sum_block, uint64_t *
 void pa_result_free(pa_result *res) {
     if (!res) return;
     hipSetDevice(res->device);
-    hipFree(res->sum_block);
-    hipFree(res->min_block);
+    pa::dev_free(res->sum_block);
+    pa::dev_free(res->min_block);
     delete res;
 }
 

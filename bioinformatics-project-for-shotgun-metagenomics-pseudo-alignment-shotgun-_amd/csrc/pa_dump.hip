@@ -312,7 +312,7 @@ pa_status dump_t(const pa_index *idx, const uint8_t *keep, unsigned long long *f
     unsigned long long *d_n = nullptr, *d_flags = nullptr;
     void *tmp = nullptr;
     auto cleanup = [&] {
-        hipFree(K); hipFree(K2); hipFree(V); hipFree(V2); hipFree(d_n); hipFree(d_flags); hipFree(tmp);
+        pa::dev_free(K); pa::dev_free(K2); pa::dev_free(V); pa::dev_free(V2); pa::dev_free(d_n); pa::dev_free(d_flags); pa::dev_free(tmp);
     };
 #define D_HIP(call)                                                                                       \
     do {                                                                                                  \
@@ -324,11 +324,11 @@ pa_status dump_t(const pa_index *idx, const uint8_t *keep, unsigned long long *f
         }                                                                                                 \
     } while (0)
     const unsigned fg = grid_for(total) > 65536 ? 65536 : grid_for(total);
-    D_HIP(hipMalloc(&K, total * sizeof(T)));
-    D_HIP(hipMalloc(&K2, total * sizeof(T)));
-    D_HIP(hipMalloc(&V, total * sizeof(T)));
-    D_HIP(hipMalloc(&V2, total * sizeof(T)));
-    D_HIP(hipMalloc(&d_n, 8));
+    D_HIP(pa::dev_malloc(&K, total * sizeof(T)));
+    D_HIP(pa::dev_malloc(&K2, total * sizeof(T)));
+    D_HIP(pa::dev_malloc(&V, total * sizeof(T)));
+    D_HIP(pa::dev_malloc(&V2, total * sizeof(T)));
+    D_HIP(pa::dev_malloc(&d_n, 8));
     D_HIP(hipMemsetAsync(d_n, 0, 8, st));
     hipLaunchKernelGGL(k_fill<T>, dim3(fg), dim3(kBlock), 0, st, K, total, (T)total);
     hipLaunchKernelGGL(k_iota<T>, dim3(fg), dim3(kBlock), 0, st, V, total);
@@ -339,14 +339,14 @@ pa_status dump_t(const pa_index *idx, const uint8_t *keep, unsigned long long *f
     rocprim::double_buffer<T> kb(K, K2), vb(V, V2);
     size_t tmp_bytes = 0;
     D_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, kb, vb, total, 0, end_bit, st));
-    D_HIP(hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)));
+    D_HIP(pa::dev_malloc(&tmp, std::max<size_t>(tmp_bytes, 16)));
     D_HIP(rocprim::radix_sort_pairs(tmp, tmp_bytes, kb, vb, total, 0, end_bit, st));
     unsigned long long nv = 0;
     D_HIP(hipMemcpyAsync(&nv, d_n, 8, hipMemcpyDeviceToHost, st));
     D_HIP(hipStreamSynchronize(st));
     n_valid = nv;
     const uint64_t nwords = (nv + 63) / 64;
-    D_HIP(hipMalloc(&d_flags, std::max<uint64_t>(nwords, 1) * 8));
+    D_HIP(pa::dev_malloc(&d_flags, std::max<uint64_t>(nwords, 1) * 8));
     if (nv) {
         hipLaunchKernelGGL(k_group_flags<T>, dim3((unsigned)((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            kb.current(), nv, d_flags);
@@ -371,7 +371,7 @@ pa_status dump_nw(const pa_index *idx, const uint8_t *keep, hipStream_t st, std:
                   std::vector<uint64_t> &h_flags, uint64_t &n_valid) {
     const uint64_t total = idx->h_goff[idx->n_genomes];
     unsigned long long *fp = nullptr;
-    PA_HIP(hipMalloc(&fp, idx->cap * 8));
+    PA_HIP(pa::dev_malloc(&fp, idx->cap * 8));
     const unsigned fg = grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap);
     hipLaunchKernelGGL(k_fill<unsigned long long>, dim3(fg), dim3(kBlock), 0, st, fp, idx->cap, ~0ull);
     launch_first<NW>(idx, fp, st);
@@ -386,7 +386,7 @@ pa_status dump_nw(const pa_index *idx, const uint8_t *keep, hipStream_t st, std:
         rc = dump_t<uint64_t, NW>(idx, keep, fp, total, st, h_t, h_flags, n_valid);
     }
     hipStreamSynchronize(st);
-    hipFree(fp);
+    pa::dev_free(fp);
     return rc;
 }
 

@@ -358,7 +358,7 @@ struct ParseBufs {
         while (ids_cap < 2 * est_rec) ids_cap <<= 1;
         hipError_t e = hipSuccess;
         auto m = [&](void **p, uint64_t b) {
-            if (e == hipSuccess) e = hipMalloc(p, b);
+            if (e == hipSuccess) e = pa::dev_malloc(p, b);
         };
         m((void **)&seq, span + kReadPad);
         m((void **)&qual, span + kReadPad);
@@ -377,8 +377,8 @@ struct ParseBufs {
         return e;
     }
     void release() {
-        hipFree(seq); hipFree(qual); hipFree(tile_cnt); hipFree(nl); hipFree(len); hipFree(tile_off);
-        hipFree(bsum); hipFree(rec_off); hipFree(ids); hipFree(tot); hipFree(meta);
+        pa::dev_free(seq); pa::dev_free(qual); pa::dev_free(tile_cnt); pa::dev_free(nl); pa::dev_free(len); pa::dev_free(tile_off);
+        pa::dev_free(bsum); pa::dev_free(rec_off); pa::dev_free(ids); pa::dev_free(tot); pa::dev_free(meta);
         hipHostFree(h_meta);
         *this = ParseBufs{};
     }
@@ -502,7 +502,7 @@ void prefetch_run(pa_fastq_prefetch *pf) {
     };
     hipError_t e = hipSetDevice(pf->device);
     size_t free_b = 0, total_b = 0;
-    if (e == hipSuccess) e = hipMemGetInfo(&free_b, &total_b);
+    if (e == hipSuccess) e = pa::dev_mem_info(&free_b, &total_b);
     // a file that would take more than a quarter of the free device memory
     // (text + parse buffers ~ 21 B per window byte) is left to the windowed stream
     uint64_t cap = free_b / 4;  // PA_PREFETCH_MAX_BYTES: a lower limit (tests: the windowed fallback)
@@ -512,7 +512,7 @@ void prefetch_run(pa_fastq_prefetch *pf) {
         return;
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&pf->st, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&pf->text, pf->size + 2 * kTile + 16);
+    if (e == hipSuccess) e = pa::dev_malloc(&pf->text, pf->size + 2 * kTile + 16);
     if (e == hipSuccess) e = pf->bufs.alloc(pf->window + 16, pf->size / 16 + 1024, pf->st);
     if (e != hipSuccess) {
         fail(e == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE,
@@ -657,7 +657,7 @@ void fastq_prefetch_free(pa_fastq_prefetch *pf) {
     if (pf->th.joinable()) pf->th.join();
     hipSetDevice(pf->device);
     if (pf->st) hipStreamSynchronize(pf->st);
-    hipFree(pf->text);
+    pa::dev_free(pf->text);
     pf->bufs.release();
     if (pf->st) hipStreamDestroy(pf->st);
     delete pf;
@@ -780,7 +780,7 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         hipStreamSynchronize(st);
         for (int i = 0; i < 2; i++) {
             hipHostFree(H[i]);
-            hipFree(D[i]);
+            pa::dev_free(D[i]);
             if (ev_h2d[i]) hipEventDestroy(ev_h2d[i]);
             if (ev_carry[i]) hipEventDestroy(ev_carry[i]);
         }
@@ -800,7 +800,7 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
     } while (0)
     for (int i = 0; i < 2; i++) {
         F_HIP(hipHostMalloc((void **)&H[i], W, hipHostMallocDefault));
-        F_HIP(hipMalloc(&D[i], dbytes));
+        F_HIP(pa::dev_malloc(&D[i], dbytes));
         F_HIP(hipEventCreateWithFlags(&ev_h2d[i], hipEventDisableTiming));
         F_HIP(hipEventCreateWithFlags(&ev_carry[i], hipEventDisableTiming));
     }

@@ -40,6 +40,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <memory>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -92,6 +93,28 @@ struct PhaseTimer {
             fprintf(stderr, "[pa_build] %s ms; total %.1f ms\n", out.c_str(),
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     }
+};
+// The build's timer, for the phases of the functions it calls (tiles,
+// neighbour bits, Bloom filters): phase_mark is a no-op outside a timed build.
+thread_local PhaseTimer *t_phase = nullptr;
+inline void phase_mark(const char *name) {
+    if (!t_phase) return;
+    t_phase->mark(name);
+    // device memory at this point: the driver's free bytes, the pool's slabs and their free part (GiB)
+    size_t f = 0, t = 0, sb = 0, sf = 0;
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipMemGetInfo(&f, &t);
+    pa::dev_pool_stats(dev, &sb, &sf);
+    char b[96];
+    snprintf(b, sizeof b, " [driver free %.1f, pool %.1f / free %.1f GiB]", f / 1073741824.0, sb / 1073741824.0,
+             sf / 1073741824.0);
+    t_phase->out += b;
+}
+struct PhaseScope {
+    PhaseTimer *prev;
+    explicit PhaseScope(PhaseTimer *t) : prev(t_phase) { t_phase = t->on ? t : nullptr; }
+    ~PhaseScope() { t_phase = prev; }
 };
 
 inline unsigned grid_for(uint64_t n, unsigned block = kBlock) {
@@ -851,8 +874,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
     unsigned long long *cnt = nullptr;  // [0] n_kmers [1] bump [2] n_multi [3] n_cls [4] bump2
     pa_status rc = PA_OK;
     auto cleanup = [&]() {
-        hipFree(off); hipFree(lists);
-        hipFree(cs_key); hipFree(cs_rep); hipFree(cs_id); hipFree(rep_of); hipFree(cnt); hipFree(err);
+        pa::dev_free(off); pa::dev_free(lists);
+        pa::dev_free(cs_key); pa::dev_free(cs_rep); pa::dev_free(cs_id); pa::dev_free(rep_of); pa::dev_free(cnt); pa::dev_free(err);
     };
 #define B_HIP(call)                                                                                 \
     do {                                                                                            \
@@ -863,9 +886,9 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             return e_ == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;                              \
         }                                                                                           \
     } while (0)
-    B_HIP(hipMalloc(&off, cap * 8));
-    B_HIP(hipMalloc(&cnt, 8 * 8));
-    B_HIP(hipMalloc(&err, 4));
+    B_HIP(pa::dev_malloc(&off, cap * 8));
+    B_HIP(pa::dev_malloc(&cnt, 8 * 8));
+    B_HIP(pa::dev_malloc(&err, 4));
     B_HIP(hipMemsetAsync(cnt, 0, 8 * 8, st));
     B_HIP(hipMemsetAsync(err, 0, 4, st));
     // pass 1
@@ -894,7 +917,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
     const uint64_t list_total = h_cnt[1], n_multi = h_cnt[2];
     idx->n_multi = 0;
     if (n_multi > 0) {
-        B_HIP(hipMalloc(&lists, list_total * 4));
+        B_HIP(pa::dev_malloc(&lists, list_total * 4));
         for (uint32_t g = 0; g < G; g++) {
             uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
             if ((uint64_t)k > len) continue;
@@ -912,8 +935,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         uint64_t cs_cap = std::min<uint64_t>(cs_max, (1ull << 24) + 64);
         unsigned sgrid = grid_for(cap) > 65536 ? 65536 : grid_for(cap);
         for (;;) {
-            B_HIP(hipMalloc(&cs_key, cs_cap * 8));
-            B_HIP(hipMalloc(&cs_rep, cs_cap * 8));
+            B_HIP(pa::dev_malloc(&cs_key, cs_cap * 8));
+            B_HIP(pa::dev_malloc(&cs_rep, cs_cap * 8));
             hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0,
                                st, cs_key, cs_cap, EMPTY);
             hipLaunchKernelGGL(k_class_insert<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, G, off, lists,
@@ -922,8 +945,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
             B_HIP(hipStreamSynchronize(st));
             if (!(h_err & 4u) || cs_cap >= cs_max) break;
-            hipFree(cs_key);
-            hipFree(cs_rep);
+            pa::dev_free(cs_key);
+            pa::dev_free(cs_rep);
             cs_key = cs_rep = nullptr;
             B_HIP(hipMemsetAsync(err, 0, 4, st));
             cs_cap = std::min<uint64_t>(cs_max, 4 * cs_cap);
@@ -933,12 +956,12 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             cleanup();
             return PA_EINTERNAL;
         }
-        B_HIP(hipMalloc(&cs_id, cs_cap * 4));
+        B_HIP(pa::dev_malloc(&cs_id, cs_cap * 4));
         // class ids: at most min(n_multi, cs_cap) classes
         const uint64_t max_cls = std::min<uint64_t>(n_multi, cs_cap);
-        B_HIP(hipMalloc(&idx->class_size, max_cls * 4));
-        B_HIP(hipMalloc(&idx->class_off, max_cls * 8));
-        B_HIP(hipMalloc(&rep_of, max_cls * 8));
+        B_HIP(pa::dev_malloc(&idx->class_size, max_cls * 4));
+        B_HIP(pa::dev_malloc(&idx->class_off, max_cls * 8));
+        B_HIP(pa::dev_malloc(&rep_of, max_cls * 8));
         hipLaunchKernelGGL(k_class_number<NW>, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock),
                            0, st, cs_key, cs_rep, cs_id, cs_cap, (const Slot<NW> *)table, idx->class_size,
                            idx->class_off, rep_of, cnt + 3, cnt + 4);
@@ -951,11 +974,11 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             cleanup();
             return PA_EUNSUPPORTED;
         }
-        B_HIP(hipMalloc(&idx->class_genomes, std::max<uint64_t>(entries, 1) * 4));
+        B_HIP(pa::dev_malloc(&idx->class_genomes, std::max<uint64_t>(entries, 1) * 4));
         hipLaunchKernelGGL(k_class_copy, dim3((unsigned)std::min<uint64_t>(n_cls, 65536)), dim3(kBlock), 0, st, n_cls,
                            rep_of, idx->class_size, idx->class_off, off, lists, idx->class_genomes);
         if (G <= 64) {
-            B_HIP(hipMalloc(&idx->class_mask, std::max<uint64_t>(entries, 1) * 8));
+            B_HIP(pa::dev_malloc(&idx->class_mask, std::max<uint64_t>(entries, 1) * 8));
             hipLaunchKernelGGL(k_class_masks, dim3((unsigned)std::min<uint64_t>((n_cls + kBlock - 1) / kBlock, 4096)),
                                dim3(kBlock), 0, st, n_cls, idx->class_off, idx->class_genomes, idx->class_mask);
         }
@@ -1002,12 +1025,14 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
     // them, PA_NB_HALF=1 forces the 12-B form (A/B measurements, tests)
     size_t free_b = 0, total_b = 0;
     const char *no_nb = std::getenv("PA_NO_NB"), *nb_half = std::getenv("PA_NB_HALF");
-    if (!(no_nb && no_nb[0] == '1') && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+    if (!(no_nb && no_nb[0] == '1') && pa::dev_mem_info(&free_b, &total_b) == hipSuccess) {
         const bool full = n * 24 <= free_b / 4 * 3 && !(nb_half && nb_half[0] == '1') && !idx->force_large;
         const uint64_t wb = full ? 8 : 4;
         if (n * 3 * wb <= free_b / 4 * 3) {
-            B_HIP(hipMalloc(&idx->tile_nb, n * 3 * wb + 64));
+            B_HIP(pa::dev_malloc(&idx->tile_nb, n * 3 * wb + 64));
+            phase_mark("nb: alloc");
             B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 3 * wb + 64, st));
+            phase_mark("nb: clear");
             // a build-time Bloom filter of the keys (~16 bits per key, in
             // HBM; freed below): most of the 3k neighbours of a window are
             // absent and share the window's Bloom line (minimizer-chosen),
@@ -1019,24 +1044,28 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
             if (!(nbb && nbb[0] == '0') && idx->n_kmers > 0) {
                 while (bb_lg < 33 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;  // (bloom_block: lg <= 33)
                 size_t fb = 0, tb = 0;
-                if (hipMemGetInfo(&fb, &tb) != hipSuccess) fb = 0;
+                if (pa::dev_mem_info(&fb, &tb) != hipSuccess) fb = 0;
                 while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
-                if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && hipMalloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
+                if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && pa::dev_malloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
                     B_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
+                    phase_mark(bb_lg >= 30 ? "nb: Bloom alloc (lg >= 30)" : "nb: Bloom alloc (lg < 30)");
                     hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
                                        dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, bb, bb_lg, k);
                 } else {
                     bb = nullptr;
                 }
             }
-            for (int pass = 0; pass < 2; pass++)
+            phase_mark("nb: build Bloom");
+            for (int pass = 0; pass < 2; pass++) {
                 hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
                                    st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
                                    idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
                                    pass, bb, bb_lg);
+                phase_mark(pass == 0 ? "nb: first occurrences" : "nb: copies");
+            }
             if (bb) {
                 B_HIP(hipStreamSynchronize(st));
-                hipFree(bb);
+                pa::dev_free(bb);
             }
             idx->nb_spec = full ? 1 : 0;
             idx->device_bytes += n * 3 * wb;
@@ -1057,12 +1086,12 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
 #define B_HIP(call) PA_HIP(call)
     if (idx->tile_n > 0) {  // tiles: 6.5 B per base (class, flags, set sizes, 2-bit string), + margin
         size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || idx->tile_n * 7 + (2ull << 30) > free_b) idx->tile_n = 0;
+        if (pa::dev_mem_info(&free_b, &total_b) != hipSuccess || idx->tile_n * 7 + (2ull << 30) > free_b) idx->tile_n = 0;
     }
     if (idx->tile_n > 0) {  // step 6: genome tiling
         const uint64_t n = idx->tile_n, nwords = n / 32 + 32;  // padded: the walk reads up to 18 words past a position
-        B_HIP(hipMalloc(&idx->tile_cls, n * 4));
-        B_HIP(hipMalloc(&idx->tile_pk, nwords * 8));
+        B_HIP(pa::dev_malloc(&idx->tile_cls, n * 4));
+        B_HIP(pa::dev_malloc(&idx->tile_pk, nwords * 8));
         B_HIP(hipMemsetAsync(idx->tile_cls, 0xFF, n * 4, st));
         hipLaunchKernelGGL(k_tile_pack, dim3(grid_for(nwords) > 65536 ? 65536 : grid_for(nwords)), dim3(kBlock), 0, st,
                            idx->codes, n, idx->tile_pk, nwords);
@@ -1074,6 +1103,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                                idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls, g, G,
                                idx->class_genomes, idx->tpos_local, wpt);
         }
+        phase_mark("tile classes");
         {  // genome of every 2^16-th position: genome_of is then one or two goff steps
             const uint64_t nb_ = (n >> 16) + 2;
             std::vector<uint32_t> gb(nb_);
@@ -1084,7 +1114,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 g = g == 0 ? 0 : g - 1;
                 gb[j] = g >= G ? G - 1 : g;
             }
-            B_HIP(hipMalloc(&idx->tile_gblk, nb_ * 4));
+            B_HIP(pa::dev_malloc(&idx->tile_gblk, nb_ * 4));
             B_HIP(hipMemcpyAsync(idx->tile_gblk, gb.data(), nb_ * 4, hipMemcpyHostToDevice, st));
             B_HIP(hipStreamSynchronize(st));
             idx->device_bytes += nb_ * 4;
@@ -1094,10 +1124,11 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                                st, idx->tile_pk, idx->tile_cls, n, k);
         if (k <= 31) {
             const uint64_t n_blocks = n / 64 + 5;  // padded: the walk reads four blocks from any position
-            B_HIP(hipMalloc(&idx->tile_lw, n_blocks * 32));
+            B_HIP(pa::dev_malloc(&idx->tile_lw, n_blocks * 32));
             hipLaunchKernelGGL(k_tile_walk, dim3((unsigned)std::min<uint64_t>((n_blocks + 3) / 4, 1u << 20)), dim3(256),
                                0, st, idx->tile_cls, idx->tile_pk, n, G, idx->tile_lw, n_blocks);
             idx->device_bytes += n_blocks * 32;
+            phase_mark("repeats + walk blocks");
             // one-substitution neighbours (build_nb): now, or -- when the caller
             // expects too few reads to repay them -- on the align that brings the
             // reads past that point (index_maybe_nb)
@@ -1106,6 +1137,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             } else {
                 PA_TRY(build_nb(idx, st));
             }
+            phase_mark("neighbour bits");
             // the Bloom filter of the keys, for the lane kernel's probes of windows
             // off the walk (almost all absent).  In the memory-side cache: 16 bits
             // per key up to PA_BLOOM_MB (default 128: with minimizer blocks of 16 B
@@ -1129,20 +1161,21 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 bool ok = cap_b > 0 && idx->n_kmers > 0 && (1ull << lg) * 64 >= idx->n_kmers * 8 && (1ull << lg) * 8 <= cap_b;
                 if (!ok && idx->n_kmers > 0 && !(bh && bh[0] == '0') && (!bm || idx->force_large)) {
                     size_t fb = 0, tb = 0;
-                    if (hipMemGetInfo(&fb, &tb) == hipSuccess) {
+                    if (pa::dev_mem_info(&fb, &tb) == hipSuccess) {
                         lg = lg16;  // 16 bits per key, fewer down to 8 if it must, in at most 1/8 of the free memory
                         while (lg > 6 && (1ull << lg) * 8 > fb / 8) lg--;
                         ok = (1ull << lg) * 64 >= idx->n_kmers * 8;
                     }
                 }
                 if (ok) {
-                    B_HIP(hipMalloc(&idx->bloom, (1ull << lg) * 8));
+                    B_HIP(pa::dev_malloc(&idx->bloom, (1ull << lg) * 8));
                     B_HIP(hipMemsetAsync(idx->bloom, 0, (1ull << lg) * 8, st));
                     hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
                                        dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg, k);
                     idx->bloom_lg = lg;
                     idx->device_bytes += (1ull << lg) * 8;
                 }
+                phase_mark("Bloom");
             }
         }
         B_HIP(hipGetLastError());
@@ -1179,45 +1212,45 @@ void extsim_slots_nw(const pa_index *idx, const uint32_t *d_group, uint32_t n_gr
 namespace pa {
 
 void index_release(pa_index *idx) {
-    hipFree(idx->table);
-    hipFree(idx->class_off);
-    hipFree(idx->class_size);
-    hipFree(idx->class_genomes);
-    hipFree(idx->class_mask);
-    hipFree(idx->codes);
-    hipFree(idx->goff);
-    hipFree(idx->tile_cls);
-    hipFree(idx->tile_pk);
-    hipFree(idx->tile_lw);
+    pa::dev_free(idx->table);
+    pa::dev_free(idx->class_off);
+    pa::dev_free(idx->class_size);
+    pa::dev_free(idx->class_genomes);
+    pa::dev_free(idx->class_mask);
+    pa::dev_free(idx->codes);
+    pa::dev_free(idx->goff);
+    pa::dev_free(idx->tile_cls);
+    pa::dev_free(idx->tile_pk);
+    pa::dev_free(idx->tile_lw);
     idx->tile_lw = nullptr;
-    hipFree(idx->tile_big);
+    pa::dev_free(idx->tile_big);
     idx->tile_big = nullptr;
     idx->tile_big_mg = -1;
-    hipFree(idx->tile_nb);
+    pa::dev_free(idx->tile_nb);
     idx->tile_nb = nullptr;
-    hipFree(idx->tile_nbbig);
+    pa::dev_free(idx->tile_nbbig);
     idx->tile_nbbig = nullptr;
     idx->tile_nbbig_mg = -1;
-    hipFree(idx->bloom);
+    pa::dev_free(idx->bloom);
     idx->bloom = nullptr;
-    hipFree(idx->tile_gblk);
+    pa::dev_free(idx->tile_gblk);
     idx->tile_gblk = nullptr;
     idx->bloom_lg = 0;
     idx->tile_cls = nullptr;
     idx->tile_pk = nullptr;
-    hipFree(idx->ws.ptr);
-    hipFree(idx->queue);
-    hipFree(idx->queue_hard);
-    hipFree(idx->queue_na);
-    hipFree(idx->na_count);
-    hipFree(idx->qmask);
-    hipFree(idx->qdrop);
+    pa::dev_free(idx->ws.ptr);
+    pa::dev_free(idx->queue);
+    pa::dev_free(idx->queue_hard);
+    pa::dev_free(idx->queue_na);
+    pa::dev_free(idx->na_count);
+    pa::dev_free(idx->qmask);
+    pa::dev_free(idx->qdrop);
     idx->qmask = nullptr;
     idx->qdrop = nullptr;
     idx->qmask_cap = 0;
     idx->queue_na = nullptr;
     idx->na_count = nullptr;
-    hipFree(idx->counters);
+    pa::dev_free(idx->counters);
     for (auto e : idx->ev_start) hipEventDestroy(e);
     for (auto e : idx->ev_stop) hipEventDestroy(e);
     for (auto &e : idx->kev) {
@@ -1237,13 +1270,16 @@ pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st) {
 pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
     if (!idx->tiles_pending) return PA_OK;
     idx->tiles_pending = 0;
+    std::unique_ptr<PhaseTimer> own;  // (timed on its own unless a timed build called it)
+    if (!t_phase) own.reset(new PhaseTimer(st));
+    PhaseScope ps(t_phase ? t_phase : own.get());
     const uint64_t bases = idx->h_goff.empty() ? 0 : idx->h_goff.back();
     idx->nb_skip = reads_hint != ~0ull && reads_hint < kNbReadsPerBase * bases;
     pa_status rc = build_tiles_nw<1>(idx, st);  // (tiles are made for single-word keys only)
     idx->nb_skip = 0;
     if (rc != PA_OK) {  // the index stays usable without its align-side view
-        hipFree(idx->tile_cls); hipFree(idx->tile_pk); hipFree(idx->tile_lw); hipFree(idx->tile_nb);
-        hipFree(idx->tile_gblk); hipFree(idx->bloom);
+        pa::dev_free(idx->tile_cls); pa::dev_free(idx->tile_pk); pa::dev_free(idx->tile_lw); pa::dev_free(idx->tile_nb);
+        pa::dev_free(idx->tile_gblk); pa::dev_free(idx->bloom);
         idx->tile_cls = nullptr, idx->tile_pk = nullptr, idx->tile_lw = nullptr, idx->tile_nb = nullptr;
         idx->tile_gblk = nullptr, idx->bloom = nullptr, idx->bloom_lg = 0, idx->tile_n = 0;
     }
@@ -1253,6 +1289,7 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
 pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
                       hipStream_t st, bool defer_tiles) {
     PhaseTimer tm(st);
+    PhaseScope ps(&tm);
     idx->k = k;
     idx->nw = k > 0 ? key_words(k) : 1;
     idx->n_genomes = n;
@@ -1280,16 +1317,16 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     if (const char *e = std::getenv("PA_LAYOUT")) idx->force_large = std::strcmp(e, "large") == 0;
     if (const char *e = std::getenv("PA_TPOS_LOCAL")) idx->tpos_local |= e[0] == '1';  // tests: the >= 4 Gbp layout
     idx->tpos_local |= idx->force_large;
-    PA_HIP(hipMalloc(&idx->codes, std::max<uint64_t>(total, 1)));
-    PA_HIP(hipMalloc(&idx->goff, (n + 1) * 8));
-    PA_HIP(hipMalloc(&idx->counters, 32 * 8));
+    PA_HIP(pa::dev_malloc(&idx->codes, std::max<uint64_t>(total, 1)));
+    PA_HIP(pa::dev_malloc(&idx->goff, (n + 1) * 8));
+    PA_HIP(pa::dev_malloc(&idx->counters, 32 * 8));
     PA_HIP(hipMemsetAsync(idx->counters, 0, 32 * 8, st));
     PA_HIP(hipMemcpyAsync(idx->goff, idx->h_goff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
     if (total > 0) {
         uint8_t *ascii = nullptr;  // ASCII staging buffer, freed before the table is allocated
         unsigned long long *bad = nullptr, h_bad = ~0ull;
-        PA_HIP(hipMalloc(&ascii, total));
-        PA_HIP(hipMalloc(&bad, 8));
+        PA_HIP(pa::dev_malloc(&ascii, total));
+        PA_HIP(pa::dev_malloc(&bad, 8));
         tm.mark("alloc");
         hipError_t e = hipMemsetAsync(bad, 0xFF, 8, st);
         if (e == hipSuccess) e = hipMemcpyAsync(ascii, genomes + goff[0], total, hipMemcpyHostToDevice, st);
@@ -1300,8 +1337,8 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
             e = hipMemcpyAsync(&h_bad, bad, 8, hipMemcpyDeviceToHost, st);
         }
         if (e == hipSuccess) e = hipStreamSynchronize(st);
-        hipFree(ascii);
-        hipFree(bad);
+        pa::dev_free(ascii);
+        pa::dev_free(bad);
         PA_HIP(e);
         if (h_bad != ~0ull) {
             set_error("genome text may only contain A, C, G, T and N (byte " + std::to_string(h_bad) + ")");
@@ -1322,7 +1359,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     const int sb = slot_bytes(idx->nw);
     const uint64_t per_slot = (uint64_t)sb + 20;
     size_t free_b = 0, total_b = 0;
-    PA_HIP(hipMemGetInfo(&free_b, &total_b));
+    PA_HIP(pa::dev_mem_info(&free_b, &total_b));
     const uint64_t reserve = windows * 4 + (1ull << 30);
     auto fits = [&](uint64_t c) { return c * per_slot + reserve <= (uint64_t)free_b; };
     uint64_t cap = 0;
@@ -1337,7 +1374,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     if (idx->force_large) cap = 0, free_b = (size_t)0;
     if (cap == 0 && k > 0 && windows > 0) {
         uint32_t *reg = nullptr;
-        PA_HIP(hipMalloc(&reg, (4ull << kHllBits)));
+        PA_HIP(pa::dev_malloc(&reg, (4ull << kHllBits)));
         PA_HIP(hipMemsetAsync(reg, 0, (4ull << kHllBits), st));
         const uint64_t mask0 = (2 * k - 64 * (idx->nw - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (idx->nw - 1))) - 1);
         for (uint32_t g = 0; g < n; g++) {
@@ -1356,7 +1393,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         std::vector<uint32_t> h(1u << kHllBits);
         hipError_t e = hipMemcpyAsync(h.data(), reg, (4ull << kHllBits), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
-        hipFree(reg);
+        pa::dev_free(reg);
         PA_HIP(e);
         const double mm = (double)(1u << kHllBits);
         double z = 0;
@@ -1370,7 +1407,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         const uint64_t distinct = (uint64_t)(est * 1.03) + 64;
         idx->distinct_estimate = distinct;
         const bool forced = free_b == 0;
-        if (forced) PA_HIP(hipMemGetInfo(&free_b, &total_b));
+        if (forced) PA_HIP(pa::dev_mem_info(&free_b, &total_b));
         for (double mult : {4.0, 2.0, 1.43}) {
             const uint64_t c = (uint64_t)(mult * (double)distinct) + 64;
             if (forced && mult > 1.5) continue;
@@ -1389,7 +1426,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     cap = (cap + 3) / 4 * 4;  // whole 64-B lines (the fast kernel probes a line per step)
     idx->cap = cap;
     idx->home = pad::HomeCfg{cap};
-    PA_HIP(hipMalloc(&idx->table, idx->cap * sb));
+    PA_HIP(pa::dev_malloc(&idx->table, idx->cap * sb));
     PA_HIP(hipMemsetAsync(idx->table, 0xFF, idx->cap * sb, st));
     idx->device_bytes = idx->cap * sb + total + (n + 1) * 8;
     tm.mark("table");
@@ -1423,9 +1460,9 @@ pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint3
     uint8_t *d_k = nullptr;
     int64_t *d_c = nullptr;
     uint32_t *d_s = nullptr;
-    PA_HIP(hipMalloc(&d_k, n * kmer_len));
-    PA_HIP(hipMalloc(&d_c, n * 8));
-    PA_HIP(hipMalloc(&d_s, n * 4));
+    PA_HIP(pa::dev_malloc(&d_k, n * kmer_len));
+    PA_HIP(pa::dev_malloc(&d_c, n * 8));
+    PA_HIP(pa::dev_malloc(&d_s, n * 4));
     PA_HIP(hipMemcpyAsync(d_k, kmers, n * kmer_len, hipMemcpyHostToDevice, st));
     pa_status rc = PA_OK;
     switch (idx->nw) {
@@ -1440,9 +1477,9 @@ pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint3
         if (size_out) PA_HIP(hipMemcpyAsync(size_out, d_s, n * 4, hipMemcpyDeviceToHost, st));
         PA_HIP(hipStreamSynchronize(st));
     }
-    hipFree(d_k);
-    hipFree(d_c);
-    hipFree(d_s);
+    pa::dev_free(d_k);
+    pa::dev_free(d_c);
+    pa::dev_free(d_s);
     return rc;
 }
 
@@ -1457,12 +1494,12 @@ pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint
     const uint64_t nm = std::max<uint64_t>(idx->n_multi, 1);
     const uint64_t n_rec = std::max<uint64_t>(idx->class_entries, 1);
     const unsigned cgrid = (unsigned)std::min<uint64_t>(nm, 1024);
-    PA_HIP(hipMalloc(&d_group, (uint64_t)idx->n_genomes * 4));
-    PA_HIP(hipMalloc(&d_tot, n_groups * 8));
-    PA_HIP(hipMalloc(&d_uniq, n_groups * 8));
-    PA_HIP(hipMalloc(&d_inter, ng2 * 8));
-    PA_HIP(hipMalloc(&d_cc, n_rec * 8));
-    PA_HIP(hipMalloc(&scratch, (uint64_t)cgrid * (idx->n_genomes + 1) * 4));
+    PA_HIP(pa::dev_malloc(&d_group, (uint64_t)idx->n_genomes * 4));
+    PA_HIP(pa::dev_malloc(&d_tot, n_groups * 8));
+    PA_HIP(pa::dev_malloc(&d_uniq, n_groups * 8));
+    PA_HIP(pa::dev_malloc(&d_inter, ng2 * 8));
+    PA_HIP(pa::dev_malloc(&d_cc, n_rec * 8));
+    PA_HIP(pa::dev_malloc(&scratch, (uint64_t)cgrid * (idx->n_genomes + 1) * 4));
     PA_HIP(hipMemcpyAsync(d_group, group_of, (uint64_t)idx->n_genomes * 4, hipMemcpyHostToDevice, st));
     PA_HIP(hipMemsetAsync(d_tot, 0, n_groups * 8, st));
     PA_HIP(hipMemsetAsync(d_uniq, 0, n_groups * 8, st));
@@ -1484,7 +1521,7 @@ pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint
     PA_HIP(hipMemcpyAsync(uniq, d_uniq, n_groups * 8, hipMemcpyDeviceToHost, st));
     PA_HIP(hipMemcpyAsync(inter, d_inter, ng2 * 8, hipMemcpyDeviceToHost, st));
     PA_HIP(hipStreamSynchronize(st));
-    hipFree(d_group); hipFree(d_tot); hipFree(d_uniq); hipFree(d_inter); hipFree(d_cc); hipFree(scratch);
+    pa::dev_free(d_group); pa::dev_free(d_tot); pa::dev_free(d_uniq); pa::dev_free(d_inter); pa::dev_free(d_cc); pa::dev_free(scratch);
     return PA_OK;
 }
 
@@ -1502,10 +1539,10 @@ pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_
     r->n_bases = n * len;
     r->max_len = len;
     uint32_t *d_elig = nullptr;
-    PA_HIP(hipMalloc(&r->seq, r->n_bases + kReadPad));
-    PA_HIP(hipMalloc(&r->qual, r->n_bases + kReadPad));
-    PA_HIP(hipMalloc(&r->off, (n + 1) * 8));
-    PA_HIP(hipMalloc(&d_elig, elig.size() * 4));
+    PA_HIP(pa::dev_malloc(&r->seq, r->n_bases + kReadPad));
+    PA_HIP(pa::dev_malloc(&r->qual, r->n_bases + kReadPad));
+    PA_HIP(pa::dev_malloc(&r->off, (n + 1) * 8));
+    PA_HIP(pa::dev_malloc(&d_elig, elig.size() * 4));
     PA_HIP(hipMemcpyAsync(d_elig, elig.data(), elig.size() * 4, hipMemcpyHostToDevice, st));
     if (n == 0 || len == 0) {
         PA_HIP(hipMemsetAsync(r->off, 0, (n + 1) * 8, st));
@@ -1520,7 +1557,7 @@ pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_
     }
     PA_HIP(hipGetLastError());
     PA_HIP(hipStreamSynchronize(st));
-    hipFree(d_elig);
+    pa::dev_free(d_elig);
     return PA_OK;
 }
 

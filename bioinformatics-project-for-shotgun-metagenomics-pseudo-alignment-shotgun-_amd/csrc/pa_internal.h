@@ -47,6 +47,20 @@ struct DevParams {
     uint32_t flags;
 };
 
+// Device memory (pa_mem.cpp): large buffers from the library's slab pool,
+// small ones straight from hipMalloc.  Every device buffer of libpa.so is
+// taken and given back through these; dev_mem_info counts the pool's free
+// ranges as free.
+hipError_t dev_malloc_raw(void **p, size_t n);
+template <typename T>
+inline hipError_t dev_malloc(T **p, size_t n) {
+    return dev_malloc_raw((void **)p, n);
+}
+hipError_t dev_free(void *p);
+hipError_t dev_mem_info(size_t *free_b, size_t *total_b);
+size_t dev_trim(int dev);
+void dev_pool_stats(int dev, size_t *slab_bytes, size_t *free_bytes);
+
 struct Workspace {  // grow-only device scratch owned by an index
     void *ptr = nullptr;
     size_t bytes = 0;

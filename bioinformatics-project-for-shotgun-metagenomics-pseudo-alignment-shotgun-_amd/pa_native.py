@@ -39,7 +39,7 @@ EXPORTS = (
     "pa_align", "pa_align_detail", "pa_align_batch", "pa_align_fastq_file",
     "pa_fastq_prefetch_start", "pa_align_fastq_prefetched", "pa_fastq_prefetch_free",
     "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_comm_count", "pa_counters_reduce",
-    "pa_profile_enable", "pa_profile_read", "pa_profile_read_kernels",
+    "pa_profile_enable", "pa_profile_read", "pa_profile_read_kernels", "pa_mem_trim",
     "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free",
 )
 
@@ -147,6 +147,7 @@ def lib():
         "pa_profile_enable": (I32, [P, I32]),
         "pa_profile_read": (I32, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "pa_profile_read_kernels": (I32, [P, P, P]),
+        "pa_mem_trim": (I32, [I32, ctypes.POINTER(U64)]),
         "pa_parse_text": (I32, [I32, P, U64, I32, I32, PP]),
         "pa_parse_file": (I32, [I32, ctypes.c_char_p, I32, PP]),
         "pa_seqset_sizes": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
@@ -205,6 +206,15 @@ def device_count() -> int:
 
 def default_device() -> int:
     return int(os.environ.get("PA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def mem_trim(device: int = -1) -> int:
+    """Give the library's idle device slabs back to the driver (pa_mem_trim);
+    returns the bytes released.  Closed indexes and reads leave their large
+    buffers in the library's pool for the next build (csrc/pa_mem.cpp)."""
+    n = U64(0)
+    _check(lib().pa_mem_trim(int(device), ctypes.byref(n)))
+    return int(n.value)
 
 
 def ingest_threads() -> int:

@@ -321,6 +321,18 @@ pa_status pa_profile_read(pa_index *idx, double *main_ms, uint64_t *launches, ui
 #define PA_PROF_KERNELS 5
 pa_status pa_profile_read_kernels(pa_index *idx, double *ms, uint64_t *launches);
 
+/* ---- device memory -------------------------------------------------------------- */
+
+/* Buffers of 256 MiB and more (tables, tiles, read columns) come from slabs
+ * the library keeps per device and reuses after a free (csrc/pa_mem.cpp: the
+ * driver reclaims given-back memory at ~60 GB/s, which stalled rebuilds such as
+ * EXTSIM's index of the kept genomes).  pa_mem_trim gives the idle slabs of
+ * `device` (-1: every device) back to the driver, for a process that needs the
+ * memory elsewhere; *released (may be NULL) = bytes given back.  Allocations
+ * that cannot be met otherwise trim by themselves.  No reference counterpart
+ * (the reference holds its index in Python dicts). */
+pa_status pa_mem_trim(int32_t device, uint64_t *released);
+
 /* ---- ingest (host only, no device) ---------------------------------------------- */
 
 /* Multi-threaded parse of FASTA (kind PA_FASTA) or FASTQ (PA_FASTQ) text into
