@@ -18,7 +18,19 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-from bench import kernel_short_name  # noqa: E402
+
+
+def kernel_short_name(mangled: str):
+    """Any kernel's identifier (k_...) from its mangled name: the length prefix
+    may run into a preceding digit ("_GLOBAL__N_1" + "10k_nb_build")."""
+    import re
+    for m in re.finditer(r"(\d+)(k_[A-Za-z0-9_]+)", mangled):
+        digits, rest = m.group(1), m.group(2)
+        for i in range(len(digits)):
+            n = int(digits[i:])
+            if n <= len(rest) and (n == len(rest) or rest[n] in "EIv."):
+                return rest[:n]
+    return None
 
 
 def main():
