@@ -46,6 +46,7 @@
 // specific one: the wave kernel.
 
 constexpr int kLaneMaxW = 128;    // windows per read on the lane path
+constexpr uint64_t kPosMask = (1ull << 40) - 1;  // concatenated positions (< 2^40 bases) in packed anchors
 constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
 constexpr int kLaneChunks = 12;   // 16-B chunks covering shift + kLaneMaxLen bases
 constexpr int kLaneWords = 6;     // 64-bit words of the packed read (32 bases each)
@@ -83,7 +84,6 @@ struct __align__(16) LaneWave {
     uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
     uint32_t again_r[128];           // reads to walk again from a specific k-mer found off their walk,
     unsigned long long again_a[128]; //   and that anchor: (window << 40) | position
-    uint32_t n_hr[64], n_qf[64];     // per-lane window counters of the settled reads (kept out of VGPRs)
 };
 
 enum : int {
@@ -185,8 +185,9 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
 struct LaneRead {
     int kind;                          // LANE_* (LANE_WALK: still resolving)
     uint32_t len, W;
-    uint64_t atp;                      // anchor: first occurrence (concatenated position)
-    uint32_t acls, aw;                 //   its class and window
+    uint64_t anc;                      // anchor: (window << 40) | first occurrence (concatenated
+                                       // position < 2^40, as the again lists hold it: one register pair)
+    uint32_t acls;                     //   its class
     uint32_t g, nspec, nincl, hr;      // walk results (anchor genome, counts)
     uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
     uint64_t F0, F1;                   // windows failing --min-kmer-quality (never looked up)
@@ -348,7 +349,8 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         }
     }
 #endif
-    row[kLaneWords] = 0;
+    // (row[kLaneWords], the zero word past the read, is cleared once per kernel:
+    // a store here kept a 64-bit zero live through the whole loop and spilled it)
     if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
 #if defined(PA_STATS) || defined(PA_DISSECT)
     if (a.dbg_mode == 13) {  // timing dissection: stop after the packing
@@ -361,8 +363,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         return;
     }
     if (cd != ~0ull) {  // walked again: from the specific k-mer found off the first walk
-        S.atp = cd & ((1ull << 40) - 1);
-        S.aw = (uint32_t)(cd >> 40);
+        S.anc = cd;
         S.acls = NONE;  // genome from the position
         S.kind = LANE_WALK;
         return;
@@ -440,15 +441,13 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         if (a.queue_na) S.kind = LANE_NOANCHOR;
         return (void)LANE_HARD_WHY(3);
     }
-    S.atp = stp[0];
+    S.anc = stp[0] | ((uint64_t)sw(0) << 40);
     S.acls = scls[0];
-    S.aw = sw(0);
 #pragma unroll
     for (int i = 1; i < NSEED; i++)
         if (at == i) {
-            S.atp = stp[i];
+            S.anc = stp[i] | ((uint64_t)sw(i) << 40);
             S.acls = scls[i];
-            S.aw = sw(i);
         }
     // no specific seed: the first occurrence of a multi-genome seed k-mer may
     // lie in a sibling of the read's genome (a family member), whose variants
@@ -456,7 +455,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     // stretches: walk the one with the fewest mismatching bases (up to three)
     if (S.acls >= a.G) {
         // distinct candidate stretches (selects only: no runtime register indexing)
-        const int64_t e0 = (int64_t)S.atp - S.aw;
+        const int64_t e0 = (int64_t)(S.anc & kPosMask) - (int64_t)(S.anc >> 40);
         int64_t e1 = INT64_MIN, e2 = INT64_MIN;
         uint64_t t1 = 0, t2 = 0;
         uint32_t w1 = 0, c1 = 0, w2 = 0, c2 = 0;
@@ -495,9 +494,9 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             if (m1 < best) best = m1, bj = 1;
             if (m2 < best) best = m2, bj = 2;
             if (bj == 1) {
-                S.atp = t1, S.aw = w1, S.acls = c1;
+                S.anc = t1 | ((uint64_t)w1 << 40), S.acls = c1;
             } else if (bj == 2) {
-                S.atp = t2, S.aw = w2, S.acls = c2;
+                S.anc = t2 | ((uint64_t)w2 << 40), S.acls = c2;
             }
         }
     }
@@ -510,7 +509,8 @@ template <bool WIN_Q, bool MG>
 __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *row, LaneRead &S) {
     const int k = a.k;
     const uint32_t W = S.W, len = S.len;
-    const int64_t A = (int64_t)S.atp - (int64_t)S.aw;  // genome position of window 0
+    const uint64_t atp = S.anc & kPosMask;
+    const int64_t A = (int64_t)atp - (int64_t)(S.anc >> 40);  // genome position of window 0
     const bool in_tile = A >= 0 && (uint64_t)A + W <= a.tile_n;
     const uint64_t Ac = in_tile ? (uint64_t)A : 0;
     // every load of the walk is issued before anything waits: the walk blocks
@@ -520,7 +520,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     const uint32_t gr = (uint32_t)(2 * Ac & 63);
     uint64_t gw[kLaneWords + 1], pa3[3], pb3[3];
     lane_blocks<true>(a, Ac, len, gw, pa3, pb3);
-    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.gblk, S.atp);
+    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.gblk, atp);
     S.g = g;
     const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
     // every window of the read must lie inside the anchor genome
@@ -839,7 +839,8 @@ void k_align_lane(AlignArgs a) {
     const size_t cnt_bytes = lds ? ((size_t)G * 12 + 15) / 16 * 16 : 0;
     unsigned long long *first = (unsigned long long *)smem;
     uint32_t *uniq = (uint32_t *)(first + (lds ? G : 0));
-    LaneWave &LW = ((LaneWave *)(smem + cnt_bytes))[threadIdx.x >> 6];
+    // (the wave's index read from lane 0: the LDS base is then a scalar, not a VGPR held all kernel long)
+    LaneWave &LW = ((LaneWave *)(smem + cnt_bytes))[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     if (lds) {
         for (uint32_t i = threadIdx.x; i < G; i += kBlock) {
             first[i] = (unsigned long long)PA_NO_FIRST_KEY;
@@ -851,8 +852,11 @@ void k_align_lane(AlignArgs a) {
     // loop's bookkeeping lives in SGPRs (wave-uniform: chunk cursor, read
     // counts by ballot) and LDS (per-lane window counters), not in VGPRs.
     uint32_t n_uniq = 0, n_amb = 0, n_unm = 0, n_drop = 0;  // wave totals (scalar)
-    LW.n_hr[lane] = 0;
-    LW.n_qf[lane] = 0;
+    // window counters of the settled reads, wave totals (scalar): summed
+    // across the wave per chunk (a per-lane LDS slot kept its address live in
+    // a VGPR all kernel long, and it spilled)
+    uint64_t n_hr = 0, n_qf = 0;
+    LW.R[lane][kLaneWords] = 0;  // the zero word past every read (lane_prep writes words 0 .. kLaneWords - 1)
     // Each wave takes chunks of 64 consecutive reads; a read whose walk finds a
     // specific k-mer off it is walked again from that k-mer, but later, with 63
     // others (a list per wave), so that the 3 % of such reads do not hold whole
@@ -1008,11 +1012,9 @@ void k_align_lane(AlignArgs a) {
         n_unm += (uint32_t)__popcll(__ballot(S.kind == LANE_UNMAPPED));
         n_drop += (uint32_t)__popcll(__ballot(S.kind == LANE_DROP));
         const bool settled = S.kind == LANE_UNIQUE || S.kind == LANE_AMB || S.kind == LANE_UNMAPPED;
-        if (settled && S.hr) LW.n_hr[lane] += S.hr;
-        if (WIN_Q && settled && S.qf) LW.n_qf[lane] += S.qf;
+        if (MG) n_hr += wave_sum(settled ? S.hr : 0u);
+        if (WIN_Q) n_qf += wave_sum(settled ? S.qf : 0u);
     }
-    const uint32_t n_hr = wave_sum(LW.n_hr[lane]);
-    const uint32_t n_qf = WIN_Q ? wave_sum(LW.n_qf[lane]) : 0u;
     if (lane == 0) {
         if (n_uniq) atomicAdd(&a.stats[0], (unsigned long long)n_uniq);
         if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
@@ -1171,6 +1173,7 @@ template <bool NEED_Q, bool WIN_Q, bool MG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WAVES))) void k_align_lane_na(AlignArgs a) {
     __shared__ uint64_t rows[kBlock][kLaneWords + 1];
     __shared__ uint4 hcarry[4][kBlock];  // per lane: the last Bloom group's last sixteen 15-mer orders
+    rows[threadIdx.x][kLaneWords] = 0;  // the zero word past every read (lane_prep writes words 0 .. kLaneWords - 1)
     const int lane = lane_id();
     const int sh = 64 - 2 * a.k;
     const uint64_t n = *a.queue_na_count;
