@@ -73,6 +73,8 @@ struct AlignArgs {
     int mg_nb;                      // --max-genomes: the neighbour bits tell every present neighbour's set vs mg
     const uint32_t *gblk;           // the genome holding position j << 16 (tiled indexes)
     const uint64_t *bloom;          // Bloom filter of the keys (null: none), 2^bloom_lg words
+    const uint64_t *tile_rcp;       // reverse-complement plane (k_tile_rcp; null: none)
+    const uint32_t *tile_rcnb;      // reverse-complement one-substitution neighbour bits (null: none)
     uint32_t bloom_lg;
     int walk_rounds;
     int tpos_local;                 // slot.tpos genome-local (first_pos), else concatenated
@@ -100,6 +102,8 @@ struct AlignArgs {
     unsigned long long *queue_hard_count;
     uint32_t *queue_na;                    // lane kernel: reads with no seed in the index (null: to the wave kernel)
     unsigned long long *queue_na_count;
+    uint32_t *queue_na2;                   // k_align_lane_rc: the reads it could not walk on the reverse strand
+    unsigned long long *queue_na2_count;   //   (on to k_align_lane_na)
     uint64_t na_min;                       // fewer than this: k_align_lane_na hands them to the wave kernel
     const uint4 *qmask;                    // (quality filters) per read: windows failing --min-kmer-quality
     const uint8_t *qdrop;                  //   and 1 if the read fails --min-read-quality (k_quality_masks)
@@ -729,6 +733,21 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
         PA_HIP(hipGetLastError());
     }
     if (a.queue_na) {  // the reads without a seed in the index (count on the device)
+        AlignArgs b = a;
+        if (a.tile_rcp && a.bloom && a.queue_na2) {  // the reverse-strand walk first; the rest on to k_align_lane_na
+            auto rc = win_q ? (mg ? k_align_lane_rc<true, true, true> : k_align_lane_rc<true, true, false>)
+                    : need_q ? (mg ? k_align_lane_rc<true, false, true> : k_align_lane_rc<true, false, false>)
+                             : (mg ? k_align_lane_rc<false, false, true> : k_align_lane_rc<false, false, false>);
+            int rc_cu = 0;
+            PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&rc_cu, rc, kBlock, 0));
+            const unsigned rgrid = (unsigned)std::max<uint64_t>(
+                1, std::min<uint64_t>(want, (uint64_t)std::max(1, rc_cu) * (uint64_t)cus));
+            KernelTimer kt(prof, st, PA_PROF_LANE_RC);
+            hipLaunchKernelGGL(rc, dim3(rgrid), dim3(kBlock), 0, st, a);
+            PA_HIP(hipGetLastError());
+            b.queue_na = a.queue_na2;
+            b.queue_na_count = a.queue_na2_count;
+        }
         auto na = win_q ? (mg ? k_align_lane_na<true, true, true> : k_align_lane_na<true, true, false>)
                 : need_q ? (mg ? k_align_lane_na<true, false, true> : k_align_lane_na<true, false, false>)
                          : (mg ? k_align_lane_na<false, false, true> : k_align_lane_na<false, false, false>);
@@ -737,9 +756,8 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
         const unsigned ngrid = (unsigned)std::max<uint64_t>(
             1, std::min<uint64_t>(want, (uint64_t)std::max(1, na_cu) * (uint64_t)cus));
         KernelTimer kt(prof, st, PA_PROF_LANE_NA);
-        hipLaunchKernelGGL(na, dim3(ngrid), dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL(na, dim3(ngrid), dim3(kBlock), 0, st, b);
         PA_HIP(hipGetLastError());
-
     }
     return PA_OK;
 }
@@ -790,6 +808,10 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.gblk = idx->tile_gblk;
     a.bloom = idx->tile_cls ? idx->bloom : nullptr;
     a.bloom_lg = idx->bloom_lg;
+    a.tile_rcp = idx->tile_cls ? idx->tile_rcp : nullptr;
+    a.tile_rcnb = idx->tile_cls ? idx->tile_rcnb : nullptr;
+    if (const char *e = std::getenv("PA_NA_RCNB")) if (e[0] == '0') a.tile_rcnb = nullptr;
+    if (const char *e = std::getenv("PA_NA_RCWALK")) if (e[0] == '0') a.tile_rcp = nullptr;
     a.tile_n = idx->tile_cls ? idx->tile_n : 0;
     a.walk_rounds = 1;
     a.tpos_local = idx->tpos_local;
@@ -875,12 +897,14 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
     pa::dev_free(idx->queue);
     pa::dev_free(idx->queue_hard);
     pa::dev_free(idx->queue_na);
-    idx->queue = idx->queue_hard = idx->queue_na = nullptr;
+    pa::dev_free(idx->queue_na2);
+    idx->queue = idx->queue_hard = idx->queue_na = idx->queue_na2 = nullptr;
     idx->queue_cap = 0;
     PA_HIP(pa::dev_malloc(&idx->queue, n * 4));
     PA_HIP(pa::dev_malloc(&idx->queue_hard, n * 4));
     PA_HIP(pa::dev_malloc(&idx->queue_na, n * 4));
-    if (!idx->na_count) PA_HIP(pa::dev_malloc(&idx->na_count, 8));
+    PA_HIP(pa::dev_malloc(&idx->queue_na2, n * 4));
+    if (!idx->na_count) PA_HIP(pa::dev_malloc(&idx->na_count, 16));  // [0] k_align_lane_na's reads, [1] k_align_lane_rc's rest
     idx->queue_cap = n;
     return PA_OK;
 }
@@ -1044,9 +1068,11 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             if (const char *e = std::getenv("PA_LANE_NOANCHOR")) na = e[0] == '1';
             a.queue_na = na ? idx->queue_na : nullptr;
             a.queue_na_count = idx->na_count;
+            a.queue_na2 = idx->queue_na2;
+            a.queue_na2_count = idx->na_count + 1;
             a.na_min = 32768;  // (PA_NA_MIN: tests)
             if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
-            if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 8, st));
+            if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 16, st));
             PA_TRY(launch_lane(a, st, idx));
             a.rlist = idx->queue_hard;
             a.rlist_count = a.queue_hard_count;

@@ -184,6 +184,15 @@ pa_status pa_index_lookup(const pa_index *idx, const char *kmers, uint64_t n, ui
     return pa::index_lookup(idx, kmers, n, kmer_len, cls_out, size_out, as_stream(stream));
 }
 
+pa_status pa_index_positions(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, uint32_t flags,
+                             pa_kmer_hit *hits, uint64_t cap, uint64_t *n_hits, void *stream) {
+    PA_CHECK(idx && n_hits && (n == 0 || kmers), PA_EINVAL, "NULL argument");
+    PA_CHECK((flags & ~PA_POS_REVERSE) == 0, PA_EINVAL, "unknown flag bits");
+    PA_CHECK(n < PA_POS_RC_BIT, PA_EINVAL, "too many queries");
+    PA_HIP(hipSetDevice(idx->device));
+    return pa::index_positions(idx, kmers, n, kmer_len, flags, hits, cap, n_hits, as_stream(stream));
+}
+
 pa_status pa_index_class_genomes(const pa_index *idx, int64_t cls, uint32_t *genomes, uint32_t cap, uint32_t *n,
                                  void *stream) {
     PA_CHECK(idx && n, PA_EINVAL, "NULL argument");

@@ -299,6 +299,16 @@ __device__ __forceinline__ bool bloom_block_has(const uint4 &b, uint32_t h) {
     return (wv & bm) == bm;
 }
 
+// ---- reverse complements (2-bit codes: complement = code ^ 3) ----------------
+
+// The 32 2-bit groups of x in reverse order.
+__device__ __forceinline__ uint64_t rev_groups64(uint64_t x) {
+    const uint64_t y = __builtin_bitreverse64(x);
+    return ((y >> 1) & 0x5555555555555555ull) | ((y & 0x5555555555555555ull) << 1);
+}
+// Reverse complement of a single-word key of k <= 31 bases.
+__device__ __forceinline__ uint64_t rc_key(uint64_t key, int k) { return rev_groups64(~key) >> (64 - 2 * k); }
+
 // ---- wavefront (64-lane) helpers ------------------------------------------
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }

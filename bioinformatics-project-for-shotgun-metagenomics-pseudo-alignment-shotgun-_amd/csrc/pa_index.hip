@@ -632,10 +632,14 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 // occurrence's in words 3 (fo + j) + b, so the copy reads 3k consecutive words
 // (~6 128-B lines) instead of probing 3k keys (C5's families repeat about half
 // of their windows).
+// rc = 1 (tile_rcnb, 32-bit present words): the same for the neighbours'
+// REVERSE COMPLEMENTS, for k_align_lane_rc's reverse-strand walk -- a read
+// window that is the reverse complement of the genome's k-mer but for one base
+// is then resolved by one bit, as a forward one by tile_nb.
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
                            const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
                            const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local,
-                           int pass, const uint64_t *__restrict__ bloom, uint32_t bloom_lg) {
+                           int pass, const uint64_t *__restrict__ bloom, uint32_t bloom_lg, int rc) {
     unsigned long long *nb = (unsigned long long *)nb_out;  // full: 64-bit words, present | specific << 32
     uint32_t *nb32 = (uint32_t *)nb_out;                    // else 32-bit words, present
     const int sh = 64 - 2 * k;
@@ -672,7 +676,10 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
             uint64_t keys[3];
             uint32_t cls3[3];
 #pragma unroll
-            for (int b = 0; b < 3; b++) keys[b] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
+            for (int b = 0; b < 3; b++) {
+                keys[b] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
+                if (rc) keys[b] = rc_key(keys[b], k);  // (tile_rcnb: the neighbour's reverse complement)
+            }
             uint32_t act = 7u;
             if (bloom) {  // surely absent neighbours are not probed; most share the window's Bloom line
 #pragma unroll
@@ -706,6 +713,40 @@ __global__ void k_bloom_build(const Slot<1> *__restrict__ table, uint64_t cap, u
         uint64_t w, m;
         bloom_word(key, k, lg, w, m);
         atomicOr((unsigned long long *)&bloom[w], (unsigned long long)m);
+    }
+}
+
+// The reverse-complement plane of the genome tiling, for k_align_lane_na's
+// reverse-strand walk (pa_lane.h): bit i of rcp[j] is 0 iff position t = 64 j +
+// i starts an indexed window whose reverse complement is NOT a key -- then a
+// read window that is the reverse complement of the genome's k-mer at t is
+// shown absent without a lookup.  1 where no indexed window starts (N, genome
+// end, padding): such a read window is looked up.  One wave per 64 positions,
+// the Bloom filter first (most reverse complements are absent), then the table.
+__global__ __launch_bounds__(256) void k_tile_rcp(const uint32_t *__restrict__ tile_cls, const uint64_t *__restrict__ pk,
+                                                  uint64_t n, int k, const Slot<1> *__restrict__ table, HomeCfg hc,
+                                                  const uint64_t *__restrict__ bloom, uint32_t bloom_lg,
+                                                  uint64_t *__restrict__ rcp, uint64_t n_blocks) {
+    const uint32_t lane = threadIdx.x & 63;
+    const int sh = 64 - 2 * k;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n_blocks; j += nw) {
+        const uint64_t t = 64 * j + lane;
+        bool maybe = true;
+        if (t < n && tile_cls[t] != NONE) {
+            Key<1> kk;
+            kk.w[0] = rc_key(get64_at(pk, 2 * t) >> sh, k);
+            if (bloom) {
+                uint64_t wi, bm;
+                bloom_word(kk.w[0], k, bloom_lg, wi, bm);
+                maybe = (bloom[wi] & bm) == bm;
+            }
+            uint64_t slot;
+            uint32_t cls, tpos;
+            if (maybe) maybe = table_find<1>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos);
+        }
+        const uint64_t b = __ballot(maybe);
+        if (lane == 0) rcp[j] = b;
     }
 }
 
@@ -1060,8 +1101,23 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                 hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
                                    st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
                                    idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
-                                   pass, bb, bb_lg);
+                                   pass, bb, bb_lg, 0);
                 phase_mark(pass == 0 ? "nb: first occurrences" : "nb: copies");
+            }
+            // the reverse-complement neighbour bits (tile_rcnb, 12 B per base)
+            // when they leave a quarter of the free memory; PA_NO_RCNB=1: none
+            const char *no_rcnb = std::getenv("PA_NO_RCNB");
+            size_t fr_b = 0, tr_b = 0;
+            if (k <= 31 && !(no_rcnb && no_rcnb[0] == '1') && pa::dev_mem_info(&fr_b, &tr_b) == hipSuccess &&
+                n * 12 <= fr_b / 4 * 3 && pa::dev_malloc(&idx->tile_rcnb, n * 12 + 64) == hipSuccess) {
+                B_HIP(hipMemsetAsync(idx->tile_rcnb, 0, n * 12 + 64, st));
+                for (int pass = 0; pass < 2; pass++)
+                    hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
+                                       st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                       (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff, idx->tpos_local,
+                                       pass, bb, bb_lg, 1);
+                idx->device_bytes += n * 12;
+                phase_mark("nb: reverse complements");
             }
             if (bb) {
                 B_HIP(hipStreamSynchronize(st));
@@ -1177,6 +1233,19 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 }
                 phase_mark("Bloom");
             }
+            {  // the reverse-complement plane (k_tile_rcp), 1 bit per base; PA_NO_RCP=1: none
+                const char *nr = std::getenv("PA_NO_RCP");
+                const uint64_t n_blocks = n / 64 + 5;  // padded like the walk blocks
+                if (!(nr && nr[0] == '1') && pa::dev_malloc(&idx->tile_rcp, n_blocks * 8) == hipSuccess) {
+                    hipLaunchKernelGGL(k_tile_rcp, dim3((unsigned)std::min<uint64_t>((n_blocks + 3) / 4, 1u << 20)),
+                                       dim3(256), 0, st, idx->tile_cls, idx->tile_pk, n, k, (const Slot<1> *)table,
+                                       idx->home, idx->bloom, idx->bloom_lg, idx->tile_rcp, n_blocks);
+                    idx->device_bytes += n_blocks * 8;
+                } else {
+                    idx->tile_rcp = nullptr;
+                }
+                phase_mark("reverse-complement plane");
+            }
         }
         B_HIP(hipGetLastError());
         B_HIP(hipStreamSynchronize(st));
@@ -1228,11 +1297,15 @@ void index_release(pa_index *idx) {
     idx->tile_big_mg = -1;
     pa::dev_free(idx->tile_nb);
     idx->tile_nb = nullptr;
+    pa::dev_free(idx->tile_rcnb);
+    idx->tile_rcnb = nullptr;
     pa::dev_free(idx->tile_nbbig);
     idx->tile_nbbig = nullptr;
     idx->tile_nbbig_mg = -1;
     pa::dev_free(idx->bloom);
     idx->bloom = nullptr;
+    pa::dev_free(idx->tile_rcp);
+    idx->tile_rcp = nullptr;
     pa::dev_free(idx->tile_gblk);
     idx->tile_gblk = nullptr;
     idx->bloom_lg = 0;
@@ -1242,6 +1315,8 @@ void index_release(pa_index *idx) {
     pa::dev_free(idx->queue);
     pa::dev_free(idx->queue_hard);
     pa::dev_free(idx->queue_na);
+    pa::dev_free(idx->queue_na2);
+    idx->queue_na2 = nullptr;
     pa::dev_free(idx->na_count);
     pa::dev_free(idx->qmask);
     pa::dev_free(idx->qdrop);
@@ -1279,9 +1354,10 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
     idx->nb_skip = 0;
     if (rc != PA_OK) {  // the index stays usable without its align-side view
         pa::dev_free(idx->tile_cls); pa::dev_free(idx->tile_pk); pa::dev_free(idx->tile_lw); pa::dev_free(idx->tile_nb);
-        pa::dev_free(idx->tile_gblk); pa::dev_free(idx->bloom);
+        pa::dev_free(idx->tile_gblk); pa::dev_free(idx->bloom); pa::dev_free(idx->tile_rcp); pa::dev_free(idx->tile_rcnb);
+        idx->tile_rcnb = nullptr;
         idx->tile_cls = nullptr, idx->tile_pk = nullptr, idx->tile_lw = nullptr, idx->tile_nb = nullptr;
-        idx->tile_gblk = nullptr, idx->bloom = nullptr, idx->bloom_lg = 0, idx->tile_n = 0;
+        idx->tile_gblk = nullptr, idx->bloom = nullptr, idx->bloom_lg = 0, idx->tile_n = 0, idx->tile_rcp = nullptr;
     }
     return rc;
 }

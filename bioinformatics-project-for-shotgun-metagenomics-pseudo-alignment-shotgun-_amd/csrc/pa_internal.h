@@ -105,6 +105,7 @@ struct pa_index {
     int64_t tile_big_mg = -1;          // the --max-genomes value tile_big was made for (-1: none)
     void *tile_nb = nullptr;           // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional:
     int nb_spec = 0;                   //   1: 64-bit words, present | specific << 32; 0: 32-bit words, present
+    uint32_t *tile_rcnb = nullptr;     // [3 tile_n] the same for the neighbours' reverse complements (present), optional
     uint32_t *tile_nbbig = nullptr;    // [3 tile_n] neighbour present with a set > tile_nbbig_mg (pa_align, cached)
     int64_t tile_nbbig_mg = -1;
     int nb_skip = 0;                   // (index_prepare) make the tiles without the neighbour bits
@@ -112,13 +113,16 @@ struct pa_index {
     uint64_t reads_seen = 0;           // reads aligned so far (the neighbour bits follow at kNbReadsPerBase)
     uint32_t *tile_gblk = nullptr;     // [(tile_n >> 16) + 2] the genome holding position j << 16
     uint64_t *bloom = nullptr;         // [2^bloom_lg] Bloom filter of the table's keys (k_bloom_build), optional
+    uint64_t *tile_rcp = nullptr;      // [tile_n / 64 + 5] bit t: the reverse complement of the k-mer at t may be
+                                       //   a key (present, or no indexed window at t) -- k_tile_rcp, optional
     uint32_t bloom_lg = 0;
     uint64_t device_bytes = 0;
     // align scratch
     pa::Workspace ws;
     uint32_t *queue = nullptr;         // read indices deferred to the exact kernel
     uint32_t *queue_hard = nullptr;    // read indices the lane kernel leaves to the wave kernel
-    uint32_t *queue_na = nullptr;      // read indices the lane kernel found no seed for (k_align_lane_na)
+    uint32_t *queue_na = nullptr;      // read indices the lane kernel found no seed for (k_align_lane_rc / _na)
+    uint32_t *queue_na2 = nullptr;     // those k_align_lane_rc could not walk on the reverse strand (k_align_lane_na)
     uint4 *qmask = nullptr;            // per read: windows failing --min-kmer-quality (k_quality_masks)
     uint8_t *qdrop = nullptr;          // per read: fails --min-read-quality
     uint64_t qmask_cap = 0;
@@ -172,6 +176,8 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint = ~0u
 pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st);
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
                        uint32_t *size_out, hipStream_t st);
+pa_status index_positions(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, uint32_t flags,
+                          pa_kmer_hit *hits, uint64_t cap, uint64_t *n_hits, hipStream_t st);
 pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint32_t n_groups, uint64_t *total,
                              uint64_t *uniq, uint64_t *inter, hipStream_t st);
 pa_status reads_synthesize(const pa_index *idx, pa_reads *r, uint64_t n, uint32_t len, uint64_t first,

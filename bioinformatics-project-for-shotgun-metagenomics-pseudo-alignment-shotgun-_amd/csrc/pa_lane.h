@@ -1057,15 +1057,14 @@ constexpr size_t lane_lds_bytes(uint32_t G) {
 #ifndef PA_NA_GROUP
 #define PA_NA_GROUP 8
 #endif
-#ifndef PA_NA_PROBES
-#define PA_NA_PROBES 4
-#endif
 __device__ __forceinline__ uint64_t bits128(uint64_t x0, uint64_t x1, int s) {  // (s constant after unrolling)
     return s == 0 ? x0 : ((x0 << s) | (x1 >> (64 - s)));
 }
-template <int NAG, int KC>  // KC: k known at compile time (31, the benchmark k), else 0
+// CARRY false: a group on its own (k_align_lane_rc's cooperative passes): all
+// its 15-mer orders computed, its first run loaded, no LDS carry.
+template <int NAG, int KC, bool CARRY = true>  // KC: k known at compile time (31, the benchmark k), else 0
 __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64_t *row, uint32_t w0, uint32_t act,
-                                                uint32_t &prev_blk, uint4 &cur, uint4 (*hc)[kBlock]) {
+                                                bool fresh, uint32_t &prev_blk, uint4 &cur, uint4 (*hc)[kBlock]) {
     static_assert(NAG == 8 || NAG == 16, "a group's bases are 128 bits from a multiple of 16");
     const int k = KC ? KC : a.k, sh = 64 - 2 * k;
     const int mm = k < 15 ? k : 15;
@@ -1086,16 +1085,23 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
     // (hc: the lane's sixteen in LDS, [i][thread]: no bank conflicts)
     uint32_t h[NAG + 16];
     const uint32_t t = threadIdx.x;
+    if (CARRY) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) {  // (the caller stores a read's first sixteen before its first group)
-        const uint4 v = hc[i][t];
-        h[4 * i] = v.x, h[4 * i + 1] = v.y, h[4 * i + 2] = v.z, h[4 * i + 3] = v.w;
+        for (int i = 0; i < 4; i++) {  // (the caller stores a read's first sixteen before its first group)
+            const uint4 v = hc[i][t];
+            h[4 * i] = v.x, h[4 * i + 1] = v.y, h[4 * i + 2] = v.z, h[4 * i + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < 16; p++) h[p] = mm_order((uint32_t)(bits128(X0, X1, 2 * p) >> (64 - 2 * mm)));
     }
 #pragma unroll
     for (int p = 16; p < NAG + 16; p++) h[p] = mm_order((uint32_t)(bits128(X0, X1, 2 * p) >> (64 - 2 * mm)));
+    if (CARRY) {
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-        hc[i][t] = make_uint4(h[NAG + 4 * i], h[NAG + 4 * i + 1], h[NAG + 4 * i + 2], h[NAG + 4 * i + 3]);
+        for (int i = 0; i < 4; i++)
+            hc[i][t] = make_uint4(h[NAG + 4 * i], h[NAG + 4 * i + 1], h[NAG + 4 * i + 2], h[NAG + 4 * i + 3]);
+    }
     // each window's minimum: with S >= 9 every window j < 8 holds 15-mers 7
     // and 8 .. j + S - 1, so it is min(suffix minimum from j to 7, prefix
     // minimum from 7 to j + S - 1)
@@ -1129,7 +1135,7 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
     for (int j = 0; j < NAG; j++) {
         blk[j] = (uint32_t)bloom_block(mn[j], a.bloom_lg);
         const uint32_t before = j ? blk[j - 1] : prev_blk;
-        news |= (blk[j] != before || (j == 0 && w0 == 0)) ? 1u << j : 0u;
+        news |= (blk[j] != before || (j == 0 && fresh)) ? 1u << j : 0u;
     }
     // (no load for a run none of whose windows is looked up; the group's last
     // run may go on in the next group, which then tests against `cur`)
@@ -1164,6 +1170,205 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
         }
     }
     return act;
+}
+
+// The first sixteen 15-mer orders of a Bloom group at window w0 (a multiple of
+// the group size): a read's first group, or the first after groups skipped.
+__device__ __forceinline__ void na_hc_init(const uint64_t *row, uint32_t w0, int k, uint4 (*hc)[kBlock]) {
+    const int mm = k < 15 ? k : 15;
+    const uint32_t o = 2 * w0, q = o >> 6, r = o & 63;
+    uint64_t X0 = row[q], X1 = row[q + 1];
+    if (r) {
+        const uint64_t X2 = row[q + 2];
+        X0 = (X0 << r) | (X1 >> (64 - r));
+        X1 = (X1 << r) | (X2 >> (64 - r));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t v[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = mm_order((uint32_t)(bits128(X0, X1, 2 * (4 * i + e)) >> (64 - 2 * mm)));
+        hc[i][threadIdx.x] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// Reverse-strand walk of a read with no seed in the index (k <= 31).  Such a
+// read is most often the reverse complement of a stretch of some genome (about
+// half of a real FASTQ): its reverse complement R' is then walked like a
+// forward read -- a seed (R' window 0, the reverse complement of the read's
+// last window; else R' window W - 1, of its first) gives the anchor A, R' is
+// compared with the genome words of the walk blocks from A on.  Read window w
+// is the reverse complement of R' window w' = W - 1 - w, and where the genome
+// window at A + w' is indexed:
+//   * R' window w' equals it: read window w is absent unless the
+//     reverse-complement plane (k_tile_rcp) has its bit set;
+//   * R' window w' differs from it in exactly one base: the reverse-complement
+//     neighbour bits (tile_rcnb) say whether read window w is present;
+// every other window (two or more mismatches, more than 8 mismatching bases,
+// an unindexed genome window, a bit set) is left to look up.  Returns in
+// lk0 / lk1 the read's windows still to look up and true; false when no
+// anchor is found or R' differs from the stretch in more than kRcMaxMis bases.
+// Exact: it only removes windows shown absent.
+constexpr uint32_t kRcMaxMis = 16;
+__device__ __forceinline__ bool na_rc_walk(const AlignArgs &a, const uint64_t *row, uint32_t len, uint32_t W,
+                                           uint64_t &lk0, uint64_t &lk1) {
+    const int k = a.k, sh = 64 - 2 * k;
+    // the seeds, one probe each: R' window 0 first, W - 1 only if it is absent
+    uint64_t sk[2];
+    sk[0] = rc_key(row_bits(row, 2 * (W - 1)) >> sh, k);
+    sk[1] = rc_key(row_bits(row, 0) >> sh, k);
+    uint32_t f, cl[2], tp[2];
+    lane_probe<2>(a, sk, 1u, f, cl, tp);
+    int64_t A = -1;
+    if (bit(f, 0) && tp[0] != NONE) {
+        A = (int64_t)first_pos(cl[0], tp[0], a.G, a.class_genomes, a.goff, a.tpos_local);
+    } else {
+        lane_probe<2>(a, sk, 2u, f, cl, tp);
+        if (bit(f, 1) && tp[1] != NONE)
+            A = (int64_t)first_pos(cl[1], tp[1], a.G, a.class_genomes, a.goff, a.tpos_local) - (int64_t)(W - 1);
+    }
+    if (A < 0 || (uint64_t)A + len > a.tile_n) return false;
+    const uint64_t Au = (uint64_t)A;
+    uint64_t gw[kLaneWords + 1], pa3[3], pb3[3];
+    lane_blocks<true>(a, Au, len, gw, pa3, pb3);
+    const uint64_t *rp = a.tile_rcp + (Au >> 6);
+    const uint64_t q0 = rp[0], q1 = rp[1], q2 = rp[2];
+    const uint32_t fr = (uint32_t)(Au & 63);
+    auto shifted = [fr](uint64_t x0, uint64_t x1) { return fr ? (x0 >> fr) | (x1 << (64 - fr)) : x0; };
+    const uint64_t IX0 = shifted(pa3[0], pa3[1]) | shifted(pb3[0], pb3[1]);  // indexed genome windows
+    const uint64_t IX1 = shifted(pa3[1], pa3[2]) | shifted(pb3[1], pb3[2]);
+    const uint32_t gr = (uint32_t)(2 * Au & 63);
+    const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;
+    const uint64_t tail = rl >= 32 ? ~0ull : ~0ull << (64 - 2 * rl);
+    const bool has_nb = a.tile_rcnb != nullptr;
+    uint64_t U0 = 0, U1 = 0, V0 = 0, V1 = 0, NP0 = 0, NP1 = 0;
+    uint64_t epk = 0;  // positions e of the mismatches to look up in the neighbour bits (8 bits each, <= 8)
+    uint32_t cpk = 0;  //   their substitution index (cr - cg - 1) & 3 (2 bits each)
+    uint32_t nnb = 0, nmis = 0;
+#pragma unroll
+    for (int i = 0; i < kLaneWords; i++) {
+        if (32 * i >= (int)len) break;
+        // R' word i: the read's bases len - 1 - 32 i down to len - 32 - 32 i,
+        // complemented (bases before the read's start read as zeros: past the
+        // end of R', masked by `tail`)
+        const int32_t o = (int32_t)len - 32 - 32 * i;
+        const uint64_t c = o >= 0 ? row_bits(row, 2 * (uint32_t)o) : row[0] >> (-2 * o);
+        const uint64_t rw = rev_groups64(~c);
+        const uint64_t gwi = gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i];
+        uint64_t d = rw ^ gwi;
+        if ((uint32_t)i == qlast) d &= tail;
+        uint64_t m = (d | (d >> 1)) & 0x5555555555555555ull;
+        while (m) {
+            const uint32_t j = __builtin_clzll(m) >> 1, e = 32 * i + j;
+            m &= ~(1ull << (62 - 2 * j));
+            const int32_t lo = (int32_t)e - k + 1 < 0 ? 0 : (int32_t)e - k + 1;
+            const int32_t hi = (int32_t)e < (int32_t)W - 1 ? (int32_t)e : (int32_t)W - 1;
+            if (lo > hi) continue;
+            const uint64_t r0 = lo < 64 ? ((~0ull << lo) & (hi >= 63 ? ~0ull : ((2ull << hi) - 1))) : 0ull;
+            const uint64_t r1 =
+                hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) & (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
+                         : 0ull;
+            if (++nmis > kRcMaxMis) return false;
+            V0 |= U0 & r0;
+            V1 |= U1 & r1;
+            U0 |= r0;
+            U1 |= r1;
+            if (has_nb && nnb < 8 && ((r0 & IX0) | (r1 & IX1))) {
+                const uint32_t cg = (uint32_t)(gwi >> (62 - 2 * j)) & 3u, cr = (uint32_t)(rw >> (62 - 2 * j)) & 3u;
+                epk |= (uint64_t)e << (8 * nnb);
+                cpk |= ((cr - cg - 1) & 3u) << (2 * nnb);
+                nnb++;
+            } else {
+                V0 |= r0;  // (no bits for it: its windows are looked up)
+                V1 |= r1;
+            }
+        }
+    }
+    // the neighbour words of the mismatches, four loads in flight at a time
+#pragma unroll 1
+    for (uint32_t b0 = 0; b0 < nnb; b0 += 4) {
+        uint32_t nv[4];
+        int32_t sf[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t q = b0 + u < nnb ? b0 + u : b0;
+            const uint32_t e = (uint32_t)(epk >> (8 * q)) & 255u, c = (cpk >> (2 * q)) & 3u;
+            nv[u] = a.tile_rcnb[3 * (Au + e) + c];
+            sf[u] = b0 + u < nnb ? (int32_t)e - k + 1 : 1000;  // bit q of the word <-> window e - k + 1 + q
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (sf[u] == 1000) continue;
+            const uint64_t nbw = nv[u];
+            const int32_t sft = sf[u];
+            if (sft >= 0) {
+                NP0 |= sft < 64 ? nbw << sft : 0ull;
+                NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 32 ? nbw >> (64 - sft) : 0ull);
+            } else {
+                NP0 |= nbw >> (-sft);
+            }
+        }
+    }
+    const uint64_t RP0 = shifted(q0, q1), RP1 = shifted(q1, q2);
+    const uint64_t in0 = W >= 64 ? ~0ull : ((1ull << W) - 1);
+    const uint64_t in1 = W <= 64 ? 0ull : (W >= 128 ? ~0ull : ((1ull << (W - 64)) - 1));
+    // R' windows to look up: unindexed genome windows; equal ones whose plane
+    // bit is set; one mismatch and the neighbour present; two or more
+    const uint64_t N0 = in0 & (~IX0 | (~U0 & RP0) | (U0 & (V0 | NP0)));
+    const uint64_t N1 = in1 & (~IX1 | (~U1 & RP1) | (U1 & (V1 | NP1)));
+    // read window w = W - 1 - w': the 128-bit mask reversed, shifted down by 128 - W
+    uint64_t lo = __builtin_bitreverse64(N1), hi = __builtin_bitreverse64(N0);
+    const uint32_t s = 128 - W;
+    if (s >= 64) {
+        lo = hi >> (s - 64);
+        hi = 0;
+    } else if (s) {
+        lo = (lo >> s) | (hi << (64 - s));
+        hi >>= s;
+    }
+    lk0 = lo;
+    lk1 = hi;
+    return true;
+}
+
+// The table probes of a lane's remaining windows (bit w of pm0 | pm1 << 64:
+// Bloom false positives, the rare present k-mer): each lane its own next NPB
+// windows, so a wave probes as often as its lane with the most (~1.3 rounds
+// on c2rc, where probing per group took ~30: some lane has a false positive in
+// almost every group).  spec: a specific k-mer found (the read goes to the
+// wave kernel); noff: multi-genome ones; hr: above --max-genomes.
+#ifndef PA_NA_PROBES
+#define PA_NA_PROBES 4
+#endif
+template <bool MG>
+__device__ __forceinline__ void na_probe_rest(const AlignArgs &a, const uint64_t *row, uint64_t pm0, uint64_t pm1,
+                                              bool &spec, uint32_t &noff, uint32_t &hr) {
+    const int sh = 64 - 2 * a.k;
+    constexpr int NPB = PA_NA_PROBES;
+#pragma unroll 1
+    while ((pm0 | pm1) && !spec) {
+        uint64_t key[NPB];
+        uint32_t act8 = 0;
+#pragma unroll
+        for (int j = 0; j < NPB; j++) {
+            const bool lo = pm0 != 0;
+            const uint64_t m = lo ? pm0 : pm1;
+            const uint32_t w = (lo ? 0u : 64u) + (uint32_t)__builtin_ctzll(m | (1ull << 63));
+            act8 |= m ? 1u << j : 0u;
+            key[j] = m ? row_bits(row, 2 * w) >> sh : 0ull;
+            if (lo) pm0 &= pm0 - 1;
+            else pm1 &= pm1 - 1;
+        }
+        uint32_t f, cl[NPB], tp[NPB];
+        lane_probe<NPB>(a, key, act8, f, cl, tp);
+#pragma unroll
+        for (int j = 0; j < NPB; j++) {
+            if (!bit(f, j)) continue;
+            if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
+            else if (cl[j] >= a.G) noff++;
+            else spec = true;
+        }
+    }
 }
 
 #ifndef PA_NA_WAVES
@@ -1202,22 +1407,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
             constexpr int NAG = PA_NA_GROUP;
             uint32_t prev_blk = 0;
             uint4 cur = make_uint4(0, 0, 0, 0);
-            if (a.bloom) {  // the read's first sixteen 15-mer orders, for its first Bloom group
-                const int mm = a.k < 15 ? a.k : 15;
-                const uint64_t X0 = row[0], X1 = row[1];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    uint32_t v[4];
-#pragma unroll
-                    for (int e = 0; e < 4; e++)
-                        v[e] = mm_order((uint32_t)(bits128(X0, X1, 2 * (4 * i + e)) >> (64 - 2 * mm)));
-                    hcarry[i][threadIdx.x] = make_uint4(v[0], v[1], v[2], v[3]);
-                }
-            }
             // the windows to look up (bit w of pm0 | pm1 << 64): every window
             // (W <= kLaneMaxW = 128) but those failing --min-kmer-quality, less
-            // those the Bloom filter shows absent
+            // those the Bloom filter shows absent.  A group with none is
+            // skipped; the next group then starts a new minimizer run
             uint64_t pm0 = 0, pm1 = 0;
+            bool fresh = true;
 #pragma unroll 1
             for (uint32_t w0 = 0; w0 < W; w0 += NAG) {
                 uint32_t act = 0;
@@ -1227,42 +1422,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
                     const bool filt = WIN_Q && (((w < 64 ? S.F0 >> w : S.F1 >> (w - 64)) & 1ull) != 0);
                     act |= (w < W && !filt) ? 1u << j : 0u;
                 }
-                if (a.bloom)  // keys surely absent are not looked up
-                    act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, prev_blk, cur, hcarry)
-                                    : bloom_group<NAG, 0>(a, row, w0, act, prev_blk, cur, hcarry);
+                if (!act) {
+                    fresh = true;
+                    continue;
+                }
+                if (a.bloom) {  // keys surely absent are not looked up
+                    if (fresh) na_hc_init(row, w0, a.k, hcarry);  // (the group's first sixteen 15-mer orders)
+                    act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, fresh, prev_blk, cur, hcarry)
+                                    : bloom_group<NAG, 0>(a, row, w0, act, fresh, prev_blk, cur, hcarry);
+                }
+                fresh = false;
                 if (w0 < 64) pm0 |= (uint64_t)act << w0;
                 else pm1 |= (uint64_t)act << (w0 - 64);
             }
             // then the table for the rest (Bloom false positives, the rare
-            // present k-mer): each lane its own next NPB windows, so a wave
-            // probes as often as its lane with the most (~1.3 rounds on c2rc,
-            // where probing per group took ~30: some lane has a false positive
-            // in almost every group)
-            constexpr int NPB = PA_NA_PROBES;
-#pragma unroll 1
-            while ((pm0 | pm1) && !spec) {
-                uint64_t key[NPB];
-                uint32_t act8 = 0;
-#pragma unroll
-                for (int j = 0; j < NPB; j++) {
-                    const bool lo = pm0 != 0;
-                    const uint64_t m = lo ? pm0 : pm1;
-                    const uint32_t w = (lo ? 0u : 64u) + (uint32_t)__builtin_ctzll(m | (1ull << 63));
-                    act8 |= m ? 1u << j : 0u;
-                    key[j] = m ? row_bits(row, 2 * w) >> sh : 0ull;
-                    if (lo) pm0 &= pm0 - 1;
-                    else pm1 &= pm1 - 1;
-                }
-                uint32_t f, cl[NPB], tp[NPB];
-                lane_probe<NPB>(a, key, act8, f, cl, tp);
-#pragma unroll
-                for (int j = 0; j < NPB; j++) {
-                    if (!bit(f, j)) continue;
-                    if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
-                    else if (cl[j] >= a.G) noff++;
-                    else spec = true;
-                }
-            }
+            // present k-mer)
+            na_probe_rest<MG>(a, row, pm0, pm1, spec, noff, hr);
             S.kind = spec ? LANE_HARD : (noff ? LANE_AMB : LANE_UNMAPPED);
             if (!spec) {
                 hr_sum += hr;
@@ -1279,6 +1454,131 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
         }
         n_amb += (uint32_t)__popcll(__ballot(S.kind == LANE_AMB));
         n_unm += (uint32_t)__popcll(__ballot(S.kind == LANE_UNMAPPED));
+    }
+    const uint32_t hr_w = wave_sum(hr_sum);
+    const uint32_t qf_w = WIN_Q ? wave_sum(qf_sum) : 0u;
+    if (lane == 0) {
+        if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
+        if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
+        if (MG && hr_w) atomicAdd(&a.stats[5], (unsigned long long)hr_w);
+        if (WIN_Q && qf_w) atomicAdd(&a.stats[4], (unsigned long long)qf_w);
+    }
+}
+
+// k_align_lane_rc: the reads k_align_lane found no seed for, walked on the
+// reverse strand first (na_rc_walk) -- about half of a real FASTQ is the
+// reverse complement of some genome stretch, and the forward-only lookups of
+// the reference (src/kmer.py:419-429) must show every one of its windows
+// absent.  A read the walk anchors needs the Bloom filter only for its
+// windows that differ from the stretch or whose plane bit is set (~25 of
+// ~120 at 0.5 % errors); the rest go on to k_align_lane_na (a.queue_na2),
+// which tests every window.  The reads' counts vary a lot (0 ... 120 windows),
+// so the Bloom groups are tested by the whole wave together: every lane lists
+// its read's groups with a window to look up, the lists are concatenated in
+// LDS and each pass takes 64 groups, one per lane (bloom_group without the
+// carry: each group's 15-mer orders computed on their own).  Then each lane
+// probes its read's remaining windows (na_probe_rest) and settles it as
+// k_align_lane_na does.
+constexpr int kRcGroups = kLaneMaxW / 8;  // Bloom groups of 8 windows per read
+template <bool NEED_Q, bool WIN_Q, bool MG>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WAVES))) void k_align_lane_rc(AlignArgs a) {
+    __shared__ uint64_t rows[kBlock][kLaneWords + 1];
+    __shared__ uint32_t glist[kWaves][64 * kRcGroups];      // (lane << 16) | (group << 8) | windows of the group
+    __shared__ unsigned long long pmask[kBlock][2];          // per lane: windows the Bloom filter lets through
+    rows[threadIdx.x][kLaneWords] = 0;
+    const int lane = lane_id();
+    const uint32_t wv = threadIdx.x >> 6, wbase = threadIdx.x & ~63u;
+    const uint64_t n = *a.queue_na_count;
+    const bool forward = n < a.na_min;  // (few such reads: all on to k_align_lane_na, which hands them on)
+    uint32_t n_amb = 0, n_unm = 0;
+    uint32_t hr_sum = 0, qf_sum = 0;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock + wbase; c0 < n; c0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i = c0 + lane;
+        LaneRead S;
+        S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
+        uint32_t r = 0;
+        if (i < n) {
+            r = a.queue_na[i];
+            if (forward) S.kind = LANE_NOANCHOR;
+            else lane_prep<NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
+        }
+        const uint64_t *row = rows[threadIdx.x];
+        uint32_t gm = 0;  // groups with a window to look up
+        uint64_t lk0 = 0, lk1 = 0;
+        if (S.kind == LANE_WALK) {
+            if (na_rc_walk(a, row, S.len, S.W, lk0, lk1)) {
+                if (WIN_Q) {  // windows failing --min-kmer-quality are never looked up
+                    lk0 &= ~S.F0;
+                    lk1 &= ~S.F1;
+                }
+#pragma unroll
+                for (int g = 0; g < kRcGroups; g++)
+                    gm |= (((g < 8 ? lk0 >> (8 * g) : lk1 >> (8 * g - 64)) & 0xFFull) != 0) ? 1u << g : 0u;
+            } else {
+                S.kind = LANE_NOANCHOR;
+            }
+        }
+        // the wave's groups, concatenated
+        const uint32_t c = (uint32_t)__popc(gm);
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t total = __shfl(incl, 63);
+        pmask[threadIdx.x][0] = 0;
+        pmask[threadIdx.x][1] = 0;
+        {
+            uint32_t e = incl - c, m = gm;
+            while (m) {
+                const uint32_t g = (uint32_t)__builtin_ctz(m);
+                m &= m - 1;
+                const uint32_t wins = (uint32_t)((g < 8 ? lk0 >> (8 * g) : lk1 >> (8 * g - 64)) & 0xFFull);
+                glist[wv][e++] = ((uint32_t)lane << 16) | (g << 8) | wins;
+            }
+        }
+        wave_sync();
+        // every pass: 64 groups, one per lane (k <= 31 on this path)
+#pragma unroll 1
+        for (uint32_t base = 0; base < total; base += 64) {
+            const uint32_t e = base + lane;
+            if (e < total) {
+                const uint32_t t = glist[wv][e];
+                const uint32_t l = t >> 16, g = (t >> 8) & 255u, act = t & 255u;
+                uint32_t pb = 0;
+                uint4 cur = make_uint4(0, 0, 0, 0);
+                const uint32_t got = a.k == 31
+                                         ? bloom_group<8, 31, false>(a, rows[wbase + l], 8 * g, act, true, pb, cur, nullptr)
+                                         : bloom_group<8, 0, false>(a, rows[wbase + l], 8 * g, act, true, pb, cur, nullptr);
+                if (got) atomicOr(&pmask[wbase + l][g >> 3], (unsigned long long)got << (8 * (g & 7)));
+            }
+        }
+        wave_sync();
+        if (S.kind == LANE_WALK) {
+            bool spec = false;
+            uint32_t noff = 0, hr = 0;
+            na_probe_rest<MG>(a, row, pmask[threadIdx.x][0], pmask[threadIdx.x][1], spec, noff, hr);
+            S.kind = spec ? LANE_HARD : (noff ? LANE_AMB : LANE_UNMAPPED);
+            if (!spec) {
+                hr_sum += hr;
+                qf_sum += S.qf;
+            }
+        }
+        const bool hard = S.kind == LANE_HARD;
+        const uint64_t hb = __ballot(hard);
+        if (hb) {
+            uint64_t qbase = 0;
+            if (lane == __builtin_ctzll(hb)) qbase = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
+            qbase = shfl64(qbase, __builtin_ctzll(hb));
+            if (hard) a.queue_hard[qbase + lanes_below(hb)] = r;
+        }
+        const bool rest = S.kind == LANE_NOANCHOR;  // on to k_align_lane_na
+        const uint64_t nb = __ballot(rest);
+        if (nb) {
+            uint64_t qbase = 0;
+            if (lane == __builtin_ctzll(nb)) qbase = atomicAdd(a.queue_na2_count, (unsigned long long)__popcll(nb));
+            qbase = shfl64(qbase, __builtin_ctzll(nb));
+            if (rest) a.queue_na2[qbase + lanes_below(nb)] = r;
+        }
+        n_amb += (uint32_t)__popcll(__ballot(S.kind == LANE_AMB));
+        n_unm += (uint32_t)__popcll(__ballot(S.kind == LANE_UNMAPPED));
+        wave_sync();  // (the group list and the rows are rewritten by the next chunk)
     }
     const uint32_t hr_w = wave_sum(hr_sum);
     const uint32_t qf_w = WIN_Q ? wave_sum(qf_sum) : 0u;

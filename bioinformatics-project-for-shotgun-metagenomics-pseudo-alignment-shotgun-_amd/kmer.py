@@ -312,15 +312,27 @@ class KmerReference:
         cls, _ = self._index.lookup([kmer])
         return [] if cls[0] < 0 else self._index.class_genomes(int(cls[0]))
 
+    def _references(self, kmer: str, reverse: bool) -> Dict[Record, Set[int]]:
+        """{genome record: positions} of the k-mer (and of its reverse complement)
+        from the device index (pa_index_positions): genomes in FASTA order, the
+        reverse complement's new genomes after the k-mer's own, as the
+        reference's dict merge orders them (src/kmer.py:338-351)."""
+        out: Dict[Record, Set[int]] = {}
+        for q, g, p in self._index.positions([kmer], reverse).tolist():
+            out.setdefault(self.genomes[g], set()).add(p)
+        return out
+
     def get_kmer_references(self, kmer: str) -> Dict[Record, Set[int]]:
         if self._view is not None:
             return self._view.get(kmer, {})
-        return {self.genomes[g]: _kmer_positions(self.genomes[g]["genome"], kmer) for g in self._genome_set(kmer)}
+        return self._references(kmer, False)
 
     def __getitem__(self, kmer: str) -> Optional[Dict[Record, Set[int]]]:
         return self.get_kmer_references(kmer) or None
 
     def get_kmer_and_reverse_references(self, kmer: str) -> Dict[Record, Set[int]]:
+        if self._view is None:
+            return self._references(kmer, True)
         result: Dict[Record, Set[int]] = {g: set(p) for g, p in self.get_kmer_references(kmer).items()}
         rev = reverse_complement(kmer)
         if rev != kmer:

@@ -27,11 +27,13 @@ PA_COMM_ID_BYTES = 128
 HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4
 NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
 PA_BUILD_DEFER_TILES = 1
+PA_POS_REVERSE, PA_POS_RC_BIT = 1, 0x80000000
 
 # every symbol declared in include/pa.h
 EXPORTS = (
     "pa_last_error", "pa_version", "pa_device_count", "pa_runtime_start",
     "pa_index_build", "pa_index_build_ex", "pa_index_prepare", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
+    "pa_index_positions",
     "pa_index_extsim_stats", "pa_index_dumpref",
     "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_reads_download", "pa_reads_free",
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
@@ -114,6 +116,7 @@ def lib():
         "pa_index_get_info": (I32, [P, ctypes.POINTER(IndexInfo)]),
         "pa_index_lookup": (I32, [P, ctypes.c_char_p, U64, U32, P, P, P]),
         "pa_index_class_genomes": (I32, [P, I64, P, U32, ctypes.POINTER(U32), P]),
+        "pa_index_positions": (I32, [P, ctypes.c_char_p, U64, U32, U32, P, U64, ctypes.POINTER(U64), P]),
         "pa_index_extsim_stats": (I32, [P, P, U32, P, P, P, P]),
         "pa_index_dumpref": (I32, [P, P, P, U32, ctypes.POINTER(ctypes.c_char_p), I32, I32, P, P, P, P,
                                    ctypes.POINTER(U64)]),
@@ -410,6 +413,39 @@ class Index:
         _check(lib().pa_index_class_genomes(self._h, int(cls), _ptr(out), out.size, ctypes.byref(n), None))
         return [int(x) for x in out[:n.value]]
 
+    # pa_kmer_hit (include/pa.h)
+    HIT_DTYPE = np.dtype([("query", np.uint32), ("genome", np.uint32), ("position", np.uint64)])
+
+    def positions(self, kmers: Sequence[str], reverse: bool = False, stream=None) -> np.ndarray:
+        """Every occurrence of the k-mers in the genomes (pa_index_positions):
+        a HIT_DTYPE array sorted by (query, strand, genome, position); `query`
+        carries PA_POS_RC_BIT for a reverse-complement hit (reverse=True)."""
+        n = len(kmers)
+        empty = np.zeros(0, dtype=self.HIT_DTYPE)
+        if n == 0:
+            return empty
+        lens = {len(x) for x in kmers}
+        if len(lens) != 1:  # mixed lengths: only k-long ones can be keys; query numbers restored
+            sel = [i for i, x in enumerate(kmers) if len(x) == self.k]
+            h = self.positions([kmers[i] for i in sel], reverse, stream)
+            rcb = np.uint32(PA_POS_RC_BIT)
+            h["query"] = np.asarray(sel, dtype=np.uint32)[h["query"] & ~rcb] | (h["query"] & rcb)
+            return h
+        kl = lens.pop()
+        blob = "".join(kmers).encode("utf-8", errors="replace") if kl else b""
+        if kl == 0 or len(blob) != n * kl:  # non-ASCII text cannot be a k-mer
+            return empty
+        flags = PA_POS_REVERSE if reverse else 0
+        nh = U64(0)
+        cap = 4096
+        while True:
+            out = np.zeros(cap, dtype=self.HIT_DTYPE)
+            _check(lib().pa_index_positions(self._h, blob, n, kl, flags, out.ctypes.data_as(P), cap,
+                                            ctypes.byref(nh), _stream(stream)))
+            if nh.value <= cap:
+                return out[:nh.value]
+            cap = int(nh.value)
+
     def extsim_stats(self, group_of: Sequence[int], n_groups: int):
         g = np.ascontiguousarray(group_of, dtype=np.uint32)
         total = np.zeros(n_groups, dtype=np.uint64)
@@ -421,7 +457,8 @@ class Index:
     def profile_enable(self, on: bool = True):
         _check(lib().pa_profile_enable(self._h, 1 if on else 0))
 
-    PROF_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_fast", "k_align_exact")
+    PROF_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_fast", "k_align_exact",
+                    "k_align_lane_rc")
 
     def profile_read_kernels(self) -> dict:
         """{kernel: (summed ms, launches)} of the align passes since the last

@@ -11,6 +11,8 @@
  *   pa_index_prepare         (the deferred view, before the first align)
  *   pa_index_lookup          KmerReference.get_kmer_references / __getitem__ src/kmer.py:284-298
  *   pa_index_class_genomes   (genome set of a k-mer, i.e. the keys of kmers[kmer]) src/kmer.py:130
+ *   pa_index_positions       KmerReference.get_kmer_references (positions) and
+ *                            get_kmer_and_reverse_references              src/kmer.py:292-298, 331-351
  *   pa_index_dumpref         KmerReference.get_summary ("Kmers" + Summary counts)
  *                            streamed as JSON text (dumpref)                src/kmer.py:300-329
  *   pa_index_extsim_stats    KmerReference._compute_genome_stats + the pairwise
@@ -164,6 +166,25 @@ pa_status pa_index_lookup(const pa_index *idx, const char *kmers, uint64_t n, ui
 /* genome indices (ascending = FASTA order) of class `cls`; *n = class size. */
 pa_status pa_index_class_genomes(const pa_index *idx, int64_t cls, uint32_t *genomes, uint32_t cap, uint32_t *n,
                                  void *stream);
+/* Positions of n k-mers (kmer_len bases each, back to back) in the genomes:
+ * every (query, genome, genome-local position) whose window holds the k-mer --
+ * kmers[kmer] = {genome: positions} of the reference (src/kmer.py:140-150,
+ * 292-298).  With PA_POS_REVERSE also every window holding its reverse
+ * complement, unless that is the k-mer itself (get_kmer_and_reverse_references,
+ * src/kmer.py:331-351); such hits carry PA_POS_RC_BIT in `query`.  A k-mer of
+ * another length than the index's k, or with anything but A/C/G/T, has none.
+ * Hits are sorted by (query, strand, genome, position); *n_hits = all of them,
+ * of which the first min(cap, *n_hits) are written (hits may be NULL to count).
+ * Genomes are numbered as built (after EXTSIM: the kept genomes). */
+#define PA_POS_REVERSE 1u
+#define PA_POS_RC_BIT 0x80000000u
+typedef struct {
+    uint32_t query;     /* query index | PA_POS_RC_BIT for a reverse-complement hit */
+    uint32_t genome;
+    uint64_t position;  /* window start within the genome */
+} pa_kmer_hit;
+pa_status pa_index_positions(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, uint32_t flags,
+                             pa_kmer_hit *hits, uint64_t cap, uint64_t *n_hits, void *stream);
 /* EXTSIM inputs at identifier-group granularity (group_of[n_genomes]):
  * total[a] = distinct k-mers touching group a, uniq[a] = k-mers contained in
  * exactly one genome which belongs to a, inter[a*n_groups+b] = k-mers touching
@@ -318,7 +339,8 @@ pa_status pa_profile_read(pa_index *idx, double *main_ms, uint64_t *launches, ui
 #define PA_PROF_LANE_NA 2   /* k_align_lane_na */
 #define PA_PROF_WAVE 3      /* k_align_fast */
 #define PA_PROF_EXACT 4     /* k_align_exact */
-#define PA_PROF_KERNELS 5
+#define PA_PROF_LANE_RC 5   /* k_align_lane_rc */
+#define PA_PROF_KERNELS 6
 pa_status pa_profile_read_kernels(pa_index *idx, double *ms, uint64_t *launches);
 
 /* ---- device memory -------------------------------------------------------------- */

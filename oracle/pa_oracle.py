@@ -13,7 +13,10 @@ the reference that are pure host control flow:
   reference's way, by walking per-read genome lists in read order;
 * ``KmerReference.get_summary`` (dumpref, ``src/kmer.py:300-329``) over the
   reference's own dict (``src/kmer.py:135-150``, pruned by identifier as
-  ``src/kmer.py:232-245`` does), pure Python: small references only.
+  ``src/kmer.py:232-245`` does), pure Python: small references only;
+* ``get_kmer_references`` / ``get_kmer_and_reverse_references``
+  (``src/kmer.py:292-298, 331-351``) over that dict (``kmer_dict`` +
+  ``kmer_references``).
 """
 
 from __future__ import annotations
@@ -378,3 +381,35 @@ def dumpref_summary(genomes: Sequence[Tuple[str, str]], k: int, kept_ids=None, s
     if similarity_info is not None:
         out["Similarity"] = similarity_info
     return out
+
+
+def kmer_dict(seqs: Sequence[str], k: int) -> Dict[str, Dict[int, set]]:
+    """The reference's ``kmers`` dict (src/kmer.py:135-150) keyed by genome
+    index: {k-mer: {genome: positions}} in insertion order, 'N' k-mers skipped."""
+    kmers: Dict[str, Dict[int, set]] = {}
+    for gi, seq in enumerate(seqs):
+        if k <= 0 or k > len(seq):  # src/kmer.py:84-94
+            continue
+        for pos in range(len(seq) - k + 1):
+            km = seq[pos:pos + k]
+            if "N" not in km:  # src/kmer.py:145
+                kmers.setdefault(km, {}).setdefault(gi, set()).add(pos)
+    return kmers
+
+
+def reverse_complement(seq: str) -> str:
+    """src/kmer.py:96-103: A<->T, C<->G, anything else kept, reversed."""
+    return seq.translate(str.maketrans("ACGT", "TGCA"))[::-1]
+
+
+def kmer_references(kmers: Dict[str, Dict[int, set]], kmer: str, reverse: bool = False) -> List[Tuple[int, List[int]]]:
+    """get_kmer_references (src/kmer.py:292-298) or, with reverse,
+    get_kmer_and_reverse_references (src/kmer.py:331-351): [(genome, sorted
+    positions)] in the result dict's order."""
+    out: Dict[int, set] = {g: set(p) for g, p in kmers.get(kmer, {}).items()}
+    if reverse:
+        rev = reverse_complement(kmer)
+        if rev != kmer:
+            for g, p in kmers.get(rev, {}).items():
+                out.setdefault(g, set()).update(p)
+    return [(g, sorted(p)) for g, p in out.items()]

@@ -25,13 +25,18 @@ Files written:
 * ``dumpref_cases.json`` - the reference CLI's ``dumpref`` stdout for small
   references (duplicate headers, N runs, k > 32, EXTSIM drops whose k-mers
   come before kept ones), and for config 1 its length and SHA-256;
+* ``lookup_cases.json`` - ``get_kmer_references`` / ``__getitem__`` /
+  ``get_kmer_and_reverse_references`` (genomes in dict order, positions) for
+  every k-mer of small references (duplicate headers, N runs, k > 32, even k
+  with palindromic k-mers, EXTSIM drops) plus absent, reverse-complement and
+  malformed queries;
 * ``config1.kdb`` / ``config1_sim.kdb`` / ``config1.aln`` - a reference and an
   alignment SAVED BY THE REFERENCE CLI (``-t reference``, ``-t align``), for
   the loader of reference-written files; ``dumpref_cases.json`` also holds the
   reference's stdout of ``dumpref -r`` / ``dumpalign -r`` / ``dumpalign -a``
   on them.
 
-    python tests/golden/make_golden.py [part ...]   (parts: unit config1 extsim parser dumpref)
+    python tests/golden/make_golden.py [part ...]   (parts: unit config1 extsim parser dumpref lookup)
 """
 
 from __future__ import annotations
@@ -402,11 +407,60 @@ def make_dumpref():
     print("dumpref cases:", len(cases), {k: v.get("length") for k, v in big_out.items()})
 
 
+# ----------------------------------------------------------------------------
+# k-mer lookups with positions (src/kmer.py:284-298, 331-351)
+# ----------------------------------------------------------------------------
+
+def make_lookup_cases():
+    rng = random.Random(11)
+    cases = [
+        {"name": "test_kmer_sample", "k": 3, "filter": None,
+         "genomes": [("Genome1", "AGCTAGCTAGCTAGCTAGCT"), ("Genome2", "TGCATGCATGCATGCATGCA"),
+                     ("Genome3", "AGCTTGCATGCAGCTAGCTA"), ("Genome4", "CCGGAAGCTTGCATGCAGCTA")]},
+        {"name": "duplicate_headers_n_runs", "k": 5, "filter": None,
+         "genomes": [("dup x", "ACGTTGCAACGTAACNNACGTTG"), ("other", "TTGCAACGTAACGGT"), ("dup x", "CAACGTAACGGTTTT"),
+                     ("short", "ACG"), ("ns", "NNNNNNN")]},
+        {"name": "even_k_palindromes", "k": 4, "filter": None,
+         "genomes": [("p1", "ACGTACGTAATTGCGCAT"), ("p2", "GGCCAATTACGT")]},
+        {"name": "k33_multiword", "k": 33, "filter": None,
+         "genomes": [(f"w{i}", "".join(rng.choice("ACGT") for _ in range(90))) for i in range(3)]},
+    ]
+    cases[3]["genomes"][2] = ("w2", cases[3]["genomes"][0][1][:60] + cases[3]["genomes"][2][1][60:])
+    gens = synth.family_genomes(5, 150, seed=400, family_size=5, sub_rate=0.01, conserved_len=20, n_rate=0.0, n_run=0)
+    cases.append({"name": "extsim_family", "k": 8, "filter": 0.6,
+                  "genomes": [(f"fam{i}", bytes(g).decode()) for i, g in enumerate(gens)]})
+    for c in cases:
+        fa = RR.FASTARecordContainer()
+        fa.parse_records(fasta_of(c["genomes"]))
+        kw = {} if c["filter"] is None else {"filter_similar": True, "similarity_threshold": c["filter"]}
+        ref = R.KmerReference(c["k"], fa, **kw)
+        gi = {id(g): i for i, g in enumerate(ref.genomes)}
+        k = c["k"]
+        queries = list(ref.kmers)
+        queries += [R.reverse_complement(q) for q in queries[:40]]
+        queries += ["".join(rng.choice("ACGT") for _ in range(k)) for _ in range(20)]
+        queries += ["A" * k, "N" * k, "a" * k, "ACGT"[: max(k - 1, 0)], "ACGT" * (k // 4 + 2), ("AC" * k)[:k]]
+        out = []
+        for q in queries:
+            fwd = ref.get_kmer_references(q)
+            both = ref.get_kmer_and_reverse_references(q)
+            item = ref[q]
+            out.append([q, [[gi[id(g)], sorted(p)] for g, p in fwd.items()],
+                        [[gi[id(g)], sorted(p)] for g, p in both.items()], item is None])
+        c["kept"] = [gi[id(g)] for g in ref.genomes]
+        c["n_genomes_kept"] = len(ref.genomes)
+        c["kept_identifiers"] = [g.identifier for g in ref.genomes]
+        c["queries"] = out
+    with open(os.path.join(HERE, "lookup_cases.json"), "w") as f:
+        json.dump(cases, f, separators=(",", ":"))
+    print("lookup cases:", len(cases), sum(len(c["queries"]) for c in cases), "queries")
+
+
 if __name__ == "__main__":
-    parts = sys.argv[1:] or ["unit", "config1", "extsim", "parser", "dumpref"]
+    parts = sys.argv[1:] or ["unit", "config1", "extsim", "parser", "dumpref", "lookup"]
     try:
         for part, fn in (("unit", make_unit_cases), ("config1", make_config1), ("extsim", make_extsim),
-                         ("parser", make_parser_cases), ("dumpref", make_dumpref)):
+                         ("parser", make_parser_cases), ("dumpref", make_dumpref), ("lookup", make_lookup_cases)):
             if part in parts:
                 fn()
     finally:

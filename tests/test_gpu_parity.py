@@ -616,6 +616,50 @@ def test_unanchored_reads_vs_oracle(ps, noanchor, monkeypatch):
     assert o.stats[2] > 5000  # many unmapped reads: the case under test
 
 
+@pytest.mark.parametrize("ps", [dict(), dict(m=0, p=0), dict(mrq=53, mkq=58, mg=10), dict(mg=2), dict(mkq=61)],
+                         ids=["default", "m0p0", "c3raw", "mg2", "mkq61"])
+@pytest.mark.parametrize("rcwalk", ["1", "0"])
+def test_reverse_strand_walk_vs_oracle(ps, rcwalk, monkeypatch):
+    """Reads on the reverse strand (60 %), walked on it by k_align_lane_rc
+    (PA_NA_RCWALK=1: the reverse-complement plane shows most of their windows
+    absent) or checked window by window by k_align_lane_na (0), against
+    genomes holding inverted repeats (a stretch followed later by its reverse
+    complement: windows whose reverse complement IS a key, plane bit set) and
+    palindromic runs; equal to the oracle (src/kmer.py:419-429)."""
+    monkeypatch.setenv("PA_NA_MIN", "0")
+    monkeypatch.setenv("PA_NA_RCWALK", rcwalk)
+    gens = synth.family_genomes(10, 30000, seed=81, family_size=3, sub_rate=0.01, conserved_len=500,
+                                n_rate=2e-4, n_run=8)
+    comp = np.zeros(256, dtype=np.uint8)
+    for a_, b_ in zip(b"ACGTN", b"TGCAN"):
+        comp[a_] = b_
+    rng = np.random.default_rng(82)
+    for g in gens:  # inverted repeats: 20 stretches of 40-400 bases copied reverse-complemented further on
+        for _ in range(20):
+            ln = int(rng.integers(40, 400))
+            a0 = int(rng.integers(0, len(g) - 2 * ln - 1))
+            b0 = int(rng.integers(a0 + ln, len(g) - ln))
+            g[b0:b0 + ln] = comp[g[a0:a0 + ln][::-1]]
+        p0 = int(rng.integers(0, len(g) - 64))
+        g[p0:p0 + 64] = np.frombuffer(b"ACGT" * 16, dtype=np.uint8)  # (ACGT)n is its own reverse complement
+    index = N.Index(gens, 31)
+    oix = O.OracleIndex(gens, 31)
+    reads = N.Reads.synthesize(index, 30000, 150, first_read=0, seed=83, sub_rate=0.006, rc_rate=0.6,
+                               foreign_rate=0.1)
+    s, q, off = reads.download()
+    full = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+    res = N.Result(index)
+    N.align(index, reads, N.Params.make(full["m"], full["p"], full["mrq"], full["mkq"], full["mg"]), 7, res)
+    stats, uq, am, fk = res.fetch()
+    o = oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"], mkq=full["mkq"],
+                  mg=full["mg"], read_base=7, detail=False)
+    assert stats.tolist() == o.stats.tolist(), ps
+    assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
+    ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+    assert fk.tolist() == ofk.tolist(), ps
+    assert o.stats[2] > 10000  # mostly unmapped reverse-strand reads: the case under test
+
+
 @pytest.mark.parametrize("k", [3, 4, 5, 8, 11, 16, 21, 28, 31])
 def test_quality_masks_every_k_vs_oracle(k):
     """k_quality_masks (the lane kernels' --min-read-quality / --min-kmer-quality

@@ -142,3 +142,19 @@ def test_oracle_dumpref_config1():
     text = json.dumps(O.dumpref_summary(genomes, 21, kept, info), indent=4) + "\n"
     g = DUMPREF["config1"]["config1_sim"]
     assert len(text) == g["length"] and hashlib.sha256(text.encode()).hexdigest() == g["sha256"]
+
+
+LOOKUP = load("lookup_cases.json")
+
+
+@pytest.mark.parametrize("case", LOOKUP, ids=[c["name"] for c in LOOKUP])
+def test_oracle_lookup_cases(case):
+    """get_kmer_references / get_kmer_and_reverse_references / __getitem__ of
+    the reference (src/kmer.py:284-298, 331-351) vs the oracle's dict."""
+    kept = [case["genomes"][i][1] for i in range(len(case["genomes"]))
+            if case["genomes"][i][0] in set(case["kept_identifiers"])] if case["filter"] else [g[1] for g in case["genomes"]]
+    kmers = O.kmer_dict(kept, case["k"])
+    for q, fwd, both, none in case["queries"]:
+        assert [list(x) for x in O.kmer_references(kmers, q)] == fwd, q
+        assert [list(x) for x in O.kmer_references(kmers, q, reverse=True)] == both, q
+        assert (not fwd) == none, q
