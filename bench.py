@@ -100,6 +100,10 @@ CONFIGS = {
     # window of such a read must be shown absent
     "c2rc": dict(BASE, rc_rate=0.5,
                  name="C2 strand mix: C2 genomes, 10M reads per GPU: 50% reverse-complement, 0.5% substitutions"),
+    # the other half of c2mix's no-seed reads: half the reads of an organism
+    # absent from the index (every window Bloom-tested, k_align_lane_na)
+    "c2fg": dict(BASE, foreign_rate=0.5,
+                 name="C2 foreign mix: C2 genomes, 10M reads per GPU: 50% unindexed organism, 0.5% substitutions"),
     "c1": dict(BASE, n_genomes=3, genome_len=5000, family=3, sub=0.02, conserved=300, k=21, reads_per_gpu=1000,
                read_len=100, read_err=0.01, name="C1: 3 x 5 kb genomes, 1k x 100 bp reads, k=21"),
 }
@@ -146,7 +150,8 @@ REQ_COUNTERS = {"TCC_EA0_RDREQ_32B_sum": 32, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_E
 # the SQ counters of the same pass (8 SQ counters and 4 TCC fit one rocprofv3
 # pass; these count quad-cycles, so only their ratios are used)
 SQ_COUNTERS = ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")
-ALIGN_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_lane_rc", "k_align_fast", "k_align_exact")
+ALIGN_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_lane_rc", "k_rc_seeds", "k_align_fast",
+                 "k_align_exact")
 
 
 def kernel_short_name(mangled: str):

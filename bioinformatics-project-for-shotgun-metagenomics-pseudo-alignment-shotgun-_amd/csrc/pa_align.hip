@@ -74,6 +74,8 @@ struct AlignArgs {
     const uint32_t *gblk;           // the genome holding position j << 16 (tiled indexes)
     const uint64_t *bloom;          // Bloom filter of the keys (null: none), 2^bloom_lg words
     const uint64_t *tile_rcp;       // reverse-complement plane (k_tile_rcp; null: none)
+    const uint32_t *mm_bits;        // minimizer presence bitmap (k_mm_build; null: none), 2^mm_lg bits
+    uint32_t mm_lg;
     const uint32_t *tile_rcnb;      // reverse-complement one-substitution neighbour bits (null: none)
     uint32_t bloom_lg;
     int walk_rounds;
@@ -102,8 +104,12 @@ struct AlignArgs {
     unsigned long long *queue_hard_count;
     uint32_t *queue_na;                    // lane kernel: reads with no seed in the index (null: to the wave kernel)
     unsigned long long *queue_na_count;
-    uint32_t *queue_na2;                   // k_align_lane_rc: the reads it could not walk on the reverse strand
-    unsigned long long *queue_na2_count;   //   (on to k_align_lane_na)
+    uint64_t *queue_na_keys;               // lane kernel: their outer seeds' reverse complements (k_rc_seeds; null: none)
+    uint32_t *queue_rc;                    // k_rc_seeds: reads with a reverse-complement seed in the index,
+    uint64_t *queue_rc_anc;                //   its first occurrence | seed << 63 (k_align_lane_rc)
+    unsigned long long *queue_rc_count;
+    uint32_t *queue_na2;                   // k_rc_seeds / k_align_lane_rc: the reads to test window by window
+    unsigned long long *queue_na2_count;   //   (k_align_lane_na)
     uint64_t na_min;                       // fewer than this: k_align_lane_na hands them to the wave kernel
     const uint4 *qmask;                    // (quality filters) per read: windows failing --min-kmer-quality
     const uint8_t *qdrop;                  //   and 1 if the read fails --min-read-quality (k_quality_masks)
@@ -734,7 +740,14 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
     }
     if (a.queue_na) {  // the reads without a seed in the index (count on the device)
         AlignArgs b = a;
-        if (a.tile_rcp && a.bloom && a.queue_na2) {  // the reverse-strand walk first; the rest on to k_align_lane_na
+        if (a.queue_na_keys) {  // reverse-complement seeds, the reverse-strand walk; the rest on to k_align_lane_na
+            {
+                KernelTimer kt(prof, st, PA_PROF_RC_SEEDS);
+                hipLaunchKernelGGL(k_rc_seeds, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(
+                                                        (a.n + kBlock * 4 - 1) / (kBlock * 4), 8192))),
+                                   dim3(kBlock), 0, st, a);
+                PA_HIP(hipGetLastError());
+            }
             auto rc = win_q ? (mg ? k_align_lane_rc<true, true, true> : k_align_lane_rc<true, true, false>)
                     : need_q ? (mg ? k_align_lane_rc<true, false, true> : k_align_lane_rc<true, false, false>)
                              : (mg ? k_align_lane_rc<false, false, true> : k_align_lane_rc<false, false, false>);
@@ -809,6 +822,9 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.bloom = idx->tile_cls ? idx->bloom : nullptr;
     a.bloom_lg = idx->bloom_lg;
     a.tile_rcp = idx->tile_cls ? idx->tile_rcp : nullptr;
+    a.mm_bits = idx->tile_cls ? idx->mm_bits : nullptr;
+    a.mm_lg = idx->mm_lg;
+    if (const char *e = std::getenv("PA_MM_BITS")) if (e[0] == '0') a.mm_bits = nullptr;
     a.tile_rcnb = idx->tile_cls ? idx->tile_rcnb : nullptr;
     if (const char *e = std::getenv("PA_NA_RCNB")) if (e[0] == '0') a.tile_rcnb = nullptr;
     if (const char *e = std::getenv("PA_NA_RCWALK")) if (e[0] == '0') a.tile_rcp = nullptr;
@@ -898,13 +914,21 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
     pa::dev_free(idx->queue_hard);
     pa::dev_free(idx->queue_na);
     pa::dev_free(idx->queue_na2);
-    idx->queue = idx->queue_hard = idx->queue_na = idx->queue_na2 = nullptr;
+    pa::dev_free(idx->queue_na_keys);
+    pa::dev_free(idx->queue_rc);
+    pa::dev_free(idx->queue_rc_anc);
+    idx->queue = idx->queue_hard = idx->queue_na = idx->queue_na2 = idx->queue_rc = nullptr;
+    idx->queue_na_keys = idx->queue_rc_anc = nullptr;
     idx->queue_cap = 0;
     PA_HIP(pa::dev_malloc(&idx->queue, n * 4));
     PA_HIP(pa::dev_malloc(&idx->queue_hard, n * 4));
     PA_HIP(pa::dev_malloc(&idx->queue_na, n * 4));
     PA_HIP(pa::dev_malloc(&idx->queue_na2, n * 4));
-    if (!idx->na_count) PA_HIP(pa::dev_malloc(&idx->na_count, 16));  // [0] k_align_lane_na's reads, [1] k_align_lane_rc's rest
+    PA_HIP(pa::dev_malloc(&idx->queue_na_keys, n * 16));
+    PA_HIP(pa::dev_malloc(&idx->queue_rc, n * 4));
+    PA_HIP(pa::dev_malloc(&idx->queue_rc_anc, n * 8));
+    // [0] the lane kernel's reads without a seed, [1] k_rc_seeds' walkable ones, [2] the rest (k_align_lane_na)
+    if (!idx->na_count) PA_HIP(pa::dev_malloc(&idx->na_count, 24));
     idx->queue_cap = n;
     return PA_OK;
 }
@@ -1068,11 +1092,18 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             if (const char *e = std::getenv("PA_LANE_NOANCHOR")) na = e[0] == '1';
             a.queue_na = na ? idx->queue_na : nullptr;
             a.queue_na_count = idx->na_count;
+            // their reverse-complement seeds (k_rc_seeds -> k_align_lane_rc):
+            // with the reverse-complement plane (PA_NA_RCWALK=0: none)
+            const bool rcw = na && a.tile_rcp && a.bloom;
+            a.queue_na_keys = rcw ? idx->queue_na_keys : nullptr;
+            a.queue_rc = idx->queue_rc;
+            a.queue_rc_anc = idx->queue_rc_anc;
+            a.queue_rc_count = idx->na_count + 1;
             a.queue_na2 = idx->queue_na2;
-            a.queue_na2_count = idx->na_count + 1;
+            a.queue_na2_count = idx->na_count + 2;
             a.na_min = 32768;  // (PA_NA_MIN: tests)
             if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
-            if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 16, st));
+            if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 24, st));
             PA_TRY(launch_lane(a, st, idx));
             a.rlist = idx->queue_hard;
             a.rlist_count = a.queue_hard_count;

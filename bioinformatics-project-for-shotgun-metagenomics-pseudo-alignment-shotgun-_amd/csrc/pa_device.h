@@ -291,6 +291,10 @@ __device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uin
     const uint32_t mn = k == 31 ? key_minimizer_c<31>(key) : key_minimizer(key, k);
     w = (bloom_block(mn, lg) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
 }
+// Minimizer presence bitmap (mm_bits, 2^lg bits): bit mm_bit(mn) is set for
+// the minimizer of every key (k_mm_build) -- a prefilter small enough to stay
+// in the L2 that answers a whole minimizer run of absent windows.
+__device__ __forceinline__ uint32_t mm_bit(uint32_t mn, uint32_t lg) { return (mn * 0x85EBCA77u) >> (32 - lg); }
 // A key's test against its (loaded) 16-B block.
 __device__ __forceinline__ bool bloom_block_has(const uint4 &b, uint32_t h) {
     const bool w1 = (h >> 31) != 0;

@@ -750,6 +750,18 @@ __global__ __launch_bounds__(256) void k_tile_rcp(const uint32_t *__restrict__ t
     }
 }
 
+// The minimizer presence bitmap: bit mm_bit(minimizer) of every key (the
+// minimizer of bloom_word's block), one pass over the slots.
+__global__ void k_mm_build(const Slot<1> *__restrict__ table, uint64_t cap, uint32_t *bits, uint32_t lg, int k) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+        const uint64_t key = table[i].key[0];
+        if (key == EMPTY) continue;
+        const uint32_t h = mm_bit(k == 31 ? key_minimizer_c<31>(key) : key_minimizer(key, k), lg);
+        atomicOr(&bits[h >> 5], 1u << (h & 31));
+    }
+}
+
 // The lane walk's view of the genomes (pa_lane.h), one 32-B block per 64
 // positions j: {2-bit words 2j and 2j+1 of tile_pk (positions 64 j .. 64 j +
 // 63), flag plane A, flag plane B}, bit i of a plane <-> position 64 j + i:
@@ -1233,6 +1245,25 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 }
                 phase_mark("Bloom");
             }
+            {  // the minimizer presence bitmap: 2^25 bits (4 MiB, the size of an XCD's L2)
+               // for references of up to ~30 M distinct minimizers (distinct
+               // k-mers / 9: a minimizer covers ~9 of a genome's k-mers), so
+               // that fewer than ~1 / 4 of the bits are set; none above (C4, C5)
+               // or with PA_NO_MM=1
+                const char *nm = std::getenv("PA_NO_MM");
+                const uint32_t lg = 25;
+                if (!(nm && nm[0] == '1') && idx->bloom && idx->n_kmers / 9 <= (1ull << lg) / 4 &&
+                    pa::dev_malloc(&idx->mm_bits, (1ull << lg) / 8) == hipSuccess) {
+                    B_HIP(hipMemsetAsync(idx->mm_bits, 0, (1ull << lg) / 8, st));
+                    hipLaunchKernelGGL(k_mm_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                       dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->mm_bits, lg, k);
+                    idx->mm_lg = lg;
+                    idx->device_bytes += (1ull << lg) / 8;
+                } else {
+                    idx->mm_bits = nullptr;
+                }
+                phase_mark("minimizer bitmap");
+            }
             {  // the reverse-complement plane (k_tile_rcp), 1 bit per base; PA_NO_RCP=1: none
                 const char *nr = std::getenv("PA_NO_RCP");
                 const uint64_t n_blocks = n / 64 + 5;  // padded like the walk blocks
@@ -1306,6 +1337,8 @@ void index_release(pa_index *idx) {
     idx->bloom = nullptr;
     pa::dev_free(idx->tile_rcp);
     idx->tile_rcp = nullptr;
+    pa::dev_free(idx->mm_bits);
+    idx->mm_bits = nullptr;
     pa::dev_free(idx->tile_gblk);
     idx->tile_gblk = nullptr;
     idx->bloom_lg = 0;
@@ -1316,7 +1349,13 @@ void index_release(pa_index *idx) {
     pa::dev_free(idx->queue_hard);
     pa::dev_free(idx->queue_na);
     pa::dev_free(idx->queue_na2);
+    pa::dev_free(idx->queue_na_keys);
+    pa::dev_free(idx->queue_rc);
+    pa::dev_free(idx->queue_rc_anc);
     idx->queue_na2 = nullptr;
+    idx->queue_na_keys = nullptr;
+    idx->queue_rc = nullptr;
+    idx->queue_rc_anc = nullptr;
     pa::dev_free(idx->na_count);
     pa::dev_free(idx->qmask);
     pa::dev_free(idx->qdrop);
@@ -1355,6 +1394,8 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
     if (rc != PA_OK) {  // the index stays usable without its align-side view
         pa::dev_free(idx->tile_cls); pa::dev_free(idx->tile_pk); pa::dev_free(idx->tile_lw); pa::dev_free(idx->tile_nb);
         pa::dev_free(idx->tile_gblk); pa::dev_free(idx->bloom); pa::dev_free(idx->tile_rcp); pa::dev_free(idx->tile_rcnb);
+        pa::dev_free(idx->mm_bits);
+        idx->mm_bits = nullptr;
         idx->tile_rcnb = nullptr;
         idx->tile_cls = nullptr, idx->tile_pk = nullptr, idx->tile_lw = nullptr, idx->tile_nb = nullptr;
         idx->tile_gblk = nullptr, idx->bloom = nullptr, idx->bloom_lg = 0, idx->tile_n = 0, idx->tile_rcp = nullptr;

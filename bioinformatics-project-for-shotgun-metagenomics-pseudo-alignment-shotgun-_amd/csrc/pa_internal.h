@@ -113,6 +113,8 @@ struct pa_index {
     uint64_t reads_seen = 0;           // reads aligned so far (the neighbour bits follow at kNbReadsPerBase)
     uint32_t *tile_gblk = nullptr;     // [(tile_n >> 16) + 2] the genome holding position j << 16
     uint64_t *bloom = nullptr;         // [2^bloom_lg] Bloom filter of the table's keys (k_bloom_build), optional
+    uint32_t *mm_bits = nullptr;       // [2^mm_lg / 32] minimizer presence bitmap (k_mm_build), optional
+    uint32_t mm_lg = 0;
     uint64_t *tile_rcp = nullptr;      // [tile_n / 64 + 5] bit t: the reverse complement of the k-mer at t may be
                                        //   a key (present, or no indexed window at t) -- k_tile_rcp, optional
     uint32_t bloom_lg = 0;
@@ -122,7 +124,10 @@ struct pa_index {
     uint32_t *queue = nullptr;         // read indices deferred to the exact kernel
     uint32_t *queue_hard = nullptr;    // read indices the lane kernel leaves to the wave kernel
     uint32_t *queue_na = nullptr;      // read indices the lane kernel found no seed for (k_align_lane_rc / _na)
-    uint32_t *queue_na2 = nullptr;     // those k_align_lane_rc could not walk on the reverse strand (k_align_lane_na)
+    uint32_t *queue_na2 = nullptr;     // those tested window by window (k_align_lane_na)
+    uint64_t *queue_na_keys = nullptr; // [2 per queue_na entry] their outer seeds' reverse complements (k_rc_seeds)
+    uint32_t *queue_rc = nullptr;      // reads with a reverse-complement seed (k_align_lane_rc)
+    uint64_t *queue_rc_anc = nullptr;  //   its first occurrence | seed << 63
     uint4 *qmask = nullptr;            // per read: windows failing --min-kmer-quality (k_quality_masks)
     uint8_t *qdrop = nullptr;          // per read: fails --min-read-quality
     uint64_t qmask_cap = 0;

@@ -439,6 +439,11 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             if (at < 0 && stp[i] != ~0ull && (pass == 1 || scls[i] < a.G)) at = i;
     if (at < 0) {  // no anchor: no seed k-mer is in the index
         if (a.queue_na) S.kind = LANE_NOANCHOR;
+        // the reverse complements of the outer seeds -- R' windows 0 and W - 1
+        // of the read's reverse complement R' -- for k_rc_seeds (S.P0 / S.P1:
+        // walk fields, unused by such a read)
+        S.P0 = rc_key(skey[NSEED - 1], k);
+        S.P1 = rc_key(skey[0], k);
         return (void)LANE_HARD_WHY(3);
     }
     S.anc = stp[0] | ((uint64_t)sw(0) << 40);
@@ -986,7 +991,13 @@ void k_align_lane(AlignArgs a) {
             uint64_t qbase = 0;
             if (lane == __builtin_ctzll(nab)) qbase = atomicAdd(a.queue_na_count, (unsigned long long)__popcll(nab));
             qbase = shfl64(qbase, __builtin_ctzll(nab));
-            if (na) a.queue_na[qbase + lanes_below(nab)] = r;
+            if (na) {
+                a.queue_na[qbase + lanes_below(nab)] = r;
+                if (a.queue_na_keys) {
+                    a.queue_na_keys[2 * (qbase + lanes_below(nab))] = S.P0;
+                    a.queue_na_keys[2 * (qbase + lanes_below(nab)) + 1] = S.P1;
+                }
+            }
         }
         const bool again = S.kind == LANE_AGAIN;
         const uint64_t ab = __ballot(again);
@@ -1064,7 +1075,8 @@ __device__ __forceinline__ uint64_t bits128(uint64_t x0, uint64_t x1, int s) {  
 // its 15-mer orders computed, its first run loaded, no LDS carry.
 template <int NAG, int KC, bool CARRY = true>  // KC: k known at compile time (31, the benchmark k), else 0
 __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64_t *row, uint32_t w0, uint32_t act,
-                                                bool fresh, uint32_t &prev_blk, uint4 &cur, uint4 (*hc)[kBlock]) {
+                                                bool fresh, uint32_t &prev_blk, uint4 &cur, bool &cur_mm,
+                                                uint4 (*hc)[kBlock]) {
     static_assert(NAG == 8 || NAG == 16, "a group's bases are 128 bits from a multiple of 16");
     const int k = KC ? KC : a.k, sh = 64 - 2 * k;
     const int mm = k < 15 ? k : 15;
@@ -1137,11 +1149,33 @@ __device__ __forceinline__ uint32_t bloom_group(const AlignArgs &a, const uint64
         const uint32_t before = j ? blk[j - 1] : prev_blk;
         news |= (blk[j] != before || (j == 0 && fresh)) ? 1u << j : 0u;
     }
+    // minimizer presence (a.mm_bits, a bitmap small enough for the L2): a run
+    // whose minimizer is no key's has none of its windows in the index -- an
+    // unindexed organism's reads have almost none -- and loads no block.  A
+    // run going on from the previous group keeps that group's answer (cur_mm)
+    uint32_t pres = (1u << NAG) - 1;
+    if (a.mm_bits) {
+        uint32_t mw[NAG], mh[NAG];
+#pragma unroll
+        for (int j = 0; j < NAG; j++) {
+            mh[j] = mm_bit(mn[j], a.mm_lg);
+            mw[j] = a.mm_bits[bit(news, j) ? mh[j] >> 5 : 0u];  // (loads issue together)
+        }
+        bool p = cur_mm;
+        pres = 0;
+#pragma unroll
+        for (int j = 0; j < NAG; j++) {
+            if (bit(news, j)) p = ((mw[j] >> (mh[j] & 31)) & 1u) != 0;
+            pres |= p ? 1u << j : 0u;
+        }
+        cur_mm = p;
+        act &= pres;
+    }
     // (no load for a run none of whose windows is looked up; the group's last
     // run may go on in the next group, which then tests against `cur`)
     uint32_t need = 0;
     {
-        bool any = true;
+        bool any = bit(pres, NAG - 1);
 #pragma unroll
         for (int j = NAG - 1; j >= 0; j--) {
             any = any || bit(act, j);
@@ -1211,22 +1245,10 @@ __device__ __forceinline__ void na_hc_init(const uint64_t *row, uint32_t w0, int
 // Exact: it only removes windows shown absent.
 constexpr uint32_t kRcMaxMis = 16;
 __device__ __forceinline__ bool na_rc_walk(const AlignArgs &a, const uint64_t *row, uint32_t len, uint32_t W,
-                                           uint64_t &lk0, uint64_t &lk1) {
-    const int k = a.k, sh = 64 - 2 * k;
-    // the seeds, one probe each: R' window 0 first, W - 1 only if it is absent
-    uint64_t sk[2];
-    sk[0] = rc_key(row_bits(row, 2 * (W - 1)) >> sh, k);
-    sk[1] = rc_key(row_bits(row, 0) >> sh, k);
-    uint32_t f, cl[2], tp[2];
-    lane_probe<2>(a, sk, 1u, f, cl, tp);
-    int64_t A = -1;
-    if (bit(f, 0) && tp[0] != NONE) {
-        A = (int64_t)first_pos(cl[0], tp[0], a.G, a.class_genomes, a.goff, a.tpos_local);
-    } else {
-        lane_probe<2>(a, sk, 2u, f, cl, tp);
-        if (bit(f, 1) && tp[1] != NONE)
-            A = (int64_t)first_pos(cl[1], tp[1], a.G, a.class_genomes, a.goff, a.tpos_local) - (int64_t)(W - 1);
-    }
+                                           uint64_t seed, uint64_t &lk0, uint64_t &lk1) {
+    const int k = a.k;
+    // seed = P | s << 63: R' window 0 (s = 0) or W - 1 (s = 1) is at P (k_rc_seeds)
+    const int64_t A = (int64_t)(seed & ~(1ull << 63)) - ((seed >> 63) ? (int64_t)(W - 1) : 0);
     if (A < 0 || (uint64_t)A + len > a.tile_n) return false;
     const uint64_t Au = (uint64_t)A;
     uint64_t gw[kLaneWords + 1], pa3[3], pb3[3];
@@ -1407,6 +1429,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
             constexpr int NAG = PA_NA_GROUP;
             uint32_t prev_blk = 0;
             uint4 cur = make_uint4(0, 0, 0, 0);
+            bool cur_mm = true;
             // the windows to look up (bit w of pm0 | pm1 << 64): every window
             // (W <= kLaneMaxW = 128) but those failing --min-kmer-quality, less
             // those the Bloom filter shows absent.  A group with none is
@@ -1428,8 +1451,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
                 }
                 if (a.bloom) {  // keys surely absent are not looked up
                     if (fresh) na_hc_init(row, w0, a.k, hcarry);  // (the group's first sixteen 15-mer orders)
-                    act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, fresh, prev_blk, cur, hcarry)
-                                    : bloom_group<NAG, 0>(a, row, w0, act, fresh, prev_blk, cur, hcarry);
+                    act = a.k == 31 ? bloom_group<NAG, 31>(a, row, w0, act, fresh, prev_blk, cur, cur_mm, hcarry)
+                                    : bloom_group<NAG, 0>(a, row, w0, act, fresh, prev_blk, cur, cur_mm, hcarry);
                 }
                 fresh = false;
                 if (w0 < 64) pm0 |= (uint64_t)act << w0;
@@ -1465,14 +1488,102 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
     }
 }
 
-// k_align_lane_rc: the reads k_align_lane found no seed for, walked on the
-// reverse strand first (na_rc_walk) -- about half of a real FASTQ is the
-// reverse complement of some genome stretch, and the forward-only lookups of
-// the reference (src/kmer.py:419-429) must show every one of its windows
-// absent.  A read the walk anchors needs the Bloom filter only for its
-// windows that differ from the stretch or whose plane bit is set (~25 of
-// ~120 at 0.5 % errors); the rest go on to k_align_lane_na (a.queue_na2),
-// which tests every window.  The reads' counts vary a lot (0 ... 120 windows),
+// k_rc_seeds: the reverse-complement seeds of the reads k_align_lane found no
+// seed for (their keys come with the queue: a.queue_na_keys, made while the
+// read was packed), kSeedReads reads per thread: a read with one
+// in the index goes to k_align_lane_rc (a.queue_rc, with the seed's first
+// occurrence), any other -- an unindexed organism, errors at both ends -- to
+// k_align_lane_na (a.queue_na2).  Classifying here, without loading or packing
+// the read, keeps the reads k_align_lane_rc cannot walk out of its waves (it
+// took ~0.2 ns per such read to load, pack and reject it).
+constexpr int kSeedReads = 4;  // reads per thread (their probes in flight together)
+__global__ __launch_bounds__(kBlock) void k_rc_seeds(AlignArgs a) {
+    // queue slots are taken per block (LDS counters, one global atomic per
+    // queue and block of kBlock * kSeedReads reads): one atomic per wave
+    // serialised on the two counters took longer than the probes (1.0-1.7 ms
+    // for 5 M reads)
+    __shared__ uint32_t cnt[2];
+    __shared__ unsigned long long base[2];
+    const uint64_t n = *a.queue_na_count;
+    const bool forward = n < a.na_min;  // (few such reads: all on to k_align_lane_na, which hands them on)
+    constexpr uint64_t kChunk = (uint64_t)kBlock * kSeedReads;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < n; c0 += (uint64_t)gridDim.x * kChunk) {
+        if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        // R' window 0 first (found for ~86 % of reverse-strand reads at 0.5 %
+        // errors), R' window W - 1 only where it is absent: 1.1 table lines
+        // per such read instead of 2 (an unindexed organism's read takes 2)
+        uint64_t sk[kSeedReads];
+        uint32_t act = 0;
+#pragma unroll
+        for (int j = 0; j < kSeedReads; j++) {
+            const uint64_t i = c0 + (uint64_t)j * kBlock + threadIdx.x;
+            sk[j] = 0;
+            if (i < n && !forward) {
+                sk[j] = a.queue_na_keys[2 * i];
+                act |= 1u << j;
+            }
+        }
+        uint32_t f0, f1, cl[kSeedReads], tp[kSeedReads];
+        lane_probe<kSeedReads>(a, sk, act, f0, cl, tp);
+        uint64_t seed[kSeedReads];
+        uint32_t walk = 0, slot[kSeedReads], act1 = 0;
+#pragma unroll
+        for (int j = 0; j < kSeedReads; j++) {
+            const uint64_t i = c0 + (uint64_t)j * kBlock + threadIdx.x;
+            seed[j] = 0;
+            if (bit(f0, j) && tp[j] != NONE) {
+                walk |= 1u << j;
+                seed[j] = first_pos(cl[j], tp[j], a.G, a.class_genomes, a.goff, a.tpos_local);
+            } else if (bit(act, j)) {
+                sk[j] = a.queue_na_keys[2 * i + 1];
+                act1 |= 1u << j;
+            }
+        }
+        if (__ballot(act1 != 0)) {
+            lane_probe<kSeedReads>(a, sk, act1, f1, cl, tp);
+#pragma unroll
+            for (int j = 0; j < kSeedReads; j++)
+                if (bit(act1, j) && bit(f1, j) && tp[j] != NONE) {
+                    walk |= 1u << j;
+                    seed[j] = first_pos(cl[j], tp[j], a.G, a.class_genomes, a.goff, a.tpos_local) | (1ull << 63);
+                }
+        }
+#pragma unroll
+        for (int j = 0; j < kSeedReads; j++) {
+            const uint64_t i = c0 + (uint64_t)j * kBlock + threadIdx.x;
+            slot[j] = i < n ? atomicAdd(&cnt[bit(walk, j) ? 0 : 1], 1u) : 0u;
+        }
+        __syncthreads();
+        if (threadIdx.x < 2 && cnt[threadIdx.x])
+            base[threadIdx.x] = atomicAdd(threadIdx.x == 0 ? a.queue_rc_count : a.queue_na2_count,
+                                          (unsigned long long)cnt[threadIdx.x]);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kSeedReads; j++) {
+            const uint64_t i = c0 + (uint64_t)j * kBlock + threadIdx.x;
+            if (i >= n) continue;
+            const uint32_t r = a.queue_na[i];
+            if (bit(walk, j)) {
+                a.queue_rc[base[0] + slot[j]] = r;
+                a.queue_rc_anc[base[0] + slot[j]] = seed[j];
+            } else {
+                a.queue_na2[base[1] + slot[j]] = r;
+            }
+        }
+        __syncthreads();  // (cnt / base are reset by the next chunk)
+    }
+}
+
+// k_align_lane_rc: the reads k_align_lane found no seed for and k_rc_seeds a
+// reverse-complement one (a.queue_rc), walked on the reverse strand
+// (na_rc_walk) -- about half of a real FASTQ is the reverse complement of
+// some genome stretch, and the forward-only lookups of the reference
+// (src/kmer.py:419-429) must show every one of its windows absent.  A walked
+// read needs the Bloom filter only for the few windows the walk leaves (N
+// runs of the genome, two mismatches in one window, a bit set); a read it
+// cannot walk goes on to k_align_lane_na (a.queue_na2), which tests every
+// window.  The reads' counts vary a lot (0 ... 120 windows),
 // so the Bloom groups are tested by the whole wave together: every lane lists
 // its read's groups with a window to look up, the lists are concatenated in
 // LDS and each pass takes 64 groups, one per lane (bloom_group without the
@@ -1488,8 +1599,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
     rows[threadIdx.x][kLaneWords] = 0;
     const int lane = lane_id();
     const uint32_t wv = threadIdx.x >> 6, wbase = threadIdx.x & ~63u;
-    const uint64_t n = *a.queue_na_count;
-    const bool forward = n < a.na_min;  // (few such reads: all on to k_align_lane_na, which hands them on)
+    const uint64_t n = *a.queue_rc_count;
     uint32_t n_amb = 0, n_unm = 0;
     uint32_t hr_sum = 0, qf_sum = 0;
     for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock + wbase; c0 < n; c0 += (uint64_t)gridDim.x * kBlock) {
@@ -1497,23 +1607,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
         LaneRead S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         uint32_t r = 0;
+        uint64_t seed = 0;
         if (i < n) {
-            r = a.queue_na[i];
-            if (forward) S.kind = LANE_NOANCHOR;
-            else lane_prep<NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
+            r = a.queue_rc[i];
+            seed = a.queue_rc_anc[i];
+            lane_prep<NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
         }
         const uint64_t *row = rows[threadIdx.x];
         uint32_t gm = 0;  // groups with a window to look up
         uint64_t lk0 = 0, lk1 = 0;
         if (S.kind == LANE_WALK) {
-            if (na_rc_walk(a, row, S.len, S.W, lk0, lk1)) {
+            if (na_rc_walk(a, row, S.len, S.W, seed, lk0, lk1)) {
                 if (WIN_Q) {  // windows failing --min-kmer-quality are never looked up
                     lk0 &= ~S.F0;
                     lk1 &= ~S.F1;
                 }
+                if (a.bloom) {
 #pragma unroll
-                for (int g = 0; g < kRcGroups; g++)
-                    gm |= (((g < 8 ? lk0 >> (8 * g) : lk1 >> (8 * g - 64)) & 0xFFull) != 0) ? 1u << g : 0u;
+                    for (int g = 0; g < kRcGroups; g++)
+                        gm |= (((g < 8 ? lk0 >> (8 * g) : lk1 >> (8 * g - 64)) & 0xFFull) != 0) ? 1u << g : 0u;
+                }
             } else {
                 S.kind = LANE_NOANCHOR;
             }
@@ -1522,8 +1635,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
         const uint32_t c = (uint32_t)__popc(gm);
         const uint32_t incl = wave_incl_scan(c);
         const uint32_t total = __shfl(incl, 63);
-        pmask[threadIdx.x][0] = 0;
-        pmask[threadIdx.x][1] = 0;
+        // (without a Bloom filter every listed window is probed)
+        pmask[threadIdx.x][0] = a.bloom ? 0ull : lk0;
+        pmask[threadIdx.x][1] = a.bloom ? 0ull : lk1;
         {
             uint32_t e = incl - c, m = gm;
             while (m) {
@@ -1543,9 +1657,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
                 const uint32_t l = t >> 16, g = (t >> 8) & 255u, act = t & 255u;
                 uint32_t pb = 0;
                 uint4 cur = make_uint4(0, 0, 0, 0);
-                const uint32_t got = a.k == 31
-                                         ? bloom_group<8, 31, false>(a, rows[wbase + l], 8 * g, act, true, pb, cur, nullptr)
-                                         : bloom_group<8, 0, false>(a, rows[wbase + l], 8 * g, act, true, pb, cur, nullptr);
+                bool cm = true;
+                const uint32_t got =
+                    a.k == 31 ? bloom_group<8, 31, false>(a, rows[wbase + l], 8 * g, act, true, pb, cur, cm, nullptr)
+                              : bloom_group<8, 0, false>(a, rows[wbase + l], 8 * g, act, true, pb, cur, cm, nullptr);
                 if (got) atomicOr(&pmask[wbase + l][g >> 3], (unsigned long long)got << (8 * (g & 7)));
             }
         }
