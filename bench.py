@@ -55,6 +55,7 @@ import argparse
 import json
 import subprocess
 import os
+import re
 import sys
 import time
 
@@ -200,7 +201,9 @@ def counter_pass(args, cfg, kept_path, save_dir=None):
     except subprocess.TimeoutExpired:
         return None, "rocprofv3 child timed out"
     if r.returncode != 0:
-        return None, f"rocprofv3 child failed (rc {r.returncode}): {r.stderr[-300:]}"
+        # (the profiler's own info / warning log lines dropped: the child's error is above them)
+        err = "\n".join(ln for ln in r.stderr.splitlines() if not re.match(r"^[IW]\d{8} ", ln))
+        return None, f"rocprofv3 child failed (rc {r.returncode}): {err[-600:]}"
     dbs = glob.glob(os.path.join(tmp, "**", "*.db"), recursive=True)
     if not dbs:
         return None, "no rocprofv3 database written"
@@ -642,6 +645,9 @@ def main():
         index.close()
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
+        # the library's slab pool keeps freed index buffers for the next build
+        # (pa_mem.cpp): handed back here, or C5's child finds no room for its own
+        N.mem_trim(local)
         per, tnote = counter_pass(args, cfg, kept_path, args.profile_dir)
     else:
         tnote = "not measured (--no-traffic, or a rank of a multi-GPU run)"
