@@ -797,7 +797,10 @@ void launch_exact_nw(int nw, const ExactArgs &x, unsigned grid, hipStream_t st) 
         case 2: launch_exact<2>(x, grid, st); break;
         case 3: launch_exact<3>(x, grid, st); break;
         case 4: launch_exact<4>(x, grid, st); break;
-        default: launch_exact<5>(x, grid, st); break;
+        case 5: launch_exact<5>(x, grid, st); break;
+        case 6: launch_exact<6>(x, grid, st); break;
+        case 7: launch_exact<7>(x, grid, st); break;
+        default: launch_exact<8>(x, grid, st); break;
     }
 }
 

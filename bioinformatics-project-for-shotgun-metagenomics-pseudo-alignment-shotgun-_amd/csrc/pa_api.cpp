@@ -115,7 +115,7 @@ pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t 
     PA_CHECK(out != nullptr, PA_EINVAL, "out must not be NULL");
     *out = nullptr;
     PA_CHECK(genome_off != nullptr, PA_EINVAL, "genome_off must not be NULL");
-    PA_CHECK(k <= PA_MAX_K, PA_EUNSUPPORTED, "k-mer length above PA_MAX_K (159) is not supported");
+    PA_CHECK(k <= PA_MAX_K, PA_EUNSUPPORTED, "k-mer length above PA_MAX_K (255) is not supported");
     PA_CHECK(n_genomes <= PA_MAX_GENOMES, PA_EUNSUPPORTED,
              "more than PA_MAX_GENOMES (2^20 - 1) genomes: the Summary order keys hold a list position in 20 bits");
     for (uint32_t g = 0; g < n_genomes; g++)

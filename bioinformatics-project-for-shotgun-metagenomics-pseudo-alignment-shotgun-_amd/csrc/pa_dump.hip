@@ -418,6 +418,9 @@ pa_status index_dumpref(const pa_index *idx, const uint8_t *keep, const uint32_t
             case 3: rc = dump_nw<3>(idx, keep, st, h_t, h_flags, nv); break;
             case 4: rc = dump_nw<4>(idx, keep, st, h_t, h_flags, nv); break;
             case 5: rc = dump_nw<5>(idx, keep, st, h_t, h_flags, nv); break;
+            case 6: rc = dump_nw<6>(idx, keep, st, h_t, h_flags, nv); break;
+            case 7: rc = dump_nw<7>(idx, keep, st, h_t, h_flags, nv); break;
+            case 8: rc = dump_nw<8>(idx, keep, st, h_t, h_flags, nv); break;
             default: set_error("unsupported k");
         }
         if (rc != PA_OK) return rc;

@@ -1504,7 +1504,10 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
                 case 2: hipLaunchKernelGGL(k_hll<2>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
                 case 3: hipLaunchKernelGGL(k_hll<3>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
                 case 4: hipLaunchKernelGGL(k_hll<4>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
-                default: hipLaunchKernelGGL(k_hll<5>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                case 5: hipLaunchKernelGGL(k_hll<5>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                case 6: hipLaunchKernelGGL(k_hll<6>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                case 7: hipLaunchKernelGGL(k_hll<7>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
+                default: hipLaunchKernelGGL(k_hll<8>, grid, dim3(kBlock), 0, st, idx->codes, idx->h_goff[g], nwin, (int)k, mask0, reg); break;
             }
         }
         std::vector<uint32_t> h(1u << kHllBits);
@@ -1555,6 +1558,9 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         case 3: rc = build_nw<3>(idx, st); break;
         case 4: rc = build_nw<4>(idx, st); break;
         case 5: rc = build_nw<5>(idx, st); break;
+        case 6: rc = build_nw<6>(idx, st); break;
+        case 7: rc = build_nw<7>(idx, st); break;
+        case 8: rc = build_nw<8>(idx, st); break;
         default: set_error("unsupported k");
     }
     tm.mark("insert + sets");
@@ -1587,7 +1593,10 @@ pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint3
         case 2: rc = lookup_nw<2>(idx, d_k, n, d_c, d_s, st); break;
         case 3: rc = lookup_nw<3>(idx, d_k, n, d_c, d_s, st); break;
         case 4: rc = lookup_nw<4>(idx, d_k, n, d_c, d_s, st); break;
-        default: rc = lookup_nw<5>(idx, d_k, n, d_c, d_s, st); break;
+        case 5: rc = lookup_nw<5>(idx, d_k, n, d_c, d_s, st); break;
+        case 6: rc = lookup_nw<6>(idx, d_k, n, d_c, d_s, st); break;
+        case 7: rc = lookup_nw<7>(idx, d_k, n, d_c, d_s, st); break;
+        default: rc = lookup_nw<8>(idx, d_k, n, d_c, d_s, st); break;
     }
     if (rc == PA_OK) {
         PA_HIP(hipMemcpyAsync(cls_out, d_c, n * 8, hipMemcpyDeviceToHost, st));
@@ -1627,7 +1636,10 @@ pa_status index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint
         case 2: extsim_slots_nw<2>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
         case 3: extsim_slots_nw<3>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
         case 4: extsim_slots_nw<4>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
-        default: extsim_slots_nw<5>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        case 5: extsim_slots_nw<5>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        case 6: extsim_slots_nw<6>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        case 7: extsim_slots_nw<7>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
+        default: extsim_slots_nw<8>(idx, d_group, n_groups, d_tot, d_uniq, d_cc, st); break;
     }
     if (idx->n_multi > 0)
         hipLaunchKernelGGL(k_extsim_classes, dim3(cgrid), dim3(kBlock), 0, st, idx->n_multi, idx->class_off,

@@ -255,7 +255,10 @@ pa_status index_positions(const pa_index *idx, const char *kmers, uint64_t n, ui
         case 2: s = scan_nw<2>(idx, keys, refs.size(), dh, st); break;
         case 3: s = scan_nw<3>(idx, keys, refs.size(), dh, st); break;
         case 4: s = scan_nw<4>(idx, keys, refs.size(), dh, st); break;
-        default: s = scan_nw<5>(idx, keys, refs.size(), dh, st); break;
+        case 5: s = scan_nw<5>(idx, keys, refs.size(), dh, st); break;
+        case 6: s = scan_nw<6>(idx, keys, refs.size(), dh, st); break;
+        case 7: s = scan_nw<7>(idx, keys, refs.size(), dh, st); break;
+        default: s = scan_nw<8>(idx, keys, refs.size(), dh, st); break;
     }
     if (s != PA_OK) return s;
     std::vector<pa_kmer_hit> outv;

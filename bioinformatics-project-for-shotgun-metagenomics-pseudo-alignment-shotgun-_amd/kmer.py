@@ -23,7 +23,7 @@ attributes, return values and exceptions.  What changes is where the work runs:
 
 Results (per-genome unique/ambiguous counts, filtered_* counters, the Summary
 key order) are bit-exact to the reference; see DESIGN.md for the quirk list
-this reproduces.  Known deviations: k above 159 raises PaUnsupported; argument
+this reproduces.  Known deviations: k above 255 raises PaUnsupported; argument
 errors of a batch (TypeError / ValueError / AddingExistingRead) are raised
 before any read of the batch is counted rather than at the offending read.
 """

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("PA_LIBRARY", os.path.join(HERE, "libpa.so"))
 
 PA_OK, PA_EINVAL, PA_ETYPE, PA_ENOMEM, PA_EDEVICE, PA_EUNSUPPORTED, PA_EINTERNAL, PA_ENOTCANON, PA_EIO = range(9)
 PA_FASTA, PA_FASTQ = 0, 1
-PA_MAX_K = 159
+PA_MAX_K = 255
 PA_MAX_GENOMES = (1 << 20) - 1
 PA_COMM_ID_BYTES = 128
 HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4

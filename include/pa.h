@@ -77,7 +77,7 @@ typedef int32_t pa_status;
 #define PA_ENOTCANON 7     /* ingest: text outside the canonical FASTA/FASTQ subset (use the exact grammar) */
 #define PA_EIO 8           /* ingest: file could not be opened / read */
 
-#define PA_MAX_K 159       /* k-mers up to 159 bases: keys of up to 5 x 64-bit words */
+#define PA_MAX_K 255       /* k-mers up to 255 bases: keys of up to 8 x 64-bit words */
 
 #define PA_DROPPED 0
 #define PA_UNMAPPED 1

@@ -100,7 +100,7 @@ def _midsize(seed, dup=True):
     return [(h, bytes(g).decode()) for h, g in zip(heads, gens)]
 
 
-@pytest.mark.parametrize("k,round_", [(31, 0), (15, 50000), (40, 0), (31, 7777)])
+@pytest.mark.parametrize("k,round_", [(31, 0), (15, 50000), (40, 0), (31, 7777), (200, 0)])
 def test_dumpref_midsize_vs_oracle(k, round_, monkeypatch, tmp_path):
     if round_:
         monkeypatch.setenv("PA_DUMP_ROUND", str(round_))

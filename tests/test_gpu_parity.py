@@ -360,7 +360,7 @@ def test_edge_cases():
         assert res.fetch()[0].tolist() == [0, 0, 2, 0, 0, 0]
     # k > PA_MAX_K fails loudly
     with pytest.raises(N.PaUnsupported):
-        N.Index(["A" * 200], 160)
+        N.Index(["A" * 300], N.PA_MAX_K + 1)
     # invalid genome characters are rejected, like the FASTA grammar
     with pytest.raises(ValueError):
         N.Index(["ACGTX"], 3)
@@ -380,6 +380,38 @@ def test_edge_cases():
     N.align(index, N.Reads.upload(seq, qual, off), N.Params.make(), 0, res)
     o = oix.align(seq.tobytes(), qual.tobytes(), off, detail=False)
     assert res.fetch()[0].tolist() == o.stats.tolist()
+
+
+@pytest.mark.parametrize("k", [160, 191, 192, 224, 255])
+def test_long_k_vs_oracle(k):
+    """k-mers of six to eight 64-bit key words (160 <= k <= PA_MAX_K): the
+    reference takes any k (src/kmer.py:84-94); index size, per-k-mer genome
+    lists and every read's outcome against the oracle, with and without the
+    filters."""
+    g = synth.family_genomes(4, 3000, seed=k, family_size=2, sub_rate=0.01, conserved_len=300, n_rate=1e-3)
+    index = N.Index(g, k)
+    oix = O.OracleIndex(g, k)
+    assert index.n_kmers == oix.n_kmers
+    L = k + 60
+    seq, qual, _ = synth.sample_reads(g, 400, L, seed=k + 1, err_rate=0.002)
+    off = np.arange(401, dtype=np.uint64) * L
+    for prm in (dict(), dict(m=0, p=0), dict(mrq=53, mkq=58, mg=1)):
+        res = N.Result(index)
+        N.align(index, N.Reads.upload(seq, qual, off), N.Params.make(prm.get("m", 1), prm.get("p", 1), prm.get("mrq"),
+                                                                       prm.get("mkq"), prm.get("mg")), 0, res)
+        stats, uq, am, _ = res.fetch()
+        o = oix.align(seq.tobytes(), qual.tobytes(), off, m=prm.get("m", 1), p=prm.get("p", 1), mrq=prm.get("mrq"),
+                      mkq=prm.get("mkq"), mg=prm.get("mg"), detail=False)
+        assert stats.tolist() == o.stats.tolist(), (k, prm)
+        assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist()
+    # the genome lists of k-mers taken from the genomes (and of absent ones)
+    text = [x.tobytes().decode() if hasattr(x, "tobytes") else x for x in g]
+    keys = [t[j:j + k] for t in text for j in (0, 777, len(t) - k)] + ["A" * k, "C" * k]
+    cls, size = index.lookup(keys)
+    for km, c, sz in zip(keys, cls, size):
+        want = oix.lookup(km)
+        got = index.class_genomes(int(c)) if c >= 0 else []
+        assert got == want and int(sz) == len(want), (k, km[:20])
 
 
 def _walk_adversarial_case(seed, n_genomes, k):
