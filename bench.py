@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the MI355X pseudo-alignment engine.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c3raw|c2mix|c2rc|c4|c5|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c3raw|c2mix|c2rc|c5|c1]
     torchrun --nproc-per-node N bench.py --gpus N ...            (one rank per GPU)
 
 With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset), this
@@ -10,18 +10,27 @@ a 127.0.0.1 rendezvous in their environment) before anything touches the GPU,
 relays rank 0's line and exits non-zero if any rank fails.  A rank whose
 WORLD_SIZE differs from an explicit --gpus exits non-zero.
 
-Metric (BASELINE.json): reads/s pseudo-aligned, k=31, 150 bp reads, plus the
-achieved fraction of the HBM roofline.  Workload (SURVEY.md section 8d,
-config C2 = BASELINE.json configs[1]): 50 synthetic 2 Mbp genomes in families
-of 5 (1% substitutions within a family, a 5 kb segment shared by all, N runs),
-k=31, and per GPU 10M x 150 bp forward-strand reads with 0.5% substitution
-errors and raw-ASCII qualities, synthesized ON the device (they are resident in
-HBM before the timed region; nothing crosses PCIe while timing).
+Metric (BASELINE.json): reads/s pseudo-aligned, k=31, 150 bp reads, at
+1/2/4/8 GPUs, plus the achieved fraction of the HBM roofline.  The DEFAULT
+workload is the metric's own configuration, C4 (BASELINE.json configs[3], the
+north star's "500-genome reference on 8 x MI355X"): 500 synthetic 2 Mbp genomes
+in families of 5 (1% substitutions within a family, a 5 kb segment shared by
+all, N runs), k=31, and per GPU 62.5M x 150 bp forward-strand reads with 0.5%
+substitution errors and raw-ASCII qualities -- 500M reads over 8 GPUs --
+synthesized ON the device (resident in HBM before the timed region; nothing
+crosses PCIe while timing).  The other configs (--config) are the parity-test
+and robustness cases of SURVEY.md section 8d.
 
-A step = one pass of the align kernels over the rank's 10M reads (counters
-reset, pa_align, and for N > 1 the RCCL SUM/MIN all-reduce of the counter
-blocks).  Scaling is weak: every rank aligns its own 10M reads (global read
-indices rank*10M ...), and value = all ranks' reads / max-over-ranks time.
+A step = one pass of the align kernels over the rank's reads (counters reset,
+pa_align, and for N > 1 the RCCL SUM/MIN all-reduce of the counter blocks).
+Scaling is weak: rank r aligns global reads [r*R, (r+1)*R) with R = the
+config's reads per GPU (rank_reads(); C4 at N = 8 tiles the 500M reads
+exactly), and value = all ranks' reads / max-over-ranks time.  With the nccl
+backend every rank checks that an RCCL communicator of the job spans all
+ranks (ncclCommCount) and exits non-zero otherwise.
+
+At N = 1 the line also carries the end-to-end `dumpalign` CLI figure on the C2
+files (scripts/e2e_cli.py, sub-record end_to_end) unless --no-e2e.
 
 roofline (the align pass: k_align_lane + k_align_fast over the reads the lane
 kernel leaves; duration from HIP events libpa records on
@@ -346,6 +355,14 @@ def cpu_baseline(cfg, genomes, index, reads, prm_kw, target_s: float, restricted
              "oracle": "restricted" if restricted else "full"})
 
 
+def rank_reads(cfg, rank: int, world: int):
+    """(first global read index, reads) of `rank` in a `world`-rank job: weak
+    scaling, R = cfg["reads_per_gpu"] reads per rank, contiguous, so the ranks
+    of a job tile [0, world * R) exactly (C4 at N = 8: 500M reads)."""
+    npg = int(cfg["reads_per_gpu"])
+    return rank * npg, npg
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as so:
@@ -412,7 +429,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=None, help="ranks (GPUs); default WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS),
+                    help="workload (default c4: the metric's configuration, BASELINE.json configs[3])")
     ap.add_argument("--reads-per-gpu", type=int, default=None)
     ap.add_argument("--genome-len", type=int, default=None, help="override the genome length (experiments)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -424,7 +442,7 @@ def main():
     ap.add_argument("--reduce", choices=("torch", "capi"), default="torch",
                     help="N > 1: all-reduce through torch.distributed (RCCL) or libpa's pa_counters_reduce")
     ap.add_argument("--no-e2e", action="store_true",
-                    help="C2 at N=1: skip the end-to-end dumpalign CLI figure (scripts/e2e_cli.py)")
+                    help="N=1: skip the end-to-end dumpalign CLI figure on the C2 files (scripts/e2e_cli.py)")
     ap.add_argument("--ranks-share-device", action="store_true", help=argparse.SUPPRESS)  # 1-GPU rehearsal
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default=None, help=argparse.SUPPRESS)
     ap.add_argument("--fail-rank", type=int, default=None, help=argparse.SUPPRESS)  # launcher test: this rank dies
@@ -516,8 +534,8 @@ def main():
     prepare_s = time.perf_counter() - t0
     index_total_s = time.perf_counter() - t_index0
     info = index.info()
-    npg = cfg["reads_per_gpu"]
-    reads = N.Reads.synthesize(index, npg, cfg["read_len"], first_read=rank * npg, seed=2, sub_rate=cfg["read_err"],
+    first_read, npg = rank_reads(cfg, rank, world)
+    reads = N.Reads.synthesize(index, npg, cfg["read_len"], first_read=first_read, seed=2, sub_rate=cfg["read_err"],
                                stream=stream, rc_rate=cfg.get("rc_rate", 0.0),
                                foreign_rate=cfg.get("foreign_rate", 0.0))
     result = N.Result(index)
@@ -536,10 +554,13 @@ def main():
         rccl_ranks = probe.n_ranks
         if probe is not comm:
             probe.close()
+        if rccl_ranks != world:
+            log(f"[rank {rank}] error: the RCCL communicator spans {rccl_ranks} ranks, WORLD_SIZE is {world}")
+            sys.exit(4)
 
     def step():
         result.reset(stream)
-        N.align(index, reads, prm, rank * npg, result, stream)
+        N.align(index, reads, prm, first_read, result, stream)
         if world > 1:
             if comm is not None:
                 pa_dist.reduce_result_capi(result, comm, stream)
@@ -590,7 +611,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic: seeded numpy genomes, reads sampled on the device (resident in HBM before timing)",
         "config": {"workload": cfg["name"], "genomes": cfg["n_genomes"], "genome_len": cfg["genome_len"],
-                   "k": cfg["k"], "reads_per_gpu": npg, "read_len": cfg["read_len"],
+                   "k": cfg["k"], "reads_per_gpu": npg, "job_reads_per_step": world * npg,
+                   "read_len": cfg["read_len"],
                    "filters": cfg["params"] or None, "parallelism": f"read-sharded x{world}, index replicated",
                    "reduce": args.reduce if world > 1 else None, "backend": backend, "rccl_ranks": rccl_ranks,
                    "read_mix": {"reverse_complement": cfg.get("rc_rate", 0.0), "foreign": cfg.get("foreign_rate", 0.0),
@@ -676,13 +698,14 @@ def main():
     rl["bound"] = bound_of(rl["frac"], rl.get("sq"))
     if kept_path:
         os.unlink(kept_path)
-    if rank == 0 and world == 1 and args.config == "c2" and not args.no_e2e and not args.traffic_child:
+    if rank == 0 and world == 1 and not args.no_e2e and not args.traffic_child:
         # the user-visible figure beside the device-resident one: `main.py -t
         # dumpalign` on the C2 files (FASTA + 3.2 GB FASTQ, page cache warm)
         for h in (result, reads, index):
             h.close()
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
+        N.mem_trim(local)
         out["end_to_end"] = e2e_pass()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -164,12 +164,18 @@ pa_status scan_nw(const pa_index *idx, const std::vector<uint64_t> &keys, size_t
     unsigned long long *d_n = nullptr;
     DevHit *d_hits = nullptr;
     uint64_t cap = 1u << 16;
-    PA_HIP(pa::dev_malloc(&d_qt, qsize * sizeof(QEnt<NW>)));
-    PA_HIP(pa::dev_malloc(&d_n, 8));
-    PA_HIP(hipMemcpyAsync(d_qt, qt.data(), qsize * sizeof(QEnt<NW>), hipMemcpyHostToDevice, st));
     pa_status rc = PA_OK;
-    for (int attempt = 0; attempt < 2; attempt++) {
-        if (hipMalloc(&d_hits, cap * sizeof(DevHit)) != hipSuccess) {  // (small: straight from the driver)
+    // (every exit below goes through the one cleanup at the end)
+    if (pa::dev_malloc(&d_qt, qsize * sizeof(QEnt<NW>)) != hipSuccess || pa::dev_malloc(&d_n, 8) != hipSuccess) {
+        pa::set_error("pa_index_positions: out of device memory for the query table");
+        rc = PA_ENOMEM;
+    } else if (hipMemcpyAsync(d_qt, qt.data(), qsize * sizeof(QEnt<NW>), hipMemcpyHostToDevice, st) != hipSuccess) {
+        pa::set_error("pa_index_positions: HIP error copying the query table");
+        rc = PA_EDEVICE;
+    }
+    for (int attempt = 0; rc == PA_OK && attempt < 2; attempt++) {
+        if (pa::dev_malloc(&d_hits, cap * sizeof(DevHit)) != hipSuccess) {
+            d_hits = nullptr;
             pa::set_error("pa_index_positions: out of device memory for the hits");
             rc = PA_ENOMEM;
             break;
@@ -194,13 +200,13 @@ pa_status scan_nw(const pa_index *idx, const std::vector<uint64_t> &keys, size_t
             }
             break;
         }
-        hipFree(d_hits);  // more hits than room: once more with room for all of them
+        pa::dev_free(d_hits);  // more hits than room: once more with room for all of them
         d_hits = nullptr;
         cap = n;
     }
-    if (d_hits) hipFree(d_hits);
-    pa::dev_free(d_qt);
-    pa::dev_free(d_n);
+    if (d_hits) pa::dev_free(d_hits);
+    if (d_qt) pa::dev_free(d_qt);
+    if (d_n) pa::dev_free(d_n);
     return rc;
 }
 

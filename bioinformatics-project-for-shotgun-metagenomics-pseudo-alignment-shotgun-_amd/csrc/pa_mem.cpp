@@ -120,10 +120,20 @@ size_t trim_locked(Pool &P, int dev) {
 
 hipError_t dev_malloc_raw(void **p, size_t n) {
     Pool &P = pool();
-    if (!P.on || n < P.min_bytes) return hipMalloc(p, n);
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
+    if (!P.on || n < P.min_bytes) {
+        e = hipMalloc(p, n);
+        if (e == hipSuccess || !P.on) return e;
+        // small buffers too: idle slabs can hold most of the device's memory
+        (void)hipGetLastError();
+        {
+            std::lock_guard<std::mutex> g(P.mu);
+            trim_locked(P, dev);
+        }
+        return hipMalloc(p, n);
+    }
     const size_t len = (n + kGranule - 1) / kGranule * kGranule;
     std::lock_guard<std::mutex> g(P.mu);
     size_t si = 0, off = 0;
@@ -149,23 +159,42 @@ hipError_t dev_malloc_raw(void **p, size_t n) {
     return hipSuccess;
 }
 
+// A pooled range is reusable only once no queued work can still touch it:
+// hipFree waits for the device, so the pool does too before the range goes
+// back (kernels of the public async API on a caller's stream may still read a
+// buffer whose handle was freed; the next dev_malloc could hand the range to a
+// memset or copy on another stream).  The range stays in `live` while
+// waiting, so no other thread can take it meanwhile.
 hipError_t dev_free(void *p) {
     if (!p) return hipSuccess;
     Pool &P = pool();
+    int sdev = -1;
     {
         std::lock_guard<std::mutex> g(P.mu);
         auto it = P.live.find(p);
-        if (it != P.live.end()) {
-            Slab &s = P.slabs[it->second.slab];
-            s.free_bytes += it->second.len;
-            give(s, it->second.off, it->second.len);
-            P.live.erase(it);
-            return hipSuccess;
-        }
+        if (it != P.live.end()) sdev = P.slabs[it->second.slab].dev;
     }
-    return hipFree(p);
+    if (sdev < 0) return hipFree(p);
+    int cur = 0;
+    hipGetDevice(&cur);
+    if (cur != sdev) hipSetDevice(sdev);
+    const hipError_t e = hipDeviceSynchronize();
+    if (cur != sdev) hipSetDevice(cur);
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.live.find(p);
+    if (it != P.live.end()) {
+        Slab &s = P.slabs[it->second.slab];
+        s.free_bytes += it->second.len;
+        give(s, it->second.off, it->second.len);
+        P.live.erase(it);
+    }
+    return e;
 }
 
+// Free memory as one allocation could use it: the driver's free bytes, plus
+// every idle slab (a request that fits none is met by trimming them), plus
+// the largest free range of a slab in use -- not the sum of scattered ranges,
+// which no single buffer can span.  Callers size tables and tiles on this.
 hipError_t dev_mem_info(size_t *free_b, size_t *total_b) {
     hipError_t e = hipMemGetInfo(free_b, total_b);
     if (e != hipSuccess) return e;
@@ -173,8 +202,16 @@ hipError_t dev_mem_info(size_t *free_b, size_t *total_b) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipSuccess;
     std::lock_guard<std::mutex> g(P.mu);
-    for (const Slab &s : P.slabs)
-        if (s.base && s.dev == dev) *free_b += s.free_bytes;
+    size_t largest = 0;
+    for (const Slab &s : P.slabs) {
+        if (!s.base || s.dev != dev) continue;
+        if (s.free_bytes == s.size) {
+            *free_b += s.size;
+            continue;
+        }
+        for (const auto &r : s.free) largest = std::max(largest, r.second);
+    }
+    *free_b += largest;
     return hipSuccess;
 }
 

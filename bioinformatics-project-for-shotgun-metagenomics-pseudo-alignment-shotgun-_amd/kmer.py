@@ -322,6 +322,17 @@ class KmerReference:
             out.setdefault(self.genomes[g], set()).add(p)
         return out
 
+    def _references_many(self, kmers: List[str]) -> List[Dict[Record, Set[int]]]:
+        """get_kmer_references of every k-mer of the list: one device scan
+        (pa_index_positions over the whole batch), hits split by query."""
+        if self._view is not None:
+            return [self._view.get(km, {}) for km in kmers]
+        out: List[Dict[Record, Set[int]]] = [{} for _ in kmers]
+        if kmers:
+            for q, g, p in self._index.positions(kmers, False).tolist():
+                out[q].setdefault(self.genomes[g], set()).add(p)
+        return out
+
     def get_kmer_references(self, kmer: str) -> Dict[Record, Set[int]]:
         if self._view is not None:
             return self._view.get(kmer, {})
@@ -447,13 +458,17 @@ class Read:
             k = ref.kmer_len
             windows = list(extract_kmers_from_genome(k, self.__raw_read))
             cls, size = ref.index.lookup([w for _, w in windows]) if windows else ([], [])
+            kept: Dict[str, int] = {}  # included k-mer -> its set size, first inclusion order
             for (start, km), c, s in zip(windows, cls, size):
                 if mkq is not None and self.kmer_quality(start, k) < mkq:
                     continue
                 if c < 0 or (mg is not None and int(s) > mg):
                     continue
-                refs = ref.get_kmer_references(km)
-                self._kmers[km] = ReadKmer(KmerSpecifity.SPECIFIC if int(s) == 1 else KmerSpecifity.UNSPECIFIC, refs)
+                kept.setdefault(km, int(s))
+            # every included k-mer's references from one batched device scan
+            names = list(kept)
+            for km, refs in zip(names, ref._references_many(names)):
+                self._kmers[km] = ReadKmer(KmerSpecifity.SPECIFIC if kept[km] == 1 else KmerSpecifity.UNSPECIFIC, refs)
         return self._kmers
 
     def _packed(self):

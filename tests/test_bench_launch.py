@@ -84,6 +84,28 @@ def test_two_ranks_launched_by_bench_equal_one_process():
     index.close()
 
 
+def test_default_is_the_north_star_job():
+    """With no --config, bench.py measures the metric's configuration C4
+    (BASELINE.json configs[3]): 500 x 2 Mbp genomes, k = 31, 150 bp reads, and
+    the ranks of `--gpus 8` tile the north star's 500M reads exactly --
+    contiguous, disjoint, in rank order -- while every other N keeps 62.5M reads
+    per GPU (weak scaling)."""
+    sys.path.insert(0, REPO)
+    import bench
+    ap_default = [a for a in open(BENCH).read().splitlines() if '"--config", default=' in a]
+    assert ap_default and 'default="c4"' in ap_default[0]
+    cfg = bench.CONFIGS["c4"]
+    assert (cfg["n_genomes"], cfg["genome_len"], cfg["k"], cfg["read_len"]) == (500, 2_000_000, 31, 150)
+    assert cfg["params"] == {} and cfg.get("rc_rate", 0) == 0 and cfg.get("foreign_rate", 0) == 0
+    for world in (1, 2, 4, 8):
+        spans = [bench.rank_reads(cfg, r, world) for r in range(world)]
+        assert all(n == 62_500_000 for _, n in spans)
+        assert spans[0][0] == 0
+        assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+        assert spans[-1][0] + spans[-1][1] == world * 62_500_000
+    assert sum(n for _, n in (bench.rank_reads(cfg, r, 8) for r in range(8))) == 500_000_000
+
+
 def test_kernel_short_names():
     """Counter rows are matched to kernels by their own mangled names (the
     length prefix keeps k_align_lane apart from k_align_lane_na)."""
