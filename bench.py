@@ -114,6 +114,12 @@ CONFIGS = {
     # absent from the index (every window Bloom-tested, k_align_lane_na)
     "c2fg": dict(BASE, foreign_rate=0.5,
                  name="C2 foreign mix: C2 genomes, 10M reads per GPU: 50% unindexed organism, 0.5% substitutions"),
+    # the lane path's limits: the reference's demo runs use k = 75
+    # and 150 (src/RUN_LOG:30, 67); longer keys and reads than the lane kernels
+    # take (k <= 31, <= 176 bp) go to the wave kernel
+    "c2k63": dict(BASE, k=63, name="C2 genomes, 10M x 150 bp reads per GPU, k=63 (2-word keys)"),
+    "c2k75": dict(BASE, k=75, name="C2 genomes, 10M x 150 bp reads per GPU, k=75 (3-word keys; src/RUN_LOG:30)"),
+    "c2l250": dict(BASE, read_len=250, name="C2 genomes, 10M x 250 bp reads per GPU, k=31"),
     "c1": dict(BASE, n_genomes=3, genome_len=5000, family=3, sub=0.02, conserved=300, k=21, reads_per_gpu=1000,
                read_len=100, read_err=0.01, name="C1: 3 x 5 kb genomes, 1k x 100 bp reads, k=21"),
 }

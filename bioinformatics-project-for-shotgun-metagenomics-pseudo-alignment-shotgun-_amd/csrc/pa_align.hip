@@ -1040,7 +1040,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
     PA_TRY(prepare_exact(idx, r, x, egrid));
     x.a = a;
     x.detail = 0;
-    const bool fast_ok = idx->k > 0 && idx->nw <= 2 && idx->n_kmers > 0;
+    const bool fast_ok = idx->k > 0 && idx->nw <= 4 && idx->n_kmers > 0;  // (k <= 127: the wave kernel's keys)
     // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
     const char *no_lane = std::getenv("PA_NO_LANE");
     const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile_lw && !(no_lane && no_lane[0] == '1');
@@ -1134,7 +1134,10 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
         }
         {
             KernelTimer kt(idx, st, PA_PROF_WAVE);
-            PA_TRY(idx->nw == 1 ? launch_fast_wpl<1>(a, wpl, st) : launch_fast_wpl<2>(a, wpl, st));
+            PA_TRY(idx->nw == 1   ? launch_fast_wpl<1>(a, wpl, st)
+                   : idx->nw == 2 ? launch_fast_wpl<2>(a, wpl, st)
+                   : idx->nw == 3 ? launch_fast_wpl<3>(a, wpl, st)
+                                  : launch_fast_wpl<4>(a, wpl, st));
         }
         if (idx->profile) {
             PA_HIP(hipEventRecord(e1, st));

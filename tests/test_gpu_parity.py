@@ -188,7 +188,12 @@ SYNTH = [
     (10, 9000, 5, 0.02, 31, 2000, 250, 0.01, [dict(), dict(m=0, p=0), dict(mkq=58)]),
     (5, 7000, 5, 0.01, 32, 2000, 120, 0.01, [dict(), dict(m=0, p=0)]),  # 2-word keys, fast path
     (5, 7000, 5, 0.01, 45, 1500, 150, 0.01, [dict(), dict(m=0, p=0)]),
-    (4, 5000, 2, 0.02, 64, 800, 150, 0.005, [dict(), dict(m=0, p=0)]),  # 3-word keys, exact path
+    (4, 5000, 2, 0.02, 64, 800, 150, 0.005, [dict(), dict(m=0, p=0)]),  # 3-word keys, wave kernel
+    (5, 7000, 5, 0.01, 63, 1500, 150, 0.01, [dict(), dict(m=0, p=0), dict(mrq=58, mkq=59, mg=2)]),
+    # the reference's own demo k (src/RUN_LOG:30, 39): 3- and 4-word keys on the wave kernel
+    (4, 6000, 2, 0.02, 75, 1000, 150, 0.005, [dict(), dict(m=0, p=0), dict(mkq=58, mg=1)]),
+    (4, 6000, 2, 0.02, 100, 1000, 150, 0.005, [dict(), dict(m=0, p=0)]),
+    (4, 6000, 2, 0.02, 75, 800, 250, 0.005, [dict(), dict(m=0, p=0), dict(mrq=57, mkq=58, mg=1)]),  # 250 bp
     (3, 4000, 1, 0.0, 17, 1500, 40, 0.02, [dict(), dict(mkq=55)]),
     (70, 3000, 10, 0.01, 15, 3000, 80, 0.01, [dict(), dict(m=0, p=0)]),  # many genomes per class
     # families (1% apart) and 1.5% read errors: off-walk k-mers, sibling walks,
