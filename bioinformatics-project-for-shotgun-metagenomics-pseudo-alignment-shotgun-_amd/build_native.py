@@ -23,8 +23,8 @@ BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libpa.so")
 ARCH = os.environ.get("PA_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["pa_index.hip", "pa_align.hip", "pa_fastq.hip", "pa_dump.hip", "pa_kpos.hip", "pa_api.cpp", "pa_ingest.cpp", "pa_comm.cpp", "pa_gz.cpp", "pa_mem.cpp"]
-HEADERS = ["pa_device.h", "pa_internal.h", "pa_fast.h", "pa_lane.h", "pa_home.h", "pa_gz.h"]
+SOURCES = ["pa_index.hip", "pa_align.hip", "pa_fastq.hip", "pa_dump.hip", "pa_kpos.hip", "pa_api.cpp", "pa_ingest.cpp", "pa_comm.cpp", "pa_gz.cpp", "pa_pgz.cpp", "pa_mem.cpp"]
+HEADERS = ["pa_device.h", "pa_internal.h", "pa_fast.h", "pa_lane.h", "pa_home.h", "pa_gz.h", "pa_pgz.h"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-value", "-Wno-unused-result", f"-I{INCLUDE}"]
 
 

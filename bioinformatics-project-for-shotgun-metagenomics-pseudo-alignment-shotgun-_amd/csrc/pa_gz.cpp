@@ -7,7 +7,9 @@
 // trailer.  Its members are located without inflating anything, so they are
 // inflated on all host threads at once, each straight into its place in the
 // caller's buffer, and each checked against its CRC-32 and size.  Any other
-// gzip file (one member, as `gzip` writes) is inflated by zlib on one thread.
+// gzip file (one member, as `gzip` writes) is inflated on all host threads by
+// pa_pgz.cpp (block boundaries found by search, 32-KiB windows resolved once
+// the previous chunk is known; PA_PGZ=0: zlib on one thread).
 // Data that is not what gzip.open would read cleanly -- a bad CRC, a truncated
 // member, bytes after the last one -- gives PA_ENOTCANON, so the caller takes
 // the exact path, which raises the reference's own error.
@@ -19,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -26,6 +29,7 @@
 
 #include "pa_gz.h"
 #include "pa_internal.h"
+#include "pa_pgz.h"
 
 namespace pa {
 
@@ -47,7 +51,8 @@ struct Gz {
     std::vector<GzMember> members;
     uint64_t next = 0;  // next member to hand out
     uint64_t total = 0;
-    // any other gzip file
+    // any other gzip file: parallel inflate of the mapped file, or zlib
+    Pgz *pgz = nullptr;
     gzFile gz = nullptr;
     bool eof = false;
 };
@@ -125,8 +130,17 @@ pa_status gz_open(const char *path, int threads, Gz **out) {
             *out = g;
             return PA_OK;
         }
-        munmap(m, len);
         g->members.clear();
+        const char *e = std::getenv("PA_PGZ");
+        Pgz *p = nullptr;
+        if (!(e && e[0] == '0') && pgz_open((const uint8_t *)m, len, g->threads, &p) == PA_OK) {
+            g->pgz = p;
+            g->map = (const uint8_t *)m;
+            g->map_len = len;
+            *out = g;
+            return PA_OK;
+        }
+        munmap(m, len);
     }
     g->gz = gzopen(path, "rb");
     if (!g->gz) {
@@ -150,6 +164,7 @@ uint64_t gz_text_size(const Gz *g) { return g && g->bgzf ? g->total : 0; }
 
 pa_status gz_read(Gz *g, uint8_t *dst, uint64_t n, uint64_t *got, bool *eof) {
     *got = 0;
+    if (g->pgz) return pgz_read(g->pgz, dst, n, got, eof);
     if (!g->bgzf) {
         uint64_t k = 0;
         while (k < n) {
@@ -208,6 +223,7 @@ pa_status gz_read(Gz *g, uint8_t *dst, uint64_t n, uint64_t *got, bool *eof) {
 
 void gz_close(Gz *g) {
     if (!g) return;
+    if (g->pgz) pgz_close(g->pgz);
     if (g->map) munmap(const_cast<uint8_t *>(g->map), g->map_len);
     if (g->gz) gzclose(g->gz);
     delete g;

@@ -42,7 +42,7 @@ EXPORTS = (
     "pa_fastq_prefetch_start", "pa_align_fastq_prefetched", "pa_fastq_prefetch_free",
     "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_comm_count", "pa_counters_reduce",
     "pa_profile_enable", "pa_profile_read", "pa_profile_read_kernels", "pa_mem_trim",
-    "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free",
+    "pa_parse_text", "pa_parse_file", "pa_seqset_sizes", "pa_seqset_export", "pa_seqset_free", "pa_gz_inflate_file",
 )
 
 
@@ -153,6 +153,7 @@ def lib():
         "pa_mem_trim": (I32, [I32, ctypes.POINTER(U64)]),
         "pa_parse_text": (I32, [I32, P, U64, I32, I32, PP]),
         "pa_parse_file": (I32, [I32, ctypes.c_char_p, I32, PP]),
+        "pa_gz_inflate_file": (I32, [ctypes.c_char_p, I32, P, U64, ctypes.POINTER(U64)]),
         "pa_seqset_sizes": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "pa_seqset_export": (I32, [P, P, P, P, P]),
         "pa_seqset_free": (None, [P]),
@@ -218,6 +219,18 @@ def mem_trim(device: int = -1) -> int:
     n = U64(0)
     _check(lib().pa_mem_trim(int(device), ctypes.byref(n)))
     return int(n.value)
+
+
+def gz_inflate_file(path: str, cap: int, threads: Optional[int] = None) -> bytes:
+    """gzip.open(path).read() (src/data_file.py:123-125) on host threads
+    (pa_gz_inflate_file: BGZF members or search-split chunks in parallel, CRC-32
+    checked).  PaError (PA_ENOTCANON) for data gzip would not read cleanly; cap bounds
+    the text (ValueError past it)."""
+    buf = np.empty(max(int(cap), 1), dtype=np.uint8)
+    n = U64(0)
+    _check(lib().pa_gz_inflate_file(path.encode(), ingest_threads() if threads is None else int(threads),
+                                    buf.ctypes.data_as(P), int(cap), ctypes.byref(n)))
+    return buf[:n.value].tobytes()
 
 
 def ingest_threads() -> int:

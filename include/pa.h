@@ -366,7 +366,7 @@ pa_status pa_mem_trim(int32_t device, uint64_t *released);
  * rejects (no records, unparsed data, duplicate ids, length mismatch) -- so
  * that the caller parses it with the exact grammar, which reproduces the
  * reference's acceptance and errors.  pa_parse_file reads plain files by mmap
- * and ".gz" files through zlib; PA_EIO if the file cannot be read.
+ * and ".gz" files as pa_gz_inflate_file does; PA_EIO if the file cannot be read.
  * A pa_seqset holds n records: FASTA genomes with whitespace removed and
  * stripped descriptions; FASTQ sequences, qualities and stripped ids. */
 #define PA_FASTA 0
@@ -382,6 +382,15 @@ pa_status pa_seqset_sizes(const pa_seqset *set, uint64_t *n_records, uint64_t *n
 /* seq[n_bases], qual[n_bases] (FASTQ; may be NULL), off[n_records + 1] (CSR), names[name_bytes] (may be NULL) */
 pa_status pa_seqset_export(const pa_seqset *set, uint8_t *seq, uint8_t *qual, uint64_t *off, char *names);
 void pa_seqset_free(pa_seqset *set);
+
+/* The text of a ".gz" file, as gzip.open(path).read() returns it
+ * (src/data_file.py:123-125), inflated on `threads` host threads: BGZF members
+ * in parallel, any other gzip member by chunks whose block boundaries are
+ * found by search (csrc/pa_pgz.cpp); every member's CRC-32 and size checked.
+ * *n = the text's length; PA_EINVAL if it exceeds cap, PA_ENOTCANON for data
+ * gzip.open would not read cleanly (the caller then raises the reference's
+ * error through Python's gzip), PA_EIO if the file cannot be opened. */
+pa_status pa_gz_inflate_file(const char *path, int32_t threads, uint8_t *dst, uint64_t cap, uint64_t *n);
 
 #ifdef __cplusplus
 }
