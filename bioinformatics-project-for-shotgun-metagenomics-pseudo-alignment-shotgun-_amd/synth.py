@@ -192,6 +192,34 @@ def write_bgzf(path: str, data: bytes, level: int = 6, workers: int = 1) -> None
         f.write(bgzf_bytes(b"", level))
 
 
+def write_gzip(path: str, data: bytes, level: int = 6, workers: int = 1, chunk: int = 1 << 20) -> None:
+    """Write ``data`` as ONE gzip member (what `gzip` and pigz write, not BGZF):
+    1 MiB slices deflated on ``workers`` threads, each with the previous 32 KiB
+    as its dictionary and ended by a sync flush (pigz's layout), so the slices
+    join into one deflate stream; CRC-32 and size in the trailer."""
+    import struct
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+    mv = memoryview(data)
+    n = len(data)
+    starts = list(range(0, n, chunk)) or [0]
+
+    def piece(i):
+        s = starts[i]
+        kw = {"zdict": bytes(mv[max(0, s - 32768):s])} if s else {}
+        co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, zlib.Z_DEFAULT_STRATEGY, **kw)
+        last = i == len(starts) - 1
+        return co.compress(mv[s:s + chunk]) + co.flush(zlib.Z_FINISH if last else zlib.Z_SYNC_FLUSH)
+
+    with ThreadPoolExecutor(max_workers=max(1, workers)) as ex:
+        parts = list(ex.map(piece, range(len(starts))))
+    with open(path, "wb") as f:
+        f.write(b"\x1f\x8b\x08\x00\x00\x00\x00\x00\x00\xff")
+        for p in parts:
+            f.write(p)
+        f.write(struct.pack("<II", zlib.crc32(mv) & 0xFFFFFFFF, n & 0xFFFFFFFF))
+
+
 def _bgzf_piece(args) -> bytes:
     data, level = args
     full = bgzf_bytes(data, level)

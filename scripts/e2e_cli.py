@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--dir", default="/tmp/pa_e2e")
     ap.add_argument("--keep", action="store_true", help="leave the generated files in --dir (profiling runs)")
-    ap.add_argument("--no-gz", action="store_true", help="skip the .fq.gz (BGZF) run")
+    ap.add_argument("--no-gz", action="store_true", help="skip the .fq.gz runs (BGZF and one plain member)")
     args = ap.parse_args()
     os.makedirs(args.dir, exist_ok=True)
     fa, fq = os.path.join(args.dir, "c2.fa"), os.path.join(args.dir, "c2.fq")
@@ -157,8 +157,33 @@ def main():
             gz["cli_stderr"] = rz.stderr[-2000:]
         if not args.keep:
             os.remove(fqz)
+    # the same reads as ONE ordinary gzip member (what `gzip` / pigz write, the
+    # reference's gzip.open path, src/data_file.py:123-125): inflated by chunks
+    # on host threads (pa_pgz.cpp), their block boundaries found by search
+    pgz = {}
+    if not args.no_gz:
+        fqz = fq + ".plain.gz"
+        t = time.perf_counter()
+        with open(fq, "rb") as f:
+            synth.write_gzip(fqz, f.read(), level=6, workers=min(16, os.cpu_count() or 1))
+        pgz["write_s"] = time.perf_counter() - t
+        cmdz = cmd[:-1] + [fqz]
+        wz = []
+        for _ in range(3):
+            time.sleep(3)
+            t = time.perf_counter()
+            rz = subprocess.run(cmdz, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+            wz.append(time.perf_counter() - t)
+        pgz.update({"fastq_gz_bytes": os.path.getsize(fqz),
+                    "format": "one gzip member (pigz layout: 1 MiB slices, sync flushes), zlib level 6",
+                    "cli_wall_s": sorted(wz)[1], "cli_wall_runs_s": wz, "cli_reads_per_s": args.reads / sorted(wz)[1],
+                    "cli_rc": rz.returncode, "cli_stdout_equals_api": rz.stdout == summary + "\n"})
+        if rz.returncode:
+            pgz["cli_stderr"] = rz.stderr[-2000:]
+        if not args.keep:
+            os.remove(fqz)
     out = {"workload": f"dumpalign C2: 50 x 2 Mbp FASTA, {args.reads} x 150 bp FASTQ, k=31",
-           "fq_gz": gz,
+           "fq_gz": gz, "fq_plain_gz": pgz,
            "fastq_bytes": os.path.getsize(fq), "cli_wall_s": cli_s, "cli_wall_runs_s": walls, "cli_reads_per_s": args.reads / cli_s,
            "cli_rc": r.returncode, "cli_stdout_equals_api": r.stdout == summary + "\n",
            "device_parse_path_taken": streamed, "host_path_summary_equal": host_equal,
