@@ -140,7 +140,7 @@ def e2e_pass():
         return {"error": f"{type(e).__name__}: {e}"}
     keep = ("workload", "cli_wall_s", "cli_wall_runs_s", "cli_reads_per_s", "cli_stdout_equals_api",
             "device_parse_path_taken", "host_path_summary_equal", "phases", "dumpref_c2_to_devnull", "fq_gz",
-            "fq_plain_gz")
+            "fq_plain_gz", "cli_stages")
     out = {k: d.get(k) for k in keep}
     out["basis"] = ("median wall time of 3 runs of the whole `main.py -t dumpalign -g c2.fa -k 31 --reads c2.fq` "
                     "command (an idle device between runs), files in the page cache; reads/s = 10 M / that")

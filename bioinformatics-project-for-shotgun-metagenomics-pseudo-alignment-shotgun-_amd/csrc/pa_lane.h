@@ -63,11 +63,20 @@ constexpr uint32_t kLaneMaxMis = PA_LANE_MAXMIS;  // mismatching bases against t
 // The seeds of every read found by a pre-pass of their own (k_lane_seeds,
 // below) rather than inside k_align_lane (PA_LANE_PREPASS=0: the round-3 kernel)
 #ifndef PA_LANE_PREPASS
-#define PA_LANE_PREPASS 1
+#define PA_LANE_PREPASS 0  // (A/B r4: C2 3.05 vs 3.77, c2mix 1.70 vs 1.85 G reads/s with it)
 #endif
 constexpr bool kPre = PA_LANE_PREPASS != 0;
+#ifndef PA_EXP_NO_NBBIG
+#define PA_EXP_NO_NBBIG 0  // (register experiments only)
+#endif
+#ifndef PA_EXP_NO_BIG
+#define PA_EXP_NO_BIG 0
+#endif
 // (the pre-pass's defaults: single-slot probe steps and a ranking on the first
 // 96 bases keep it at 96 VGPRs -- 5 waves per SIMD -- without scratch)
+#ifndef PA_LANE_R2_ALL
+#define PA_LANE_R2_ALL 1  // (A/B r4: the middle seed alone when both outer seeds are absent: C2 3.35 vs 3.77, c2mix 1.50 vs 1.84 G reads/s)
+#endif
 #ifndef PA_SEED_SLOTS
 #define PA_SEED_SLOTS (PA_LANE_PREPASS ? 1 : 2)  // table slots per probe step of the seed probes
 #endif
@@ -422,7 +431,11 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             bool spec = false;
 #pragma unroll
             for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && scls[i] < a.G && stp32[i] != NONE;
-            act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
+            // (neither outer seed in the index at all -- a reverse-strand or
+            // unindexed read, or a forward one with errors at both ends: the
+            // middle seed alone, which finds the latter; PA_LANE_R2_ALL=1: all three)
+            const uint32_t r2 = (PA_LANE_R2_ALL || sfound) ? all & ~outer : 1u << (NSEED / 2);
+            act = (round == 0 && act != all && !spec) ? r2 : 0u;
 #ifdef PA_SEED_BLOOM  // (A/B r3: c2rc +0 %, C2 -7 % -- it pushed the kernel's spills from 20 to 44 B/lane)
             // neither outer seed in the index (a reverse-strand read, an
             // unindexed organism -- or sequencing errors at both ends): the
@@ -677,7 +690,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             uint64_t v8;
             __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
             nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
-            if (MG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
+            if (MG && !PA_EXP_NO_NBBIG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
                 const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
                 ng[u] = a.tile_nbbig ? gv : 0u;
             } else {
@@ -763,7 +776,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         } else if (mg == 1) {
             big0 = walked0 & ~spec0;
             big1 = walked1 & ~spec1;
-        } else {  // the plane "set size > mg" of this mg (k_tile_big)
+        } else if (!PA_EXP_NO_BIG) {  // the plane "set size > mg" of this mg (k_tile_big)
             const uint64_t *bp = a.tile_big + (Ac >> 6);
             const uint64_t b0 = bp[0], b1 = bp[1], b2 = bp[2];
             big0 = walked0 & ~spec0 & (fr ? (b0 >> fr) | (b1 << (64 - fr)) : b0);

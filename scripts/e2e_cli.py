@@ -162,7 +162,7 @@ def main():
     # on host threads (pa_pgz.cpp), their block boundaries found by search
     pgz = {}
     if not args.no_gz:
-        fqz = fq + ".plain.gz"
+        fqz = fq[:-3] + "_plain.fq.gz"  # (the CLI takes .fq / .fq.gz names only)
         t = time.perf_counter()
         with open(fq, "rb") as f:
             synth.write_gzip(fqz, f.read(), level=6, workers=min(16, os.cpu_count() or 1))

@@ -8,6 +8,8 @@ reads mid-kernel.  The counters of the in-flight align must equal a
 synchronous align of the same reads.
 """
 
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -17,13 +19,22 @@ import synth
 pytestmark = pytest.mark.gpu
 
 
+def _hip():
+    """The HIP runtime libpa.so runs on (streams for the test; the runtime
+    bundled with torch is a different one and sees no device libpa uses)."""
+    h = ctypes.CDLL("libamdhip64.so.7")
+    h.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    h.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    return h
+
+
 def _stats(res):
     stats, uq, am, fk = res.fetch()
     return stats.tolist(), uq.tolist(), am.tolist(), fk.tolist()
 
 
 def test_free_reads_while_align_in_flight_then_reupload():
-    import torch
+    hip = _hip()
     gens = synth.family_genomes(20, 200_000, seed=1, family_size=5, sub_rate=0.01, conserved_len=2000)
     index = N.Index(gens, 31, device=0)
     n = 2_500_000  # 375 MB of bases: a pooled range
@@ -32,9 +43,11 @@ def test_free_reads_while_align_in_flight_then_reupload():
     a = N.Reads.synthesize(index, n, 150, first_read=0, seed=2, sub_rate=0.005)
     N.align(index, a, prm, 0, want)
     a.close()
-    torch.cuda.synchronize()
+    assert hip.hipDeviceSynchronize() == 0
 
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1, s2 = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(s1)) == 0 and hip.hipStreamCreate(ctypes.byref(s2)) == 0
+    s1, s2 = s1.value, s2.value
     got = N.Result(index)
     a = N.Reads.synthesize(index, n, 150, first_read=0, seed=2, sub_rate=0.005, stream=s1)
     for _ in range(3):  # several passes queued, so the kernels are still running at the free
@@ -43,7 +56,7 @@ def test_free_reads_while_align_in_flight_then_reupload():
     a.close()  # its range goes back to the pool only once the queued passes are done
     b = N.Reads.synthesize(index, n, 150, first_read=n, seed=7, sub_rate=0.02, stream=s2,
                            rc_rate=0.5, foreign_rate=0.3)
-    torch.cuda.synchronize()
+    assert hip.hipDeviceSynchronize() == 0
     assert _stats(got) == _stats(want)
     # the new batch is intact too: its align equals the same reads made alone
     r1 = N.Result(index)
@@ -52,10 +65,12 @@ def test_free_reads_while_align_in_flight_then_reupload():
     c = N.Reads.synthesize(index, n, 150, first_read=n, seed=7, sub_rate=0.02, rc_rate=0.5, foreign_rate=0.3)
     r2 = N.Result(index)
     N.align(index, c, prm, n, r2)
-    torch.cuda.synchronize()
+    assert hip.hipDeviceSynchronize() == 0
     assert _stats(r1) == _stats(r2)
     for h in (c, got, want, r1, r2, index):
         h.close()
+    hip.hipStreamDestroy(s1)
+    hip.hipStreamDestroy(s2)
 
 
 def test_small_allocation_trims_idle_slabs():
