@@ -167,7 +167,7 @@ REQ_COUNTERS = {"TCC_EA0_RDREQ_32B_sum": 32, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_E
 # the SQ counters of the same pass (8 SQ counters and 4 TCC fit one rocprofv3
 # pass; these count quad-cycles, so only their ratios are used)
 SQ_COUNTERS = ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")
-ALIGN_KERNELS = ("k_quality_masks", "k_lane_seeds", "k_align_lane", "k_align_lane_na", "k_align_lane_rc", "k_rc_seeds",
+ALIGN_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_lane_rc", "k_rc_seeds",
                  "k_align_fast", "k_align_exact")
 
 

@@ -53,8 +53,6 @@ constexpr uint32_t kLdsGenomeCap = 2048;  // per-workgroup LDS counters up to th
 
 enum : uint32_t { F_MRQ = 1, F_MKQ = 2, F_MG = 4 };
 
-struct LaneRec;  // (pa_lane.h) a walkable read as the seed pre-pass leaves it
-
 struct AlignArgs {
     const void *table;
     uint64_t cap;
@@ -113,8 +111,6 @@ struct AlignArgs {
     uint32_t *queue_na2;                   // k_rc_seeds / k_align_lane_rc: the reads to test window by window
     unsigned long long *queue_na2_count;   //   (k_align_lane_na)
     uint64_t na_min;                       // fewer than this: k_align_lane_na hands them to the wave kernel
-    LaneRec *walk_rec;                     // k_lane_seeds -> k_align_lane: the walkable reads, compacted
-    unsigned long long *walk_count;        //   and their number
     const uint4 *qmask;                    // (quality filters) per read: windows failing --min-kmer-quality
     const uint8_t *qdrop;                  //   and 1 if the read fails --min-read-quality (k_quality_masks)
     // wave kernel input: a list of read indices (null: reads 0 .. n-1)
@@ -737,17 +733,6 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
     const uint64_t want = (a.n + kBlock - 1) / kBlock;
     const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)cus;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
-    if (kPre) {  // the seed pre-pass: every read packed and seeded, walkable ones compacted (a.walk_rec)
-        auto seeds = need_q ? k_lane_seeds<true> : k_lane_seeds<false>;
-        int s_cu = 0;
-        PA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&s_cu, seeds, kBlock, 0));
-        const unsigned sgrid = (unsigned)std::max<uint64_t>(
-            1, std::min<uint64_t>(want, (uint64_t)std::max(1, s_cu) * (uint64_t)cus));
-        PA_HIP(hipMemsetAsync(a.walk_count, 0, 8, st));
-        KernelTimer kt(prof, st, PA_PROF_SEEDS);
-        hipLaunchKernelGGL(seeds, dim3(sgrid), dim3(kBlock), 0, st, a);
-        PA_HIP(hipGetLastError());
-    }
     {
         KernelTimer kt(prof, st, PA_PROF_LANE);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), shm, st, a);
@@ -935,10 +920,8 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
     pa::dev_free(idx->queue_na_keys);
     pa::dev_free(idx->queue_rc);
     pa::dev_free(idx->queue_rc_anc);
-    pa::dev_free(idx->walk_rec);
     idx->queue = idx->queue_hard = idx->queue_na = idx->queue_na2 = idx->queue_rc = nullptr;
     idx->queue_na_keys = idx->queue_rc_anc = nullptr;
-    idx->walk_rec = nullptr;
     idx->queue_cap = 0;
     PA_HIP(pa::dev_malloc(&idx->queue, n * 4));
     PA_HIP(pa::dev_malloc(&idx->queue_hard, n * 4));
@@ -947,10 +930,8 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
     PA_HIP(pa::dev_malloc(&idx->queue_na_keys, n * 16));
     PA_HIP(pa::dev_malloc(&idx->queue_rc, n * 4));
     PA_HIP(pa::dev_malloc(&idx->queue_rc_anc, n * 8));
-    if (kPre) PA_HIP(pa::dev_malloc(&idx->walk_rec, n * 64));  // (LaneRec)
-    // [0] the lane kernel's reads without a seed, [1] k_rc_seeds' walkable ones, [2] the rest (k_align_lane_na),
-    // [3] the walkable reads of the seed pre-pass
-    if (!idx->na_count) PA_HIP(pa::dev_malloc(&idx->na_count, 32));
+    // [0] the lane kernel's reads without a seed, [1] k_rc_seeds' walkable ones, [2] the rest (k_align_lane_na)
+    if (!idx->na_count) PA_HIP(pa::dev_malloc(&idx->na_count, 24));
     idx->queue_cap = n;
     return PA_OK;
 }
@@ -1123,8 +1104,6 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.queue_rc_count = idx->na_count + 1;
             a.queue_na2 = idx->queue_na2;
             a.queue_na2_count = idx->na_count + 2;
-            a.walk_rec = (LaneRec *)idx->walk_rec;
-            a.walk_count = idx->na_count + 3;
             a.na_min = 32768;  // (PA_NA_MIN: tests)
             if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
             if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 24, st));

@@ -1352,8 +1352,6 @@ void index_release(pa_index *idx) {
     pa::dev_free(idx->queue_na_keys);
     pa::dev_free(idx->queue_rc);
     pa::dev_free(idx->queue_rc_anc);
-    pa::dev_free(idx->walk_rec);
-    idx->walk_rec = nullptr;
     idx->queue_na2 = nullptr;
     idx->queue_na_keys = nullptr;
     idx->queue_rc = nullptr;

@@ -128,7 +128,6 @@ struct pa_index {
     uint64_t *queue_na_keys = nullptr; // [2 per queue_na entry] their outer seeds' reverse complements (k_rc_seeds)
     uint32_t *queue_rc = nullptr;      // reads with a reverse-complement seed (k_align_lane_rc)
     uint64_t *queue_rc_anc = nullptr;  //   its first occurrence | seed << 63
-    void *walk_rec = nullptr;          // [queue_cap] 64-B records of the walkable reads (k_lane_seeds -> k_align_lane)
     uint4 *qmask = nullptr;            // per read: windows failing --min-kmer-quality (k_quality_masks)
     uint8_t *qdrop = nullptr;          // per read: fails --min-read-quality
     uint64_t qmask_cap = 0;

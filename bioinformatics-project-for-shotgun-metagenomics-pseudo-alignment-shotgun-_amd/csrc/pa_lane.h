@@ -60,28 +60,14 @@ constexpr uint32_t kLaneMaxMis = PA_LANE_MAXMIS;  // mismatching bases against t
 #ifndef PA_LANE_SEEDS
 #define PA_LANE_SEEDS 5   // seed windows probed per read (first ... last, evenly spread)
 #endif
-// The seeds of every read found by a pre-pass of their own (k_lane_seeds,
-// below) rather than inside k_align_lane (PA_LANE_PREPASS=0: the round-3 kernel)
-#ifndef PA_LANE_PREPASS
-#define PA_LANE_PREPASS 0  // (A/B r4: C2 3.05 vs 3.77, c2mix 1.70 vs 1.85 G reads/s with it)
-#endif
-constexpr bool kPre = PA_LANE_PREPASS != 0;
-#ifndef PA_EXP_NO_NBBIG
-#define PA_EXP_NO_NBBIG 0  // (register experiments only)
-#endif
-#ifndef PA_EXP_NO_BIG
-#define PA_EXP_NO_BIG 0
-#endif
-// (the pre-pass's defaults: single-slot probe steps and a ranking on the first
-// 96 bases keep it at 96 VGPRs -- 5 waves per SIMD -- without scratch)
 #ifndef PA_LANE_R2_ALL
 #define PA_LANE_R2_ALL 1  // (A/B r4: the middle seed alone when both outer seeds are absent: C2 3.35 vs 3.77, c2mix 1.50 vs 1.84 G reads/s)
 #endif
 #ifndef PA_SEED_SLOTS
-#define PA_SEED_SLOTS (PA_LANE_PREPASS ? 1 : 2)  // table slots per probe step of the seed probes
+#define PA_SEED_SLOTS 2  // table slots per probe step of the seed probes
 #endif
 #ifndef PA_LANE_RANK_WORDS
-#define PA_LANE_RANK_WORDS (PA_LANE_PREPASS ? 3 : 6)  // 2-bit words of the read its candidate stretches are ranked on (6: all)
+#define PA_LANE_RANK_WORDS 6  // 2-bit words of the read its candidate stretches are ranked on (6: all)
 #endif
 #ifndef PA_LANE_SLOTS
 #define PA_LANE_SLOTS 1   // table slots per probe step in the cooperative passes
@@ -214,19 +200,6 @@ struct LaneRead {
     uint32_t qf;                       // their number (src/kmer.py:420-423)
     uint32_t uoff;                     // walk windows whose k-mer is off the walk, present and multi-genome (neighbour bits)
 };
-
-// A read the lane kernel walks, as the seed pre-pass (k_lane_seeds) leaves it:
-// its anchor and the packed read, 64 B, in the order the pre-pass compacted
-// them (the lane kernel's waves then hold walkable reads only, and its lanes
-// load their records as one contiguous 4 KB per wave).
-struct __align__(16) LaneRec {
-    uint64_t anc;              // (window << 40) | first occurrence, | len << 48
-    uint32_t acls;             // the anchor k-mer's class
-    uint32_t r;                // the read (batch index)
-    uint64_t row[kLaneWords];  // the read, 2-bit packed (LaneWave::R)
-};
-static_assert(sizeof(LaneRec) == 64, "one 64-B record per walked read");
-constexpr uint64_t kAncMask = (1ull << 48) - 1;  // LaneRec::anc without the length
 
 // 64 bits of an LDS row of MSB-first packed words starting at bit o.
 __device__ __forceinline__ uint64_t row_bits(const uint64_t *row, uint32_t o) {
@@ -545,45 +518,6 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     S.kind = LANE_WALK;
 }
 
-// Phase 1 from the pre-pass: record i of the walkable reads (k_lane_seeds)
-// into the lane's LDS row and the lane state (a read walked again: the given
-// anchor, cd != ~0).  Returns the read's batch index.
-template <bool WIN_Q>
-__device__ __forceinline__ uint32_t lane_load(const AlignArgs &a, uint32_t i, unsigned long long cd, uint64_t *row,
-                                              LaneRead &S) {
-    const uint4 *rp = (const uint4 *)(a.walk_rec + i);
-    const uint4 h = rp[0], v0 = rp[1], v1 = rp[2], v2 = rp[3];  // (one contiguous 64 B per lane)
-    const uint64_t anc = (uint64_t)h.x | ((uint64_t)h.y << 32);
-    const uint32_t r = h.w;
-    row[0] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
-    row[1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
-    row[2] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
-    row[3] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
-    row[4] = (uint64_t)v2.x | ((uint64_t)v2.y << 32);
-    row[5] = (uint64_t)v2.z | ((uint64_t)v2.w << 32);
-    S.kind = LANE_WALK;
-    S.hr = S.nspec = S.nincl = 0;
-    S.F0 = S.F1 = 0;
-    S.qf = 0;
-    S.uoff = 0;
-    S.len = (uint32_t)(anc >> 48);
-    S.W = S.len - (uint32_t)a.k + 1;
-    if (WIN_Q) {  // the windows failing --min-kmer-quality (k_quality_masks)
-        const uint4 m = a.qmask[r];
-        S.F0 = (uint64_t)m.x | ((uint64_t)m.y << 32);
-        S.F1 = (uint64_t)m.z | ((uint64_t)m.w << 32);
-        S.qf = (uint32_t)(__popcll(S.F0) + __popcll(S.F1));
-    }
-    if (cd != ~0ull) {
-        S.anc = cd;
-        S.acls = NONE;  // genome from the position
-    } else {
-        S.anc = anc & kAncMask;
-        S.acls = h.z;
-    }
-    return r;
-}
-
 // Phase 2: walk from the anchor; walked windows resolve from the tile, the
 // others are left in P0 / P1 for the cooperative probes.
 template <bool WIN_Q, bool MG>
@@ -690,7 +624,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
             uint64_t v8;
             __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
             nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
-            if (MG && !PA_EXP_NO_NBBIG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
+            if (MG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
                 const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
                 ng[u] = a.tile_nbbig ? gv : 0u;
             } else {
@@ -776,7 +710,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
         } else if (mg == 1) {
             big0 = walked0 & ~spec0;
             big1 = walked1 & ~spec1;
-        } else if (!PA_EXP_NO_BIG) {  // the plane "set size > mg" of this mg (k_tile_big)
+        } else {  // the plane "set size > mg" of this mg (k_tile_big)
             const uint64_t *bp = a.tile_big + (Ac >> 6);
             const uint64_t b0 = bp[0], b1 = bp[1], b2 = bp[2];
             big0 = walked0 & ~spec0 & (fr ? (b0 >> fr) | (b1 << (64 - fr)) : b0);
@@ -943,26 +877,23 @@ void k_align_lane(AlignArgs a) {
     // specific k-mer off it is walked again from that k-mer, but later, with 63
     // others (a list per wave), so that the 3 % of such reads do not hold whole
     // waves for a second walk.  Every decision below is wave-uniform.
-    // with the seed pre-pass (kPre) the waves take its records of walkable
-    // reads (k_lane_seeds); else the batch's reads, packed and seeded here
-    const uint64_t nrec = kPre ? *a.walk_count : a.n;
-    const uint64_t n_chunks = (nrec + 63) / 64, wave_stride = (uint64_t)gridDim.x * kWaves;
+    const uint64_t n_chunks = (a.n + 63) / 64, wave_stride = (uint64_t)gridDim.x * kWaves;
     uint64_t chunk = (uint64_t)blockIdx.x * kWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t n_again = 0;  // entries in LW.again_r / again_a
     while (true) {
-        uint32_t i = ~0u;  // the record (kPre) or read (a batch holds < 2^32 reads: pa::align)
+        uint32_t r = ~0u;  // (a batch holds < 2^32 reads: pa::align)
         unsigned long long cd = ~0ull;
         bool again_batch = false;
         if (n_again >= 64 || (chunk >= n_chunks && n_again > 0)) {
             const uint32_t take = n_again < 64 ? n_again : 64;
             if ((uint32_t)lane < take) {
-                i = LW.again_r[n_again - take + lane];
+                r = LW.again_r[n_again - take + lane];
                 cd = LW.again_a[n_again - take + lane];
             }
             n_again -= take;
             again_batch = true;
         } else if (chunk < n_chunks) {
-            i = chunk * 64 + lane < nrec ? (uint32_t)(chunk * 64 + lane) : ~0u;
+            r = chunk * 64 + lane < a.n ? (uint32_t)(chunk * 64 + lane) : ~0u;
             chunk += wave_stride;
         } else {
             break;
@@ -970,13 +901,7 @@ void k_align_lane(AlignArgs a) {
         LaneRead S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows (and the taken list entries) are done with
-        uint32_t r = i;
-        if (i != ~0u) {
-            if (kPre)
-                r = lane_load<WIN_Q>(a, i, cd, LW.R[lane], S);
-            else
-                lane_prep<NEED_Q, WIN_Q>(a, i, cd, LW.R[lane], S);
-        }
+        if (r != ~0u) lane_prep<NEED_Q, WIN_Q>(a, r, cd, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
@@ -1071,7 +996,7 @@ void k_align_lane(AlignArgs a) {
             qbase = shfl64(qbase, __builtin_ctzll(hb));
             if (hard) a.queue_hard[qbase + lanes_below(hb)] = r;
         }
-        const bool na = !kPre && S.kind == LANE_NOANCHOR;  // (kPre: the pre-pass queued them)
+        const bool na = S.kind == LANE_NOANCHOR;
         const uint64_t nab = __ballot(na);
         if (nab) {  // one queue allocation per wave
             uint64_t qbase = 0;
@@ -1089,7 +1014,7 @@ void k_align_lane(AlignArgs a) {
         const uint64_t ab = __ballot(again);
         if (ab) {  // (at most 63 + 64 entries: a batch is taken once 64 wait)
             if (again) {
-                LW.again_r[n_again + lanes_below(ab)] = i;
+                LW.again_r[n_again + lanes_below(ab)] = r;
                 LW.again_a[n_again + lanes_below(ab)] = LW.cand[lane];
             }
             n_again += (uint32_t)__popcll(ab);
@@ -1126,91 +1051,6 @@ void k_align_lane(AlignArgs a) {
             if (uniq[i]) atomicAdd(&a.uniq[i], (unsigned long long)uniq[i]);
             if (first[i] != (unsigned long long)PA_NO_FIRST_KEY) atomicMin(&a.first[i], first[i]);
         }
-    }
-}
-
-// k_lane_seeds: phase 1 of the lane path for every read of the batch, one read
-// per thread -- qualities (the read's mean test from k_quality_masks), the
-// 2-bit packing and the seed probes with the choice of anchor (lane_prep) --
-// in a kernel of its own: a pass of few live registers and no wave-wide
-// bookkeeping keeps more waves resident than k_align_lane (5 per SIMD against
-// 4), and the seeds' random table lines are most of what it waits for, so they
-// overlap better here than between the lane kernel's walks.  Outcomes:
-//   * walkable (an anchor): a LaneRec, compacted -- the lane kernel's waves
-//     then hold walkable reads only (on c2mix 40 % of the reads have no seed);
-//   * no seed in the index: queue_na with its reverse-complement seed keys
-//     (k_rc_seeds), as k_align_lane queued them;
-//   * anything the lane path does not take (long, non-ACGT): queue_hard;
-//   * dropped by --min-read-quality, no windows: counted here.
-// Queue slots are taken per block (one global atomic per queue and block
-// round of 256 reads: per-wave atomics on one counter serialise, see k_rc_seeds).
-#ifndef PA_SEED_WAVES
-#define PA_SEED_WAVES 5
-#endif
-template <bool NEED_Q>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_SEED_WAVES)))
-void k_lane_seeds(AlignArgs a) {
-    __shared__ uint64_t rows[kBlock][kLaneWords + 1];
-    __shared__ uint32_t qn[2][kWaves];           // walkable / seedless reads per wave of this round
-    __shared__ unsigned long long qb[2];         // the round's first slot in walk_rec / queue_na
-    rows[threadIdx.x][kLaneWords] = 0;  // the zero word past every read (lane_prep writes words 0 .. kLaneWords - 1)
-    const int lane = lane_id();
-    const uint32_t wv = threadIdx.x >> 6;
-    uint32_t n_unm = 0, n_drop = 0;  // wave totals (scalar)
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock; c0 < a.n; c0 += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t r = c0 + threadIdx.x;
-        LaneRead S;
-        S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
-        if (r < a.n) lane_prep<NEED_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
-        const bool hard = S.kind == LANE_HARD;  // (rare: per-wave slots)
-        const uint64_t hb = __ballot(hard);
-        if (hb) {
-            uint64_t qbase = 0;
-            if (lane == __builtin_ctzll(hb)) qbase = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
-            qbase = shfl64(qbase, __builtin_ctzll(hb));
-            if (hard) a.queue_hard[qbase + lanes_below(hb)] = (uint32_t)r;
-        }
-        n_unm += (uint32_t)__popcll(__ballot(S.kind == LANE_UNMAPPED));
-        n_drop += (uint32_t)__popcll(__ballot(S.kind == LANE_DROP));
-        const bool walk = S.kind == LANE_WALK, na = S.kind == LANE_NOANCHOR;
-        const uint64_t wb = __ballot(walk), nb = __ballot(na);
-        if (lane == 0) {
-            qn[0][wv] = (uint32_t)__popcll(wb);
-            qn[1][wv] = (uint32_t)__popcll(nb);
-        }
-        __syncthreads();
-        if (threadIdx.x < 2) {
-            uint32_t t = 0;
-#pragma unroll
-            for (int w = 0; w < kWaves; w++) t += qn[threadIdx.x][w];
-            qb[threadIdx.x] = t ? atomicAdd(threadIdx.x == 0 ? a.walk_count : a.queue_na_count, (unsigned long long)t)
-                                : 0ull;
-        }
-        __syncthreads();
-        uint32_t before = 0;  // this wave's offset in the round
-#pragma unroll
-        for (int w = 0; w < kWaves; w++) before += (uint32_t)w < wv ? qn[walk ? 0 : 1][w] : 0u;
-        if (walk) {
-            const uint64_t q = qb[0] + before + lanes_below(wb);
-            const uint64_t *row = rows[threadIdx.x];
-            uint4 *dst = (uint4 *)(a.walk_rec + q);
-            dst[0] = make_uint4((uint32_t)S.anc, (uint32_t)(S.anc >> 32) | (S.len << 16), S.acls, (uint32_t)r);
-            dst[1] = make_uint4((uint32_t)row[0], (uint32_t)(row[0] >> 32), (uint32_t)row[1], (uint32_t)(row[1] >> 32));
-            dst[2] = make_uint4((uint32_t)row[2], (uint32_t)(row[2] >> 32), (uint32_t)row[3], (uint32_t)(row[3] >> 32));
-            dst[3] = make_uint4((uint32_t)row[4], (uint32_t)(row[4] >> 32), (uint32_t)row[5], (uint32_t)(row[5] >> 32));
-        } else if (na) {
-            const uint64_t q = qb[1] + before + lanes_below(nb);
-            a.queue_na[q] = (uint32_t)r;
-            if (a.queue_na_keys) {
-                a.queue_na_keys[2 * q] = S.P0;
-                a.queue_na_keys[2 * q + 1] = S.P1;
-            }
-        }
-        __syncthreads();  // (qn / qb are rewritten by the next round)
-    }
-    if (lane == 0) {
-        if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
-        if (n_drop) atomicAdd(&a.stats[3], (unsigned long long)n_drop);
     }
 }
 

@@ -471,7 +471,7 @@ class Index:
         _check(lib().pa_profile_enable(self._h, 1 if on else 0))
 
     PROF_KERNELS = ("k_quality_masks", "k_align_lane", "k_align_lane_na", "k_align_fast", "k_align_exact",
-                    "k_align_lane_rc", "k_rc_seeds", "k_lane_seeds")
+                    "k_align_lane_rc", "k_rc_seeds")
 
     def profile_read_kernels(self) -> dict:
         """{kernel: (summed ms, launches)} of the align passes since the last

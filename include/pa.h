@@ -341,8 +341,7 @@ pa_status pa_profile_read(pa_index *idx, double *main_ms, uint64_t *launches, ui
 #define PA_PROF_EXACT 4     /* k_align_exact */
 #define PA_PROF_LANE_RC 5   /* k_align_lane_rc */
 #define PA_PROF_RC_SEEDS 6  /* k_rc_seeds */
-#define PA_PROF_SEEDS 7     /* k_lane_seeds (the lane path's seed pre-pass) */
-#define PA_PROF_KERNELS 8
+#define PA_PROF_KERNELS 7
 pa_status pa_profile_read_kernels(pa_index *idx, double *ms, uint64_t *launches);
 
 /* ---- device memory -------------------------------------------------------------- */
