@@ -233,7 +233,13 @@ __device__ __forceinline__ void quality_reads(const uint8_t *__restrict__ qual, 
         const uint64_t o = off[r], L64 = off[r + 1] - o;
         uint4 m = make_uint4(0, 0, 0, 0);
         uint8_t d = 0;
-        if (L64 <= 4u * kQmDwords) quality_read<KQ>(qual, o, (uint32_t)L64, k, T, mrq, flags, m, d);
+        if (L64 <= 4u * kQmDwords) {
+            quality_read<KQ>(qual, o, (uint32_t)L64, k, T, mrq, flags, m, d);
+        } else if (flags & 1u) {  // a longer read (the 250-bp lane shape): its mean test only
+            uint64_t tot = 0;
+            for (uint64_t i = 0; i < L64; i++) tot += qual[o + i];
+            d = (int64_t)tot < mrq * (int64_t)L64 ? 1 : 0;
+        }
         qmask[r] = m;
         qdrop[r] = d;
     }
@@ -717,12 +723,19 @@ struct KernelTimer {
     }
 };
 
-pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr) {
+// long_reads: the batch holds reads longer than the 150-bp shape takes (176
+// bases): the 250-bp shape (NM = 4, <= 272 bases, <= 256 windows) walks them,
+// unless --min-kmer-quality is set (its window masks cover 128 windows: such
+// reads then go to the wave kernel).
+pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr, bool long_reads = false) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
-    const size_t shm = lane_lds_bytes(a.G);
     const bool win_q = (a.prm.flags & F_MKQ) != 0;
     const bool mg = (a.prm.flags & F_MG) != 0;
-    auto kern = win_q ? (mg ? k_align_lane<true, true, true> : k_align_lane<true, true, false>)
+    const bool nm4 = long_reads && !win_q;
+    const size_t shm = lane_lds_bytes(a.G, nm4 ? 4 : 2);
+    auto kern = nm4 ? (need_q ? (mg ? k_align_lane<true, false, true, 4> : k_align_lane<true, false, false, 4>)
+                              : (mg ? k_align_lane<false, false, true, 4> : k_align_lane<false, false, false, 4>))
+              : win_q ? (mg ? k_align_lane<true, true, true> : k_align_lane<true, true, false>)
               : need_q ? (mg ? k_align_lane<true, false, true> : k_align_lane<true, false, false>)
                        : (mg ? k_align_lane<false, false, true> : k_align_lane<false, false, false>);
     if (shm > 64 * 1024) PA_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
@@ -1036,7 +1049,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
         }
         if (lane_ok) {
             if ((a.prm.flags & F_MG) && a.prm.mg >= 2) {
-                const uint64_t n_words = a.tile_n / 64 + 4;
+                const uint64_t n_words = a.tile_n / 64 + 8;  // (padded: the 250-bp walk reads five words from any position)
                 if (!idx->tile_big) PA_HIP(pa::dev_malloc(&idx->tile_big, n_words * 8));
                 if (idx->tile_big_mg != a.prm.mg) {
                     hipLaunchKernelGGL(k_tile_big, dim3((unsigned)std::min<uint64_t>((n_words + 3) / 4, 1u << 20)),
@@ -1107,7 +1120,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.na_min = 32768;  // (PA_NA_MIN: tests)
             if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
             if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 24, st));
-            PA_TRY(launch_lane(a, st, idx));
+            PA_TRY(launch_lane(a, st, idx, r->max_len > (uint32_t)kLaneMaxLen));
             a.rlist = idx->queue_hard;
             a.rlist_count = a.queue_hard_count;
         }

@@ -19,7 +19,7 @@ namespace pad {
 constexpr uint64_t EMPTY = ~0ull;        // empty slot (top key word)
 constexpr uint64_t BUSY = ~0ull - 1;     // slot being written (multi-word inserts)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr uint32_t PA_TILE_REP = 0x80000000u;  // tile_cls flag: the k-mer repeats within the next 127 positions
+constexpr uint32_t PA_TILE_REP = 0x80000000u;  // tile_cls flag: the k-mer repeats within the next 255 positions
 // compact tile (uint16 per position) of the lane kernel
 
 template <int NW>

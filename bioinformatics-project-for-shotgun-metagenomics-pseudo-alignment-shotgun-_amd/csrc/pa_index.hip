@@ -589,7 +589,7 @@ __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, u
 // twice only if one of its walked windows carries the flag (its windows are
 // < kTileRepDist apart), which the lane kernel (pa_lane.h) tests instead of
 // deduplicating.  One block per 256 positions, keys staged in LDS.
-constexpr int kTileRepDist = 127;
+constexpr int kTileRepDist = 255;  // (>= the lane kernels' longest span of windows: 256 windows, pa_lane.h)
 __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ pk, uint32_t *tile_cls, uint64_t n,
                                                   int k) {
     __shared__ uint64_t keys[256 + kTileRepDist];
@@ -766,7 +766,7 @@ __global__ void k_mm_build(const Slot<1> *__restrict__ table, uint64_t cap, uint
 // positions j: {2-bit words 2j and 2j+1 of tile_pk (positions 64 j .. 64 j +
 // 63), flag plane A, flag plane B}, bit i of a plane <-> position 64 j + i:
 // (A,B) = (0,0) no indexed window, (1,0) a multi-genome k-mer, (1,1) a
-// specific one, (0,1) a k-mer that repeats within 127 positions (PA_TILE_REP).
+// specific one, (0,1) a k-mer that repeats within 255 positions (PA_TILE_REP).
 // A read's walk needs the bases of [A, A + 150) and the flags of its 120
 // windows: 3 or 4 consecutive blocks, 96-128 B -- on gfx950, where every miss
 // is a 128-B request, 1.6 lines on average, against 2.6 for the separate
@@ -1191,7 +1191,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
                                st, idx->tile_pk, idx->tile_cls, n, k);
         if (k <= 31) {
-            const uint64_t n_blocks = n / 64 + 5;  // padded: the walk reads four blocks from any position
+            const uint64_t n_blocks = n / 64 + 8;  // padded: the 250-bp walk reads six blocks from any position
             B_HIP(pa::dev_malloc(&idx->tile_lw, n_blocks * 32));
             hipLaunchKernelGGL(k_tile_walk, dim3((unsigned)std::min<uint64_t>((n_blocks + 3) / 4, 1u << 20)), dim3(256),
                                0, st, idx->tile_cls, idx->tile_pk, n, G, idx->tile_lw, n_blocks);

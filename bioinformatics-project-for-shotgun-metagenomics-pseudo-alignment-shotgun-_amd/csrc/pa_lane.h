@@ -45,11 +45,21 @@
 // balanced) -- nothing found: UNMAPPED; only multi-genome k-mers: AMBIGUOUS; a
 // specific one: the wave kernel.
 
-constexpr int kLaneMaxW = 128;    // windows per read on the lane path
 constexpr uint64_t kPosMask = (1ull << 40) - 1;  // concatenated positions (< 2^40 bases) in packed anchors
-constexpr int kLaneMaxLen = 176;  // bases per read on the lane path
-constexpr int kLaneChunks = 12;   // 16-B chunks covering shift + kLaneMaxLen bases
-constexpr int kLaneWords = 6;     // 64-bit words of the packed read (32 bases each)
+// Lane-path read shapes, by NM = 64-bit words of a read's window masks:
+//   NM = 2: up to 128 windows and 176 bases (the 150-bp reads of the benchmark);
+//   NM = 4: up to 256 windows and 272 bases (250-bp reads), a kernel variant of
+//           its own (more registers: 3 waves per SIMD)
+template <int NM>
+struct LaneShape {
+    static constexpr int MAXW = 64 * NM;             // windows
+    static constexpr int NWD = NM == 2 ? 6 : 9;      // 64-bit words of the packed read (32 bases each)
+    static constexpr int MAXLEN = 32 * NWD - 16;     // bases (the 16-B staging shift stays inside NWD words)
+    static constexpr int NB = NM + 1;                // flag-plane words of the walk blocks a read spans
+};
+constexpr int kLaneMaxW = LaneShape<2>::MAXW;      // (the 150-bp shape: k_align_lane_na / _rc)
+constexpr int kLaneMaxLen = LaneShape<2>::MAXLEN;
+constexpr int kLaneWords = LaneShape<2>::NWD;
 #ifndef PA_LANE_MAXMIS
 #define PA_LANE_MAXMIS 40
 #endif
@@ -82,8 +92,9 @@ constexpr int kPassEntries = 64 * PA_LANE_PROBES;
 constexpr uint32_t kLaneLdsGenomeCap = PA_LANE_LDS_GENOMES;
 
 // Per-wave LDS of the lane kernel.
+template <int NM>
 struct __align__(16) LaneWave {
-    uint64_t R[64][kLaneWords + 1];  // every lane's packed read (+ a zero word), for keys of listed windows
+    uint64_t R[64][LaneShape<NM>::NWD + 1];  // every lane's packed read (+ a zero word), for keys of listed windows
     unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 40) | position
     uint32_t flags[64];              // bit 0: specific k-mer found off the walk; bits 2..: unspecific ones found
     uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
@@ -188,6 +199,7 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
 // itself lives in the lane's LDS row (LW.R[lane]): every lane of the wave needs
 // it for the keys of listed windows, and rolled loops over LDS words keep the
 // register footprint (and so the occupancy) of this latency-bound kernel low.
+template <int NM>
 struct LaneRead {
     int kind;                          // LANE_* (LANE_WALK: still resolving)
     uint32_t len, W;
@@ -195,8 +207,8 @@ struct LaneRead {
                                        // position < 2^40, as the again lists hold it: one register pair)
     uint32_t acls;                     //   its class
     uint32_t g, nspec, nincl, hr;      // walk results (anchor genome, counts)
-    uint64_t P0, P1;                   // unwalked windows 0-63, 64-127
-    uint64_t F0, F1;                   // windows failing --min-kmer-quality (never looked up)
+    uint64_t P[NM];                    // unwalked windows (bit w of word w / 64)
+    uint64_t F[NM];                    // windows failing --min-kmer-quality (never looked up)
     uint32_t qf;                       // their number (src/kmer.py:420-423)
     uint32_t uoff;                     // walk windows whose k-mer is off the walk, present and multi-genome (neighbour bits)
 };
@@ -220,9 +232,9 @@ __device__ __forceinline__ uint32_t in_read_mask(uint32_t p0, uint32_t shift, ui
 // with PLANES, the flag planes of blocks A >> 6 .. +2.  Three 32-B blocks, a
 // fourth only when the read reaches into it (every load issued before any is
 // used): 1.6 128-B lines per read on average.
-template <bool PLANES, int NWD = kLaneWords>
+template <bool PLANES, int NWD = kLaneWords, int NB = 3>
 __device__ __forceinline__ void lane_blocks(const AlignArgs &a, uint64_t A, uint32_t len, uint64_t (&gw)[NWD + 1],
-                                            uint64_t (&pa3)[3], uint64_t (&pb3)[3]) {
+                                            uint64_t (&pa3)[NB], uint64_t (&pb3)[NB]) {
     const uint64_t *lb = a.tile_lw + 4 * (A >> 6);
     const uint32_t r0 = (uint32_t)(A & 63), o = r0 >> 5, last = r0 + len - 1;
 #pragma unroll
@@ -232,7 +244,7 @@ __device__ __forceinline__ void lane_blocks(const AlignArgs &a, uint64_t A, uint
     }
     if (PLANES) {
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
+        for (int i = 0; i < NB; i++) {
             const ulonglong2 p = *(const ulonglong2 *)(lb + 4 * i + 2);
             pa3[i] = p.x;
             pb3[i] = p.y;
@@ -268,12 +280,16 @@ __device__ __forceinline__ bool lane_fits(const AlignArgs &a, uint32_t len, int6
 
 // Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor (a
 // read walked again: the given anchor, cd != ~0).
-template <bool NEED_Q, bool WIN_Q, bool SEEDS = true>
+template <int NM, bool NEED_Q, bool WIN_Q, bool SEEDS = true>
 __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsigned long long cd, uint64_t *row,
-                                          LaneRead &S) {
+                                          LaneRead<NM> &S) {
+    using SH = LaneShape<NM>;
+    static_assert(NM == 2 || !WIN_Q, "the window-quality masks cover 128 windows");
+    constexpr int NWD = SH::NWD;
     S.kind = LANE_HARD;
     S.hr = S.nspec = S.nincl = 0;
-    S.F0 = S.F1 = 0;
+#pragma unroll
+    for (int i = 0; i < NM; i++) S.F[i] = 0;
     S.qf = 0;
     S.uoff = 0;
     const int k = a.k;
@@ -283,7 +299,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     const uint64_t o0 = o & ~15ull;
     const uint32_t shift = (uint32_t)(o & 15);
     S.len = len;
-    if (len > (uint32_t)kLaneMaxLen) return (void)LANE_HARD_WHY(0);
+    if (len > (uint32_t)SH::MAXLEN) return (void)LANE_HARD_WHY(0);
     // ---- qualities: the read's mean test (src/kmer.py:399, 587) and the windows
     // failing --min-kmer-quality (src/kmer.py:404-408, 420-423), made for every
     // read up front by k_quality_masks
@@ -294,9 +310,9 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         }
         if (WIN_Q) {
             const uint4 m = a.qmask[r];
-            S.F0 = (uint64_t)m.x | ((uint64_t)m.y << 32);
-            S.F1 = (uint64_t)m.z | ((uint64_t)m.w << 32);
-            S.qf = (uint32_t)(__popcll(S.F0) + __popcll(S.F1));
+            S.F[0] = (uint64_t)m.x | ((uint64_t)m.y << 32);
+            S.F[NM - 1] = (uint64_t)m.z | ((uint64_t)m.w << 32);  // (NM == 2 here)
+            S.qf = (uint32_t)(__popcll(S.F[0]) + __popcll(S.F[NM - 1]));
         }
     }
     if (len < (uint32_t)k) {
@@ -305,24 +321,30 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     }
     const uint32_t W = len - k + 1;
     S.W = W;
-    if (W > (uint32_t)kLaneMaxW) return (void)LANE_HARD_WHY(0);
+    if (W > (uint32_t)SH::MAXW) return (void)LANE_HARD_WHY(0);
     // ---- 2-bit pack: staged word q (32 bases from the 16-B aligned start) from
     // chunks 2q, 2q+1; row word q-1 = the read's bases from 0 on, shifted
     const uint4 *sp = (const uint4 *)(a.seq + o0);
     const uint32_t s2 = 2 * shift;
     uint32_t bad = 0;
     uint64_t prev = 0;
-    // every chunk load of the read issued before any is used (one round trip);
+    // every chunk load of the read issued before any is used (one round trip;
+    // the 250-bp shape: three, of six chunks each -- its registers);
     // chunks past the read read as "AAAA" (code 0, valid)
-    uint4 ch[2 * kLaneWords];
+    constexpr int CG = NM == 2 ? 2 * NWD : 6;  // chunks per round trip
 #pragma unroll
-    for (int c = 0; c < 2 * kLaneWords; c++)
-        ch[c] = 16u * c < shift + len ? sp[c] : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    for (int g0 = 0; g0 < 2 * NWD; g0 += CG) {
+    uint4 ch[CG];
 #pragma unroll
-    for (int q = 0; q <= kLaneWords; q++) {
+    for (int c = 0; c < CG; c++)
+        ch[c] = (g0 + c < 2 * NWD && 16u * (g0 + c) < shift + len)
+                    ? sp[g0 + c]
+                    : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+#pragma unroll
+    for (int q = g0 / 2; q < (g0 + CG) / 2 && q < NWD; q++) {
         uint64_t P = 0;
-        if (q < kLaneWords && 32u * q < shift + len) {
-            const uint4 v0 = ch[2 * q], v1 = ch[2 * q + 1];
+        if (32u * q < shift + len) {
+            const uint4 v0 = ch[2 * q - g0], v1 = ch[2 * q + 1 - g0];
             const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
             for (int e = 0; e < 8; e++) {
@@ -338,6 +360,8 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         if (q > 0) row[q - 1] = s2 ? ((prev << s2) | (P >> (64 - s2))) : prev;
         prev = P;
     }
+    }
+    row[NWD - 1] = prev << s2;  // (staged word NWD would be zero: shift + len <= 32 NWD - 1)
 #ifndef PA_PACK_MASKED
     // a non-ACGT byte in the staged chunks, most likely outside the read (the
     // buffer's padding after the last read): only the read's own bytes count
@@ -345,7 +369,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     if (bad) {
         bad = 0;
 #pragma unroll 1
-        for (int c = 0; c < 2 * kLaneWords; c++) {
+        for (int c = 0; c < 2 * NWD; c++) {
             if (16u * c >= shift + len) break;
             const uint4 v = sp[c];
             const uint32_t d[4] = {v.x, v.y, v.z, v.w};
@@ -355,7 +379,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         }
     }
 #endif
-    // (row[kLaneWords], the zero word past the read, is cleared once per kernel:
+    // (row[NWD], the zero word past the read, is cleared once per kernel:
     // a store here kept a 64-bit zero live through the whole loop and spilled it)
     if (bad) return (void)LANE_HARD_WHY(2);  // non-ACGT base: the wave kernel poisons its windows
 #if defined(PA_STATS) || defined(PA_DISSECT)
@@ -450,10 +474,10 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     if (at < 0) {  // no anchor: no seed k-mer is in the index
         if (a.queue_na) S.kind = LANE_NOANCHOR;
         // the reverse complements of the outer seeds -- R' windows 0 and W - 1
-        // of the read's reverse complement R' -- for k_rc_seeds (S.P0 / S.P1:
+        // of the read's reverse complement R' -- for k_rc_seeds (S.P[0] / S.P[1]:
         // walk fields, unused by such a read)
-        S.P0 = rc_key(skey[NSEED - 1], k);
-        S.P1 = rc_key(skey[0], k);
+        S.P[0] = rc_key(skey[NSEED - 1], k);
+        S.P[1] = rc_key(skey[0], k);
         return (void)LANE_HARD_WHY(3);
     }
     S.anc = stp[0] | ((uint64_t)sw(0) << 40);
@@ -495,7 +519,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             // the choice only steers the walk (any stretch gives the exact
             // result), and the genome words of three whole reads in flight
             // made the kernel spill
-            constexpr int NR = PA_LANE_RANK_WORDS;
+            constexpr int NR = NM == 2 ? PA_LANE_RANK_WORDS : 3;  // (the 250-bp shape: its registers)
             const uint32_t rlen = len < 32u * NR ? len : 32u * NR;
             const bool f0 = lane_fits(a, len, e0), f1 = lane_fits(a, len, e1), f2 = e2 != INT64_MIN && lane_fits(a, len, e2);
             uint64_t g0[NR + 1], g1[NR + 1], g2[NR + 1], u3[3];
@@ -518,10 +542,58 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     S.kind = LANE_WALK;
 }
 
+template <int NM>
+__device__ __forceinline__ uint64_t lane_any(const uint64_t (&m)[NM]) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < NM; i++) x |= m[i];
+    return x;
+}
+template <int NM>
+__device__ __forceinline__ uint32_t lane_popc(const uint64_t (&m)[NM]) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < NM; i++) x += (uint32_t)__popcll(m[i]);
+    return x;
+}
+
+// Bits lo .. hi (inclusive, 0 <= lo <= hi < 64 NM) as NM mask words (constant
+// word indices: selects, no scratch).
+template <int NM>
+__device__ __forceinline__ void range_mask(int32_t lo, int32_t hi, uint64_t (&r)[NM]) {
+#pragma unroll
+    for (int i = 0; i < NM; i++) {
+        const int32_t b = 64 * i, l = lo - b, h = hi - b;
+        r[i] = (h < 0 || l > 63) ? 0ull
+                                 : ((l <= 0 ? ~0ull : (~0ull << l)) & (h >= 63 ? ~0ull : ((2ull << h) - 1)));
+    }
+}
+
+// m |= v << sft over NM words, v a 32-bit word (sft may be negative: its low
+// bits fall below window 0).
+template <int NM>
+__device__ __forceinline__ void or_at(uint64_t (&m)[NM], uint64_t v, int32_t sft) {
+#pragma unroll
+    for (int i = 0; i < NM; i++) {
+        const int32_t s = sft - 64 * i;
+        m[i] |= (s >= 64 || s <= -32) ? 0ull : (s >= 0 ? v << s : v >> (-s));
+    }
+}
+
+// The NM words of planes p (NB = NM + 1 words from block A >> 6 on), shifted
+// down by fr = A & 63: bit w <-> genome position A + w.
+template <int NM>
+__device__ __forceinline__ void shifted_planes(const uint64_t (&p)[NM + 1], uint32_t fr, uint64_t (&out)[NM]) {
+#pragma unroll
+    for (int i = 0; i < NM; i++) out[i] = fr ? (p[i] >> fr) | (p[i + 1] << (64 - fr)) : p[i];
+}
+
 // Phase 2: walk from the anchor; walked windows resolve from the tile, the
-// others are left in P0 / P1 for the cooperative probes.
+// others are left in S.P for the cooperative probes.  The 150-bp shape (NM =
+// 2) in named words: the NM-general form (lane_walk_long) needs ~10 more
+// VGPRs here, and the kernel then spills at 4 waves per SIMD.
 template <bool WIN_Q, bool MG>
-__device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *row, LaneRead &S) {
+__device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t *row, LaneRead<2> &S) {
     const int k = a.k;
     const uint32_t W = S.W, len = S.len;
     const uint64_t atp = S.anc & kPosMask;
@@ -679,7 +751,7 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     const uint64_t in0 = W >= 64 ? ~0ull : ((1ull << W) - 1);
     const uint64_t in1 = W <= 64 ? 0ull : (W >= 128 ? ~0ull : ((1ull << (W - 64)) - 1));
     // windows failing the k-mer quality filter are never looked up (src/kmer.py:420-423)
-    const uint64_t live0 = WIN_Q ? in0 & ~S.F0 : in0, live1 = WIN_Q ? in1 & ~S.F1 : in1;
+    const uint64_t live0 = WIN_Q ? in0 & ~S.F[0] : in0, live1 = WIN_Q ? in1 & ~S.F[1] : in1;
     const uint64_t valid0 = IX0 & live0, valid1 = IX1 & live1;
     // probe: not an indexed genome window, or a mismatch that the neighbour
     // bits do not settle (two or more in the window, or the neighbour present)
@@ -725,8 +797,8 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     S.nspec = nspec;
     S.nincl = nincl;
     S.hr = hr + hr_off;  // windows, repeats included (quirk 4)
-    S.P0 = P0;
-    S.P1 = P1;
+    S.P[0] = P0;
+    S.P[1] = P1;
     // a read with very many unwalked windows is left to the wave kernel
     if ((uint32_t)(__popcll(P0) + __popcll(P1)) > a.lane_maxpend) {
         S.kind = LANE_HARD;
@@ -734,10 +806,237 @@ __device__ __forceinline__ void lane_walk(const AlignArgs &a, const uint64_t *ro
     }
 }
 
-// Phase 3 (whole wave): probe windows (Q0, Q1) of the walking lanes; `reset`
+// Phase 2 for the 250-bp shape (NM = 4; lane_walk_150 below states the steps):
+// the same walk over NM-word window masks.
+template <int NM, bool WIN_Q, bool MG>
+__device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_t *row, LaneRead<NM> &S) {
+    using SH = LaneShape<NM>;
+    constexpr int NWD = SH::NWD;
+    const int k = a.k;
+    const uint32_t W = S.W, len = S.len;
+    const uint64_t atp = S.anc & kPosMask;
+    const int64_t A = (int64_t)atp - (int64_t)(S.anc >> 40);  // genome position of window 0
+    const bool in_tile = A >= 0 && (uint64_t)A + W <= a.tile_n;
+    const uint64_t Ac = in_tile ? (uint64_t)A : 0;
+    // every load of the walk is issued before anything waits: the walk blocks
+    // of the read's span -- its genome words and the flag planes of windows
+    // 0 .. 64 NM - 1 (bit w <-> genome position A + w; tile_lw is padded) --
+    // and the anchor genome's range
+    const uint32_t gr = (uint32_t)(2 * Ac & 63);
+    uint64_t gw[NWD + 1], pa3[NM + 1], pb3[NM + 1];
+    lane_blocks<true, NWD, NM + 1>(a, Ac, len, gw, pa3, pb3);
+    const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.gblk, atp);
+    S.g = g;
+    const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
+    // every window of the read must lie inside the anchor genome
+    if (!in_tile || A < (int64_t)gs || (uint64_t)A + W - 1 + k > ge) {
+        S.kind = LANE_HARD;
+        return (void)LANE_HARD_WHY(4);
+    }
+    const uint32_t fr = (uint32_t)(Ac & 63);
+    uint64_t PA[NM], PB[NM], IX[NM];
+    shifted_planes<NM>(pa3, fr, PA);
+    shifted_planes<NM>(pb3, fr, PB);
+#pragma unroll
+    for (int i = 0; i < NM; i++) IX[i] = PA[i] | PB[i];  // indexed genome windows
+    // ---- mismatching bases against the genome from A on.  U: windows with a
+    // mismatch, V: windows with two or more; with the neighbour bits (tile_nb)
+    // a window with exactly one mismatch is resolved by its bit (NP: the bits set).
+    // A mismatch inside no indexed window (an N run of the genome, where the
+    // read has some base) changes nothing that is decided here -- unindexed
+    // windows are probed anyway -- and does not count toward the cap
+    uint64_t U[NM], V[NM], NP[NM], NS[NM], NG[NM];
+#pragma unroll
+    for (int i = 0; i < NM; i++) U[i] = V[i] = NP[i] = NS[i] = NG[i] = 0;
+    uint32_t nmis = 0;
+    const bool has_nb = a.tile_nb != nullptr;
+    uint64_t epk = 0;  // positions e of the mismatches to look up in the neighbour bits (low 8 bits each, <= 8)
+    uint32_t ehi = 0;  //   and bit 8 of each (positions up to 271)
+    uint32_t cpk = 0;  //   their substitution index (cr - cg - 1) & 3 (2 bits each)
+    uint32_t nnb = 0;
+    const uint32_t qlast = (len - 1) >> 5, rl = len - 32 * qlast;  // the last word holds rl bases
+    const uint64_t tail = rl >= 32 ? ~0ull : ~0ull << (64 - 2 * rl);
+#pragma unroll
+    for (int i = 0; i < NWD; i++) {
+        if (32 * i >= (int)len) break;
+        const uint64_t gwi = gr ? ((gw[i] << gr) | (gw[i + 1] >> (64 - gr))) : gw[i];
+        uint64_t d = row[i] ^ gwi;
+        if ((uint32_t)i == qlast) d &= tail;
+        uint64_t m = (d | (d >> 1)) & 0x5555555555555555ull;  // one bit per mismatching base
+        while (m) {
+            const uint32_t j = __builtin_clzll(m) >> 1, e = 32 * i + j;
+            m &= ~(1ull << (62 - 2 * j));
+            const int32_t lo = (int32_t)e - k + 1 < 0 ? 0 : (int32_t)e - k + 1;
+            const int32_t hi = (int32_t)e < (int32_t)W - 1 ? (int32_t)e : (int32_t)W - 1;
+            if (lo > hi) continue;
+            uint64_t rr[NM];
+            range_mask<NM>(lo, hi, rr);
+            uint64_t hit = 0;
+#pragma unroll
+            for (int q = 0; q < NM; q++) hit |= rr[q] & IX[q];
+            if (!hit) continue;
+            if (++nmis > 8) {
+                // past the neighbour-bit budget (a sibling's stretch, not a few
+                // sequencing errors): its windows are probed; the walked ones
+                // still hold (a found specific k-mer re-anchors the read)
+                if (nmis > kLaneMaxMis) {
+                    S.kind = LANE_HARD;
+                    return (void)LANE_HARD_WHY(5);
+                }
+#pragma unroll
+                for (int q = 0; q < NM; q++) {
+                    V[q] |= rr[q];
+                    U[q] |= rr[q];
+                }
+                continue;
+            }
+#pragma unroll
+            for (int q = 0; q < NM; q++) {
+                V[q] |= U[q] & rr[q];
+                U[q] |= rr[q];
+            }
+            if (has_nb) {  // the neighbour word of the genome base at A + e and the read's base there
+                const uint32_t cg = (uint32_t)(gwi >> (62 - 2 * j)) & 3u, cr = (uint32_t)(row[i] >> (62 - 2 * j)) & 3u;
+                epk |= (uint64_t)(e & 255u) << (8 * nnb);
+                ehi |= (e >> 8) << nnb;
+                cpk |= ((cr - cg - 1) & 3u) << (2 * nnb);
+                nnb++;
+            }
+        }
+    }
+    // the neighbour words, four loads in flight at a time (one round trip for
+    // up to four mismatches, not one per mismatch)
+#pragma unroll 1
+    for (uint32_t b0 = 0; b0 < nnb; b0 += 4) {
+        uint64_t nv[4];
+        uint32_t ng[4];
+        int32_t sf[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t q = b0 + u < nnb ? b0 + u : b0;  // (a repeated load past the last)
+            const uint32_t e = ((uint32_t)(epk >> (8 * q)) & 255u) | (((ehi >> q) & 1u) << 8), c = (cpk >> (2 * q)) & 3u;
+            const uint64_t ni = 3 * ((uint64_t)A + e) + c;
+            // (one 8-B load either way, 4-B aligned, no branch: the 12-B form's
+            // 32-bit words loaded under a branch waited one by one)
+            uint64_t v8;
+            __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
+            nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
+            if (MG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
+                const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
+                ng[u] = a.tile_nbbig ? gv : 0u;
+            } else {
+                ng[u] = 0u;
+            }
+            sf[u] = b0 + u < nnb ? (int32_t)e - k + 1 : 1000;  // bit q of the word <-> window e - k + 1 + q
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (sf[u] == 1000) continue;
+            // present, present and specific (the 32-bit form: present only)
+            const uint64_t nbw = nv[u] & 0xFFFFFFFFull, nbs = a.nb_spec ? nv[u] >> 32 : nbw, nbg = ng[u];
+#ifdef PA_STATS
+            atomicAdd(&a.dbg[16], 1ull);
+#endif
+            const int32_t sft = sf[u];
+            or_at<NM>(NP, nbw, sft);
+            or_at<NM>(NS, nbs, sft);
+            if (MG) or_at<NM>(NG, nbg, sft);
+        }
+    }
+    if (!has_nb) {
+#pragma unroll
+        for (int q = 0; q < NM; q++) NP[q] = NS[q] = ~0ull;  // every mismatching window is probed
+    }
+    // a window with one mismatch whose k-mer is present but multi-genome needs
+    // no probe: it only makes the read ambiguous (if no specific k-mer is
+    // included) or sends it to the wave kernel (if one is).  Under
+    // --max-genomes its set size decides whether it is included at all or
+    // counted as highly redundant (src/kmer.py:425-427): known from the bits
+    // when a.mg_nb (NB: present with a set larger than mg -- every present one
+    // for mg <= 0, every multi-genome one for mg == 1, the per-mg bits
+    // tile_nbbig above), else the present neighbours are probed
+    const bool has_mg = MG;  // (a.prm.flags & F_MG)
+    const int32_t mgv = a.prm.mg;
+    const bool mgk = has_mg && a.mg_nb;
+    // ---- walked windows: masks from the planes.  valid: an indexed genome
+    // window, spec: its k-mer is specific (to g, the genome it lies in), rep:
+    // it may repeat inside the read
+    uint64_t P[NM], walked[NM];
+    uint32_t uoff = 0, hr_off = 0, npend = 0;
+    uint64_t reps = 0;
+#pragma unroll
+    for (int q = 0; q < NM; q++) {
+        const int32_t wl = (int32_t)W - 64 * q;
+        const uint64_t in = wl >= 64 ? ~0ull : (wl <= 0 ? 0ull : ((1ull << wl) - 1));
+        const uint64_t NB = !mgk ? 0ull : (mgv <= 0 ? NP[q] : (mgv == 1 ? NP[q] & ~NS[q] : NG[q]));
+        const uint64_t NQ = !has_mg ? NS[q] : (mgk ? NS[q] & ~NB : NP[q]);
+        // windows failing the k-mer quality filter are never looked up (src/kmer.py:420-423)
+        const uint64_t live = WIN_Q ? in & ~S.F[q] : in;
+        const uint64_t valid = IX[q] & live;
+        // probe: not an indexed genome window, or a mismatch that the neighbour
+        // bits do not settle (two or more in the window, or the neighbour present)
+        P[q] = (live & ~valid) | (valid & U[q] & (V[q] | NQ));
+        uoff += (uint32_t)__popcll(valid & U[q] & ~V[q] & NP[q] & ~NQ & ~NB);
+        hr_off += (uint32_t)__popcll(valid & U[q] & ~V[q] & NB);
+        walked[q] = valid & ~U[q];
+        reps |= walked[q] & PB[q] & ~PA[q];
+        npend += (uint32_t)__popcll(P[q]);
+#ifdef PA_STATS
+        atomicAdd(&a.dbg[17], (unsigned long long)__popcll(live & ~valid));
+        atomicAdd(&a.dbg[18], (unsigned long long)__popcll(valid & U[q] & V[q]));
+        atomicAdd(&a.dbg[19], (unsigned long long)__popcll(valid & U[q] & NQ & ~V[q]));
+#endif
+    }
+    S.uoff = uoff;
+    if (reps) {  // a k-mer that may repeat inside the read
+        S.kind = LANE_HARD;
+        return (void)LANE_HARD_WHY(6);
+    }
+    // highly redundant walked windows (src/kmer.py:425-427): set size > mg.  A
+    // specific k-mer has size 1, a multi-genome one at least 2, so only mg >= 2
+    // needs the sizes of the multi-genome windows (one bit plane per mg)
+    uint32_t hr = 0, nincl = 0, nspec = 0;
+    uint64_t bb[NM + 1];
+    if (has_mg && a.prm.mg >= 2) {  // the plane "set size > mg" of this mg (k_tile_big)
+        const uint64_t *bp = a.tile_big + (Ac >> 6);
+#pragma unroll
+        for (int q = 0; q <= NM; q++) bb[q] = bp[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NM; q++) {
+        const uint64_t spec = PA[q] & PB[q];
+        uint64_t big = 0;
+        if (has_mg) {
+            const int32_t mg = a.prm.mg;
+            if (mg < 1)
+                big = walked[q];
+            else if (mg == 1)
+                big = walked[q] & ~spec;
+            else
+                big = walked[q] & ~spec & (fr ? (bb[q] >> fr) | (bb[q + 1] << (64 - fr)) : bb[q]);
+        }
+        const uint64_t incl = walked[q] & ~big;
+        hr += (uint32_t)__popcll(big);
+        nincl += (uint32_t)__popcll(incl);
+        // a specific k-mer at a position inside genome g is specific to g
+        nspec += (uint32_t)__popcll(incl & spec);
+        S.P[q] = P[q];
+    }
+    S.nspec = nspec;
+    S.nincl = nincl;
+    S.hr = hr + hr_off;  // windows, repeats included (quirk 4)
+    // a read with very many unwalked windows is left to the wave kernel
+    if (npend > a.lane_maxpend * (uint32_t)(NM / 2)) {
+        S.kind = LANE_HARD;
+        return (void)LANE_HARD_WHY(8);
+    }
+}
+
+// Phase 3 (whole wave): probe windows Q of the walking lanes; `reset`
 // clears the lanes' outcomes first (LW.flags / hr / cand accumulate otherwise).
-__device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW, const LaneRead &S, uint64_t Q0,
-                                                uint64_t Q1, bool reset) {
+template <int NM>
+__device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM> &LW, const LaneRead<NM> &S,
+                                                const uint64_t (&Qin)[NM], bool reset) {
     const int lane = lane_id();
     const int sh = 64 - 2 * a.k;
     const bool walking = S.kind == LANE_WALK;
@@ -746,8 +1045,13 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
         LW.hr[lane] = 0;
         LW.cand[lane] = ~0ull;
     }
-    if (!walking) Q0 = Q1 = 0;
-    const uint32_t c = (uint32_t)(__popcll(Q0) + __popcll(Q1));
+    uint64_t Q[NM];
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < NM; q++) {
+        Q[q] = walking ? Qin[q] : 0ull;
+        c += (uint32_t)__popcll(Q[q]);
+    }
     const uint32_t incl = wave_incl_scan(c);
     const uint32_t pre = incl - c;
     const uint32_t total = __shfl(incl, 63);
@@ -758,13 +1062,25 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
         // this pass's entries of the lane: global indices [max(pre, base), min(pre + c, base + 256))
         const uint32_t lo = max(pre, base), hi = min(pre + c, base + (uint32_t)kPassEntries);
         for (uint32_t e = lo; e < hi; e++) {
-            uint32_t w;
-            if (Q0) {
-                w = __builtin_ctzll(Q0);
-                Q0 &= Q0 - 1;
+            uint32_t w = 0;
+            if constexpr (NM == 2) {
+                if (Q[0]) {
+                    w = __builtin_ctzll(Q[0]);
+                    Q[0] &= Q[0] - 1;
+                } else {
+                    w = 64 + __builtin_ctzll(Q[1]);
+                    Q[1] &= Q[1] - 1;
+                }
             } else {
-                w = 64 + __builtin_ctzll(Q1);
-                Q1 &= Q1 - 1;
+                bool got = false;
+#pragma unroll
+                for (int q = 0; q < NM; q++) {
+                    if (!got && Q[q]) {
+                        w = 64 * q + __builtin_ctzll(Q[q]);
+                        Q[q] &= Q[q] - 1;
+                        got = true;
+                    }
+                }
             }
             LW.list[e - base] = (uint16_t)((lane << 8) | w);
         }
@@ -845,9 +1161,15 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave &LW
 #ifndef PA_LANE_WAVES_Q
 #define PA_LANE_WAVES_Q 3
 #endif
-template <bool NEED_Q, bool WIN_Q, bool MG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((WIN_Q || MG) ? PA_LANE_WAVES_Q : PA_LANE_WAVES)))
+#ifndef PA_LANE_WAVES_LONG
+#define PA_LANE_WAVES_LONG 3  // the 250-bp shape (NM = 4: ~191-210 VGPRs; it spills 104-228 B/lane, but runs 1.15x faster than at 2 waves)
+#endif
+template <bool NEED_Q, bool WIN_Q, bool MG, int NM = 2>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
+    NM == 4 ? PA_LANE_WAVES_LONG : ((WIN_Q || MG) ? PA_LANE_WAVES_Q : PA_LANE_WAVES))))
 void k_align_lane(AlignArgs a) {
+    using LW_t = LaneWave<NM>;
+    constexpr int NWD = LaneShape<NM>::NWD;
     extern __shared__ __align__(16) unsigned char smem[];
     const uint32_t G = a.G;
     const int lane = lane_id();
@@ -856,7 +1178,7 @@ void k_align_lane(AlignArgs a) {
     unsigned long long *first = (unsigned long long *)smem;
     uint32_t *uniq = (uint32_t *)(first + (lds ? G : 0));
     // (the wave's index read from lane 0: the LDS base is then a scalar, not a VGPR held all kernel long)
-    LaneWave &LW = ((LaneWave *)(smem + cnt_bytes))[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    LW_t &LW = ((LW_t *)(smem + cnt_bytes))[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     if (lds) {
         for (uint32_t i = threadIdx.x; i < G; i += kBlock) {
             first[i] = (unsigned long long)PA_NO_FIRST_KEY;
@@ -872,7 +1194,7 @@ void k_align_lane(AlignArgs a) {
     // across the wave per chunk (a per-lane LDS slot kept its address live in
     // a VGPR all kernel long, and it spilled)
     uint64_t n_hr = 0, n_qf = 0;
-    LW.R[lane][kLaneWords] = 0;  // the zero word past every read (lane_prep writes words 0 .. kLaneWords - 1)
+    LW.R[lane][NWD] = 0;  // the zero word past every read (lane_prep writes words 0 .. NWD - 1)
     // Each wave takes chunks of 64 consecutive reads; a read whose walk finds a
     // specific k-mer off it is walked again from that k-mer, but later, with 63
     // others (a list per wave), so that the 3 % of such reads do not hold whole
@@ -898,16 +1220,21 @@ void k_align_lane(AlignArgs a) {
         } else {
             break;
         }
-        LaneRead S;
+        LaneRead<NM> S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows (and the taken list entries) are done with
-        if (r != ~0u) lane_prep<NEED_Q, WIN_Q>(a, r, cd, LW.R[lane], S);
+        if (r != ~0u) lane_prep<NM, NEED_Q, WIN_Q>(a, r, cd, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
 #pragma unroll 1
         for (int attempt = again_batch ? 1 : 0; attempt < 2; attempt++) {
-            if (S.kind == LANE_WALK) lane_walk<WIN_Q, MG>(a, LW.R[lane], S);
+            if (S.kind == LANE_WALK) {
+                if constexpr (NM == 2)
+                    lane_walk_150<WIN_Q, MG>(a, LW.R[lane], S);
+                else
+                    lane_walk_long<NM, WIN_Q, MG>(a, LW.R[lane], S);
+            }
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
 #endif
@@ -922,8 +1249,8 @@ void k_align_lane(AlignArgs a) {
             // Under --max-genomes the filtered_hr_kmers count needs the set size
             // of every window found off the walk: only when every one is known
             // from the bits (a.mg_nb, nothing left to probe).
-            if (S.kind == LANE_WALK && S.nspec > 0 && (!MG || (a.mg_nb && !(S.P0 | S.P1)))) {
-                const int64_t X = (int64_t)(__popcll(S.P0) + __popcll(S.P1) + S.uoff);
+            if (S.kind == LANE_WALK && S.nspec > 0 && (!MG || (a.mg_nb && !lane_any(S.P)))) {
+                const int64_t X = (int64_t)(lane_popc(S.P) + S.uoff);
                 const int64_t ns = (int64_t)S.nspec;
                 if (ns >= X + (a.prm.m > 0 ? a.prm.m : 1) && (a.prm.p < 0 || X - ns <= a.prm.p)) {
                     S.kind = LANE_UNIQUE;
@@ -939,7 +1266,7 @@ void k_align_lane(AlignArgs a) {
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
             }
-            lane_probe_wave(a, LW, S, S.P0, S.P1, true);
+            lane_probe_wave<NM>(a, LW, S, S.P, true);
             if (S.kind == LANE_WALK) {
                 const uint32_t fl = LW.flags[lane];
                 if (fl & 1u) {  // a specific k-mer off the walk: walk again from it (once)
@@ -1005,8 +1332,8 @@ void k_align_lane(AlignArgs a) {
             if (na) {
                 a.queue_na[qbase + lanes_below(nab)] = r;
                 if (a.queue_na_keys) {
-                    a.queue_na_keys[2 * (qbase + lanes_below(nab))] = S.P0;
-                    a.queue_na_keys[2 * (qbase + lanes_below(nab)) + 1] = S.P1;
+                    a.queue_na_keys[2 * (qbase + lanes_below(nab))] = S.P[0];
+                    a.queue_na_keys[2 * (qbase + lanes_below(nab)) + 1] = S.P[1];
                 }
             }
         }
@@ -1054,8 +1381,9 @@ void k_align_lane(AlignArgs a) {
     }
 }
 
-constexpr size_t lane_lds_bytes(uint32_t G) {
-    return (G <= kLaneLdsGenomeCap ? ((size_t)G * 12 + 15) / 16 * 16 : 0) + (size_t)kWaves * sizeof(LaneWave);
+constexpr size_t lane_lds_bytes(uint32_t G, int NM = 2) {
+    return (G <= kLaneLdsGenomeCap ? ((size_t)G * 12 + 15) / 16 * 16 : 0) +
+           (size_t)kWaves * (NM == 4 ? sizeof(LaneWave<4>) : sizeof(LaneWave<2>));
 }
 
 // k_align_lane_na: the reads k_align_lane found no seed for, one per lane.
@@ -1424,13 +1752,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
     for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); c0 < n;
          c0 += (uint64_t)gridDim.x * kBlock) {
         const uint64_t i = c0 + lane;
-        LaneRead S;
+        LaneRead<2> S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         uint32_t r = 0;
         if (i < n) {
             r = a.queue_na[i];
             if (forward) S.kind = LANE_HARD;
-            else lane_prep<NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
+            else lane_prep<2, NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
         }
         if (S.kind == LANE_WALK) {
             const uint64_t *row = rows[threadIdx.x];
@@ -1453,7 +1781,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
 #pragma unroll
                 for (int j = 0; j < NAG; j++) {
                     const uint32_t w = w0 + j;
-                    const bool filt = WIN_Q && (((w < 64 ? S.F0 >> w : S.F1 >> (w - 64)) & 1ull) != 0);
+                    const bool filt = WIN_Q && (((w < 64 ? S.F[0] >> w : S.F[1] >> (w - 64)) & 1ull) != 0);
                     act |= (w < W && !filt) ? 1u << j : 0u;
                 }
                 if (!act) {
@@ -1615,14 +1943,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
     uint32_t hr_sum = 0, qf_sum = 0;
     for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock + wbase; c0 < n; c0 += (uint64_t)gridDim.x * kBlock) {
         const uint64_t i = c0 + lane;
-        LaneRead S;
+        LaneRead<2> S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         uint32_t r = 0;
         uint64_t seed = 0;
         if (i < n) {
             r = a.queue_rc[i];
             seed = a.queue_rc_anc[i];
-            lane_prep<NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
+            lane_prep<2, NEED_Q, WIN_Q, false>(a, r, ~0ull, rows[threadIdx.x], S);
         }
         const uint64_t *row = rows[threadIdx.x];
         uint32_t gm = 0;  // groups with a window to look up
@@ -1630,8 +1958,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
         if (S.kind == LANE_WALK) {
             if (na_rc_walk(a, row, S.len, S.W, seed, lk0, lk1)) {
                 if (WIN_Q) {  // windows failing --min-kmer-quality are never looked up
-                    lk0 &= ~S.F0;
-                    lk1 &= ~S.F1;
+                    lk0 &= ~S.F[0];
+                    lk1 &= ~S.F[1];
                 }
                 if (a.bloom) {
 #pragma unroll

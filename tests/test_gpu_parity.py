@@ -185,7 +185,10 @@ SYNTH = [
                                                 dict(mg=1), dict(mg=0)]),
     (6, 8000, 3, 0.03, 21, 4000, 100, 0.02, [dict(), dict(m=0, p=0), dict(mkq=60), dict(mg=2)]),
     (8, 6000, 4, 0.05, 25, 3000, 60, 0.01, [dict(), dict(m=2, p=0)]),
-    (10, 9000, 5, 0.02, 31, 2000, 250, 0.01, [dict(), dict(m=0, p=0), dict(mkq=58)]),
+    # 250-bp reads: the lane kernel's 256-window shape (NM = 4), with and without filters
+    (10, 9000, 5, 0.02, 31, 2000, 250, 0.01, [dict(), dict(m=0, p=0), dict(mkq=58), dict(mrq=58, mg=2), dict(mg=1),
+                                               dict(mrq=57), dict(m=3, p=0)]),
+    (25, 40000, 5, 0.01, 31, 12000, 272, 0.01, [dict(), dict(m=0, p=-1), dict(mg=3), dict(m=2, p=0)]),
     (5, 7000, 5, 0.01, 32, 2000, 120, 0.01, [dict(), dict(m=0, p=0)]),  # 2-word keys, fast path
     (5, 7000, 5, 0.01, 45, 1500, 150, 0.01, [dict(), dict(m=0, p=0)]),
     (4, 5000, 2, 0.02, 64, 800, 150, 0.005, [dict(), dict(m=0, p=0)]),  # 3-word keys, wave kernel
@@ -351,6 +354,28 @@ def test_synthesized_reads_parity():
                       mg=full["mg"], detail=False)
         assert stats.tolist() == o.stats.tolist()
         assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist()
+
+
+@pytest.mark.parametrize("read_len", [177, 250, 272])
+def test_synthesized_long_reads_parity(read_len):
+    """Device-synthesized reads longer than the 150-bp lane shape takes (the
+    256-window shape, or the wave kernel past 272 bases) against the oracle."""
+    gens = synth.family_genomes(20, 60000, seed=7, family_size=5, sub_rate=0.01, conserved_len=1000)
+    index = N.Index(gens, 31)
+    reads = N.Reads.synthesize(index, 30000, read_len, first_read=0, seed=3, sub_rate=0.008)
+    s, q, off = reads.download()
+    oix = O.OracleIndex(gens, 31)
+    for ps in (dict(), dict(mrq=58, mg=3), dict(m=0, p=0)):
+        full = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+        result = N.Result(index)
+        N.align(index, reads, N.Params.make(full["m"], full["p"], full["mrq"], full["mkq"], full["mg"]), 0, result)
+        stats, uq, am, fk = result.fetch()
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=full["m"], p=full["p"], mrq=full["mrq"], mkq=full["mkq"],
+                      mg=full["mg"], detail=False)
+        assert stats.tolist() == o.stats.tolist(), ps
+        assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
+        ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+        assert fk.tolist() == ofk.tolist(), ps
 
 
 def test_edge_cases():
