@@ -834,11 +834,9 @@ __device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_
         return (void)LANE_HARD_WHY(4);
     }
     const uint32_t fr = (uint32_t)(Ac & 63);
-    uint64_t PA[NM], PB[NM], IX[NM];
+    uint64_t PA[NM], PB[NM];  // (indexed genome windows: PA | PB, recomputed where used -- registers)
     shifted_planes<NM>(pa3, fr, PA);
     shifted_planes<NM>(pb3, fr, PB);
-#pragma unroll
-    for (int i = 0; i < NM; i++) IX[i] = PA[i] | PB[i];  // indexed genome windows
     // ---- mismatching bases against the genome from A on.  U: windows with a
     // mismatch, V: windows with two or more; with the neighbour bits (tile_nb)
     // a window with exactly one mismatch is resolved by its bit (NP: the bits set).
@@ -873,7 +871,7 @@ __device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_
             range_mask<NM>(lo, hi, rr);
             uint64_t hit = 0;
 #pragma unroll
-            for (int q = 0; q < NM; q++) hit |= rr[q] & IX[q];
+            for (int q = 0; q < NM; q++) hit |= rr[q] & (PA[q] | PB[q]);
             if (!hit) continue;
             if (++nmis > 8) {
                 // past the neighbour-bit budget (a sibling's stretch, not a few
@@ -972,7 +970,7 @@ __device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_
         const uint64_t NQ = !has_mg ? NS[q] : (mgk ? NS[q] & ~NB : NP[q]);
         // windows failing the k-mer quality filter are never looked up (src/kmer.py:420-423)
         const uint64_t live = WIN_Q ? in & ~S.F[q] : in;
-        const uint64_t valid = IX[q] & live;
+        const uint64_t valid = (PA[q] | PB[q]) & live;
         // probe: not an indexed genome window, or a mismatch that the neighbour
         // bits do not settle (two or more in the window, or the neighbour present)
         P[q] = (live & ~valid) | (valid & U[q] & (V[q] | NQ));
