@@ -218,10 +218,11 @@ __device__ __forceinline__ void quality_read(const uint8_t *__restrict__ qual, u
         const int32_t hi = (int32_t)len - 32 * d;
         E[d] &= hi >= 32 ? ~0u : hi <= 0 ? 0u : (1u << hi) - 1;
     }
-    const uint32_t sh = (uint32_t)k - 1;  // < 32
+    const uint32_t sh = (uint32_t)k - 1, shb = sh & 31;  // (k <= 63: a shift of up to one word and 31 bits)
+    const bool w1 = sh >= 32;
     uint32_t F[4];
 #pragma unroll
-    for (int d = 0; d < 4; d++) F[d] = __builtin_amdgcn_alignbit(E[d + 1], E[d], sh);
+    for (int d = 0; d < 4; d++) F[d] = __builtin_amdgcn_alignbit(w1 ? E[d + 2] : E[d + 1], w1 ? E[d + 1] : E[d], shb);
     mask = make_uint4(F[0], F[1], F[2], F[3]);
 }
 
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(256) void k_quality_masks(const uint8_t *__restrict
                                                        uint4 *__restrict__ qmask, uint8_t *__restrict__ qdrop) {
     const int64_t T64 = mkq * (int64_t)k;
     const uint32_t T = T64 <= 0 ? 0u : (T64 > (1 << 24) ? (1u << 24) : (uint32_t)T64);
-    switch (k >> 2) {  // (k <= 31 on the lane path; uniform)
+    switch (k >> 2) {  // (k <= 63 on the lane path; uniform)
         case 0: quality_reads<0>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 1: quality_reads<1>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 2: quality_reads<2>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
@@ -259,7 +260,15 @@ __global__ __launch_bounds__(256) void k_quality_masks(const uint8_t *__restrict
         case 5: quality_reads<5>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 6: quality_reads<6>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 7: quality_reads<7>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
-        default: break;  // (unreachable: the launch requires k <= 31)
+        case 8: quality_reads<8>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 9: quality_reads<9>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 10: quality_reads<10>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 11: quality_reads<11>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 12: quality_reads<12>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 13: quality_reads<13>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 14: quality_reads<14>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        case 15: quality_reads<15>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+        default: break;  // (unreachable: the launch requires k <= 63)
     }
 }
 
@@ -727,13 +736,20 @@ struct KernelTimer {
 // bases): the 250-bp shape (NM = 4, <= 272 bases, <= 256 windows) walks them,
 // unless --min-kmer-quality is set (its window masks cover 128 windows: such
 // reads then go to the wave kernel).
-pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr, bool long_reads = false) {
+// nw: key words (2: 31 < k <= 63 -- the 150-bp shape, no reverse-strand path:
+// reads without a seed go to the wave kernel).
+pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr, bool long_reads = false,
+                      int nw = 1) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
     const bool win_q = (a.prm.flags & F_MKQ) != 0;
     const bool mg = (a.prm.flags & F_MG) != 0;
-    const bool nm4 = long_reads && !win_q;
+    const bool nm4 = long_reads && !win_q && nw == 1;
     const size_t shm = lane_lds_bytes(a.G, nm4 ? 4 : 2);
-    auto kern = nm4 ? (need_q ? (mg ? k_align_lane<true, false, true, 4> : k_align_lane<true, false, false, 4>)
+    auto kern = nw == 2
+                    ? (win_q ? (mg ? k_align_lane<true, true, true, 2, 2> : k_align_lane<true, true, false, 2, 2>)
+                       : need_q ? (mg ? k_align_lane<true, false, true, 2, 2> : k_align_lane<true, false, false, 2, 2>)
+                                : (mg ? k_align_lane<false, false, true, 2, 2> : k_align_lane<false, false, false, 2, 2>))
+              : nm4 ? (need_q ? (mg ? k_align_lane<true, false, true, 4> : k_align_lane<true, false, false, 4>)
                               : (mg ? k_align_lane<false, false, true, 4> : k_align_lane<false, false, false, 4>))
               : win_q ? (mg ? k_align_lane<true, true, true> : k_align_lane<true, true, false>)
               : need_q ? (mg ? k_align_lane<true, false, true> : k_align_lane<true, false, false>)
@@ -1037,7 +1053,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
     const bool fast_ok = idx->k > 0 && idx->nw <= 4 && idx->n_kmers > 0;  // (k <= 127: the wave kernel's keys)
     // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
     const char *no_lane = std::getenv("PA_NO_LANE");
-    const bool lane_ok = fast_ok && idx->nw == 1 && a.tile_n > 0 && a.tile_lw && !(no_lane && no_lane[0] == '1');
+    const bool lane_ok = fast_ok && idx->nw <= 2 && a.tile_n > 0 && a.tile_lw && !(no_lane && no_lane[0] == '1');
     if (fast_ok) {
         const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
         const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4
@@ -1090,8 +1106,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.queue_hard_count = (unsigned long long *)idx->counters + 3;
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));
             if (a.prm.flags & (F_MRQ | F_MKQ)) {  // the quality filters of every read, up front
-                if (idx->k > 31) {  // (k_quality_masks realigns by k >> 2 <= 7: lane_ok implies k <= 31)
-                    set_error("internal: quality pre-pass for k > 31");
+                if (idx->k > 63) {  // (k_quality_masks realigns by k >> 2 <= 15: lane_ok implies k <= 63)
+                    set_error("internal: quality pre-pass for k > 63");
                     return PA_EINTERNAL;
                 }
                 PA_TRY(ensure_qmask(idx, r->n));
@@ -1106,6 +1122,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             // reads without a seed in the index: k_align_lane_na (with a Bloom filter; PA_LANE_NOANCHOR=0/1)
             bool na = a.bloom != nullptr;
             if (const char *e = std::getenv("PA_LANE_NOANCHOR")) na = e[0] == '1';
+            if (idx->nw != 1) na = false;  // (the reverse-strand / Bloom-group kernels take single-word keys)
             a.queue_na = na ? idx->queue_na : nullptr;
             a.queue_na_count = idx->na_count;
             // their reverse-complement seeds (k_rc_seeds -> k_align_lane_rc):
@@ -1120,7 +1137,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.na_min = 32768;  // (PA_NA_MIN: tests)
             if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
             if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 24, st));
-            PA_TRY(launch_lane(a, st, idx, r->max_len > (uint32_t)kLaneMaxLen));
+            PA_TRY(launch_lane(a, st, idx, r->max_len > (uint32_t)kLaneMaxLen, idx->nw));
             a.rlist = idx->queue_hard;
             a.rlist_count = a.queue_hard_count;
         }

@@ -291,6 +291,15 @@ __device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uin
     const uint32_t mn = k == 31 ? key_minimizer_c<31>(key) : key_minimizer(key, k);
     w = (bloom_block(mn, lg) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
 }
+// The Bloom word of a two-word key (31 < k <= 63, the lane path of long k):
+// the block by a hash of the key (no minimizer runs: a read's windows off the
+// walk are probed one by one), the bits by its mix as above.
+__device__ __forceinline__ void bloom_word2(const Key<2> &key, uint32_t lg, uint64_t &w, uint64_t &m) {
+    const uint32_t h = bloom_key_mix(key.w[1] ^ (key.w[0] * 0x9E3779B97F4A7C15ull));
+    m = bloom_bits(h);
+    const uint64_t b = fmix64(key.w[1] ^ (key.w[0] * 0xC2B2AE3D27D4EB4Full) ^ 0x5851F42D4C957F2Dull);
+    w = ((b >> (64 - (lg - kBloomLgBW))) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
+}
 // Minimizer presence bitmap (mm_bits, 2^lg bits): bit mm_bit(mn) is set for
 // the minimizer of every key (k_mm_build) -- a prefilter small enough to stay
 // in the L2 that answers a whole minimizer run of absent windows.

@@ -590,25 +590,38 @@ __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, u
 // < kTileRepDist apart), which the lane kernel (pa_lane.h) tests instead of
 // deduplicating.  One block per 256 positions, keys staged in LDS.
 constexpr int kTileRepDist = 255;  // (>= the lane kernels' longest span of windows: 256 windows, pa_lane.h)
+template <int NW>  // (1: k <= 31, 2: k <= 63 -- the key words compared)
 __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ pk, uint32_t *tile_cls, uint64_t n,
                                                   int k) {
-    __shared__ uint64_t keys[256 + kTileRepDist];
+    __shared__ uint64_t keys[NW][256 + kTileRepDist];
     __shared__ uint32_t valid[256 + kTileRepDist];
-    const int sh = 64 - 2 * k;
+    const int sh = 64 - 2 * k, hb = 2 * k - 64;
     for (uint64_t b = (uint64_t)blockIdx.x * 256; b < n; b += (uint64_t)gridDim.x * 256) {
         __syncthreads();
         for (int i = threadIdx.x; i < 256 + kTileRepDist; i += 256) {
             const uint64_t t = b + i;
             const bool ok = t < n && tile_cls[t] != NONE;
             valid[i] = ok;
-            keys[i] = ok ? (get64_at(pk, 2 * t) >> sh) : 0;
+            if (NW == 1) {
+                keys[0][i] = ok ? (get64_at(pk, 2 * t) >> sh) : 0;
+            } else {  // the key's words (pa_lane.h row_key)
+                keys[NW - 1][i] = ok ? get64_at(pk, 2 * t + 2 * k - 64) : 0;
+                keys[0][i] = ok && hb ? get64_at(pk, 2 * t) >> (64 - hb) : 0;
+            }
         }
         __syncthreads();
         const uint64_t t = b + threadIdx.x;
         if (t < n && valid[threadIdx.x]) {
-            const uint64_t me = keys[threadIdx.x];
+            uint64_t me[NW];
+#pragma unroll
+            for (int j = 0; j < NW; j++) me[j] = keys[j][threadIdx.x];
             bool rep = false;
-            for (int d = 1; d <= kTileRepDist; d++) rep |= valid[threadIdx.x + d] && keys[threadIdx.x + d] == me;
+            for (int d = 1; d <= kTileRepDist; d++) {
+                bool eq = valid[threadIdx.x + d] != 0;
+#pragma unroll
+                for (int j = 0; j < NW; j++) eq = eq && keys[j][threadIdx.x + d] == me[j];
+                rep |= eq;
+            }
             if (rep) tile_cls[t] |= PA_TILE_REP;
         }
     }
@@ -698,6 +711,73 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
                     atomicOr(&nb[3 * (t + j) + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
                 else
                     atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
+            }
+        }
+    }
+}
+
+// The same for two-word keys (31 < k <= 63: pa_device.h bloom_word2).
+__global__ void k_bloom_build2(const Slot<2> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+        const Slot<2> s = table[i];
+        if (s.key[0] == EMPTY) continue;
+        Key<2> kk;
+        kk.w[0] = s.key[0];
+        kk.w[1] = s.key[1];
+        uint64_t w, m;
+        bloom_word2(kk, lg, w, m);
+        atomicOr((unsigned long long *)&bloom[w], (unsigned long long)m);
+    }
+}
+
+// The neighbour bits of two-word keys (31 < k <= 63; k_nb_build states the
+// scheme): bit i of nb[3 p + b] says whether the k-mer starting at p - k + 1 +
+// i with its base at p replaced by the b-th other base is in the index --
+// 64-bit words of present neighbours only (a present one is then probed by the
+// lane kernel).  The build-time Bloom filter (bloom_word2) in front of the probes.
+__global__ void k_nb_build2(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
+                            const Slot<2> *__restrict__ table, HomeCfg hc, uint32_t G, unsigned long long *nb,
+                            const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local,
+                            int pass, const uint64_t *__restrict__ bloom, uint32_t bloom_lg) {
+    const int hb = 2 * k - 64;  // bits of the key's top word
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; t < n; t += stride) {
+        if (tile_cls[t] == NONE) continue;
+        Key<2> K;
+        K.w[1] = get64_at(pk, 2 * t + 2 * k - 64);
+        K.w[0] = hb ? get64_at(pk, 2 * t) >> (64 - hb) : 0ull;
+        uint64_t slot;
+        uint32_t cls, tpos;
+        if (!table_find<2>(table, hc.cap, K, home_of<2>(K, key_hash(K), hc), slot, cls, tpos)) continue;
+        const uint64_t fo = first_pos(cls, tpos, G, class_genomes, goff, local != 0);
+        if ((fo == t) != (pass == 0)) continue;
+        if (pass == 1) {  // copy the first occurrence's bits of this window
+            for (int j = 0; j < k; j++)
+#pragma unroll
+                for (int b = 0; b < 3; b++) {
+                    const unsigned long long m = nb[3 * (fo + j) + b] & (1ull << (k - 1 - j));
+                    if (m) atomicOr(&nb[3 * (t + j) + b], m);
+                }
+            continue;
+        }
+        for (int j = 0; j < k; j++) {
+            const int bs = 2 * (k - 1 - j);  // the base's bit offset in the 2k-bit key
+            const int wi = bs >= 64 ? 0 : 1, bo = bs >= 64 ? bs - 64 : bs;
+            const uint64_t cj = (K.w[wi] >> bo) & 3;
+            for (int b = 0; b < 3; b++) {
+                Key<2> N = K;
+                N.w[wi] ^= (cj ^ ((cj + 1 + b) & 3)) << bo;
+                if (bloom) {
+                    uint64_t w, m;
+                    bloom_word2(N, bloom_lg, w, m);
+                    if ((bloom[w] & m) != m) continue;
+                }
+                uint64_t s2;
+                uint32_t c2, p2;
+                if (table_find<2>(table, hc.cap, N, home_of<2>(N, key_hash(N), hc), s2, c2, p2))
+                    atomicOr(&nb[3 * (t + j) + b], 1ull << (k - 1 - j));
             }
         }
     }
@@ -1066,7 +1146,10 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
 // One-substitution neighbour bits of the genome tiling (k_nb_build, tile_nb):
 // 24 B per base, made once per index (C2: ~50 ms of kernels, ~0.12 s with the
 // allocation) -- they repay themselves after ~4 reads per genome base.
+pa_status build_nb2(pa_index *idx, hipStream_t st);
+
 pa_status build_nb(pa_index *idx, hipStream_t st) {
+    if (idx->nw == 2) return build_nb2(idx, st);
     const uint64_t n = idx->tile_n;
     const int k = (int)idx->k;
     const uint32_t G = idx->n_genomes;
@@ -1144,6 +1227,50 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
     return PA_OK;
 }
 
+// Neighbour bits of two-word keys (k_nb_build2): 24 B per base (64-bit
+// present words) when that leaves a quarter of the free memory; no
+// reverse-complement bits (single-word keys only).
+pa_status build_nb2(pa_index *idx, hipStream_t st) {
+    const uint64_t n = idx->tile_n;
+    const int k = (int)idx->k;
+    const char *no_nb = std::getenv("PA_NO_NB");
+    size_t free_b = 0, total_b = 0;
+    if (!(no_nb && no_nb[0] == '1') && pa::dev_mem_info(&free_b, &total_b) == hipSuccess && n * 24 <= free_b / 4 * 3) {
+        PA_HIP(pa::dev_malloc(&idx->tile_nb, n * 24 + 64));
+        PA_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 24 + 64, st));
+        uint64_t *bb = nullptr;  // the build-time Bloom filter, 16 bits per key (freed below)
+        uint32_t bb_lg = 6;
+        if (idx->n_kmers > 0) {
+            while (bb_lg < 33 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;
+            size_t fb = 0, tb = 0;
+            if (pa::dev_mem_info(&fb, &tb) != hipSuccess) fb = 0;
+            while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
+            if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && pa::dev_malloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
+                PA_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
+                hipLaunchKernelGGL(k_bloom_build2, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                   dim3(kBlock), 0, st, (const Slot<2> *)idx->table, idx->cap, bb, bb_lg);
+            } else {
+                bb = nullptr;
+            }
+        }
+        for (int pass = 0; pass < 2; pass++)
+            hipLaunchKernelGGL(k_nb_build2, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
+                               idx->tile_pk, idx->tile_cls, n, k, (const Slot<2> *)idx->table, idx->home,
+                               idx->n_genomes, (unsigned long long *)idx->tile_nb, idx->class_genomes, idx->goff,
+                               idx->tpos_local, pass, bb, bb_lg);
+        PA_HIP(hipGetLastError());
+        if (bb) {
+            PA_HIP(hipStreamSynchronize(st));
+            pa::dev_free(bb);
+        }
+        idx->nb_spec = 0;
+        idx->device_bytes += n * 24;
+        phase_mark("nb: two-word keys");
+    }
+    idx->nb_pending = 0;
+    return PA_OK;
+}
+
 template <int NW>
 pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
     const uint32_t G = idx->n_genomes;
@@ -1187,10 +1314,12 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             B_HIP(hipStreamSynchronize(st));
             idx->device_bytes += nb_ * 4;
         }
-        if (k <= 31)
-            hipLaunchKernelGGL(k_tile_rep, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)), dim3(256), 0,
-                               st, idx->tile_pk, idx->tile_cls, n, k);
-        if (k <= 31) {
+        // the lane kernels' view: keys of one word (k <= 31) or two (k <= 63)
+        const bool lane_view = NW <= 2 && k <= 32 * NW - 1;
+        if (lane_view)
+            hipLaunchKernelGGL(k_tile_rep<NW <= 2 ? NW : 1>, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)),
+                               dim3(256), 0, st, idx->tile_pk, idx->tile_cls, n, k);
+        if (lane_view) {
             const uint64_t n_blocks = n / 64 + 8;  // padded: the 250-bp walk reads six blocks from any position
             B_HIP(pa::dev_malloc(&idx->tile_lw, n_blocks * 32));
             hipLaunchKernelGGL(k_tile_walk, dim3((unsigned)std::min<uint64_t>((n_blocks + 3) / 4, 1u << 20)), dim3(256),
@@ -1238,8 +1367,12 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                 if (ok) {
                     B_HIP(pa::dev_malloc(&idx->bloom, (1ull << lg) * 8));
                     B_HIP(hipMemsetAsync(idx->bloom, 0, (1ull << lg) * 8, st));
-                    hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
-                                       dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg, k);
+                    if (NW == 1)
+                        hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                           dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg, k);
+                    else
+                        hipLaunchKernelGGL(k_bloom_build2, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                           dim3(kBlock), 0, st, (const Slot<2> *)table, idx->cap, idx->bloom, lg);
                     idx->bloom_lg = lg;
                     idx->device_bytes += (1ull << lg) * 8;
                 }
@@ -1252,7 +1385,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                // or with PA_NO_MM=1
                 const char *nm = std::getenv("PA_NO_MM");
                 const uint32_t lg = 25;
-                if (!(nm && nm[0] == '1') && idx->bloom && idx->n_kmers / 9 <= (1ull << lg) / 4 &&
+                if (NW == 1 && !(nm && nm[0] == '1') && idx->bloom && idx->n_kmers / 9 <= (1ull << lg) / 4 &&
                     pa::dev_malloc(&idx->mm_bits, (1ull << lg) / 8) == hipSuccess) {
                     B_HIP(hipMemsetAsync(idx->mm_bits, 0, (1ull << lg) / 8, st));
                     hipLaunchKernelGGL(k_mm_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
@@ -1267,7 +1400,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             {  // the reverse-complement plane (k_tile_rcp), 1 bit per base; PA_NO_RCP=1: none
                 const char *nr = std::getenv("PA_NO_RCP");
                 const uint64_t n_blocks = n / 64 + 5;  // padded like the walk blocks
-                if (!(nr && nr[0] == '1') && pa::dev_malloc(&idx->tile_rcp, n_blocks * 8) == hipSuccess) {
+                if (NW == 1 && !(nr && nr[0] == '1') && pa::dev_malloc(&idx->tile_rcp, n_blocks * 8) == hipSuccess) {
                     hipLaunchKernelGGL(k_tile_rcp, dim3((unsigned)std::min<uint64_t>((n_blocks + 3) / 4, 1u << 20)),
                                        dim3(256), 0, st, idx->tile_cls, idx->tile_pk, n, k, (const Slot<1> *)table,
                                        idx->home, idx->bloom, idx->bloom_lg, idx->tile_rcp, n_blocks);
@@ -1389,7 +1522,7 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
     PhaseScope ps(t_phase ? t_phase : own.get());
     const uint64_t bases = idx->h_goff.empty() ? 0 : idx->h_goff.back();
     idx->nb_skip = reads_hint != ~0ull && reads_hint < kNbReadsPerBase * bases;
-    pa_status rc = build_tiles_nw<1>(idx, st);  // (tiles are made for single-word keys only)
+    pa_status rc = idx->nw == 2 ? build_tiles_nw<2>(idx, st) : build_tiles_nw<1>(idx, st);  // (one- or two-word keys)
     idx->nb_skip = 0;
     if (rc != PA_OK) {  // the index stays usable without its align-side view
         pa::dev_free(idx->tile_cls); pa::dev_free(idx->tile_pk); pa::dev_free(idx->tile_lw); pa::dev_free(idx->tile_nb);
@@ -1419,12 +1552,12 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     }
     for (auto &o : idx->h_goff) o -= goff[0];
     idx->total_windows = windows;
-    // genome tiling for single-word keys while positions fit 32 bits (tpos);
+    // genome tiling for keys of one or two words (k <= 63) while positions fit 32 bits (tpos);
     // PA_NO_TILE=1 turns it off (A/B measurements)
     const char *no_tile = std::getenv("PA_NO_TILE");
     uint64_t max_glen = 0;
     for (uint32_t g = 0; g < n; g++) max_glen = std::max<uint64_t>(max_glen, goff[g + 1] - goff[g]);
-    idx->tile_n = (idx->nw == 1 && k > 0 && total > 0 && max_glen < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
+    idx->tile_n = (idx->nw <= 2 && k > 0 && total > 0 && max_glen < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
                       ? total : 0;
     idx->tpos_local = total >= 0xFFFFFFFFull ? 1 : 0;
     // PA_LAYOUT=large (tests): every choice the build makes for a reference too

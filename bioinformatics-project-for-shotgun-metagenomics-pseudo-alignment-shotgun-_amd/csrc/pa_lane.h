@@ -70,9 +70,6 @@ constexpr uint32_t kLaneMaxMis = PA_LANE_MAXMIS;  // mismatching bases against t
 #ifndef PA_LANE_SEEDS
 #define PA_LANE_SEEDS 5   // seed windows probed per read (first ... last, evenly spread)
 #endif
-#ifndef PA_LANE_R2_ALL
-#define PA_LANE_R2_ALL 1  // (A/B r4: the middle seed alone when both outer seeds are absent: C2 3.35 vs 3.77, c2mix 1.50 vs 1.84 G reads/s)
-#endif
 #ifndef PA_SEED_SLOTS
 #define PA_SEED_SLOTS 2  // table slots per probe step of the seed probes
 #endif
@@ -189,6 +186,52 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
     }
 }
 
+// The same for keys of NW words (the lane path of 31 < k <= 63: NW = 2).
+template <int NP, int NS, int NW>
+__device__ __forceinline__ void lane_probe_k(const AlignArgs &a, const Key<NW> (&key)[NP], uint32_t act,
+                                             uint32_t &found, uint32_t (&cls)[NP], uint32_t (&tpos)[NP]) {
+    const Slot<NW> *table = (const Slot<NW> *)a.table;
+    uint64_t pos[NP];
+#pragma unroll
+    for (int i = 0; i < NP; i++) pos[i] = bit(act, i) ? home_of<NW>(key[i], key_hash(key[i]), a.home) : 0;
+    found = 0;
+    while (act) {
+        Slot<NW> s[NP][NS];
+#pragma unroll
+        for (int i = 0; i < NP; i++)
+            if (bit(act, i)) {
+                const uint64_t b = pos[i] & ~(uint64_t)(NS - 1);
+#pragma unroll
+                for (int h = 0; h < NS; h++) s[i][h] = table[b + h];
+            }
+#pragma unroll
+        for (int i = 0; i < NP; i++) {
+            if (!bit(act, i)) continue;
+            const uint64_t b = pos[i] & ~(uint64_t)(NS - 1);
+            bool done = false;
+#pragma unroll
+            for (int h = 0; h < NS; h++) {
+                if (done || b + h < pos[i]) continue;
+                if (s[i][h].key[0] == EMPTY) {
+                    done = true;
+                    continue;
+                }
+                bool eq = true;
+#pragma unroll
+                for (int j = 0; j < NW; j++) eq &= s[i][h].key[j] == key[i].w[j];
+                if (eq) {
+                    done = true;
+                    found |= 1u << i;
+                    cls[i] = s[i][h].cls;
+                    tpos[i] = s[i][h].tpos;
+                }
+            }
+            if (done) act &= ~(1u << i);
+            pos[i] = (b + NS == a.cap) ? 0 : b + NS;
+        }
+    }
+}
+
 #ifdef PA_STATS
 #define LANE_HARD_WHY(i) atomicAdd(&a.dbg[4 + (i)], 1ull)
 #else
@@ -218,6 +261,23 @@ __device__ __forceinline__ uint64_t row_bits(const uint64_t *row, uint32_t o) {
     const uint32_t q = o >> 6, r = o & 63;
     const uint64_t hi = row[q] << r;
     return r ? (hi | (row[q + 1] >> (64 - r))) : hi;
+}
+
+// The key of window w of a packed row: k bases from bit 2 w, laid out as
+// key_push builds them (the last 32 bases in the low word; for NW = 2 the
+// first k - 32 in the top one, zero at k = 32).
+template <int NW>
+__device__ __forceinline__ Key<NW> row_key(const uint64_t *row, uint32_t w, int k) {
+    Key<NW> K;
+    if constexpr (NW == 1) {
+        K.w[0] = row_bits(row, 2 * w) >> (64 - 2 * k);
+    } else {
+        static_assert(NW == 2, "lane-path keys: one or two words");
+        K.w[1] = row_bits(row, 2 * w + 2 * k - 64);
+        const int hb = 2 * k - 64;
+        K.w[0] = hb ? row_bits(row, 2 * w) >> (64 - hb) : 0ull;
+    }
+    return K;
 }
 
 // Bytes [lo, hi) of a dword at staged position p0 that belong to the read.
@@ -280,7 +340,7 @@ __device__ __forceinline__ bool lane_fits(const AlignArgs &a, uint32_t len, int6
 
 // Phase 1: qualities, packing (into the lane's LDS row), seeds -> anchor (a
 // read walked again: the given anchor, cd != ~0).
-template <int NM, bool NEED_Q, bool WIN_Q, bool SEEDS = true>
+template <int NM, bool NEED_Q, bool WIN_Q, bool SEEDS = true, int NW = 1>
 __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsigned long long cd, uint64_t *row,
                                           LaneRead<NM> &S) {
     using SH = LaneShape<NM>;
@@ -404,9 +464,16 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     constexpr int NSEED = PA_LANE_SEEDS;
     // (seed i's window, recomputed where needed rather than kept in registers)
     auto sw = [W](int i) { return (uint32_t)(((uint64_t)(W - 1) * (uint32_t)i) / (NSEED - 1)); };
-    uint64_t skey[NSEED];
+    uint64_t skey[NW == 1 ? NSEED : 1];  // (single-word keys)
+    Key<NW> skk[NW == 1 ? 1 : NSEED];    // (two-word keys, 31 < k <= 63)
+    if constexpr (NW == 1) {
 #pragma unroll
-    for (int i = 0; i < NSEED; i++) skey[i] = row_bits(row, 2 * sw(i)) >> sh;
+        for (int i = 0; i < NSEED; i++) skey[i] = row_bits(row, 2 * sw(i)) >> sh;
+    } else {
+        (void)sh;
+#pragma unroll
+        for (int i = 0; i < NSEED; i++) skk[i] = row_key<NW>(row, sw(i), k);
+    }
 #ifndef PA_LANE_SEED_ROUNDS
 #define PA_LANE_SEED_ROUNDS 2
 #endif
@@ -423,35 +490,15 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #pragma unroll 1
         for (int round = 0; round < 2 && act; round++) {
             uint32_t f;
-            lane_probe<NSEED, PA_SEED_SLOTS>(a, skey, act, f, scls, stp32);
+            if constexpr (NW == 1)
+                lane_probe<NSEED, PA_SEED_SLOTS>(a, skey, act, f, scls, stp32);
+            else
+                lane_probe_k<NSEED, PA_SEED_SLOTS, NW>(a, skk, act, f, scls, stp32);
             sfound |= f;
             bool spec = false;
 #pragma unroll
             for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && scls[i] < a.G && stp32[i] != NONE;
-            // (neither outer seed in the index at all -- a reverse-strand or
-            // unindexed read, or a forward one with errors at both ends: the
-            // middle seed alone, which finds the latter; PA_LANE_R2_ALL=1: all three)
-            const uint32_t r2 = (PA_LANE_R2_ALL || sfound) ? all & ~outer : 1u << (NSEED / 2);
-            act = (round == 0 && act != all && !spec) ? r2 : 0u;
-#ifdef PA_SEED_BLOOM  // (A/B r3: c2rc +0 %, C2 -7 % -- it pushed the kernel's spills from 20 to 44 B/lane)
-            // neither outer seed in the index (a reverse-strand read, an
-            // unindexed organism -- or sequencing errors at both ends): the
-            // middle seeds go through the Bloom filter first, and only those it
-            // lets through cost a table line
-            if (act && !sfound && a.bloom) {
-                uint64_t bw[NSEED], bm[NSEED];
-#pragma unroll
-                for (int i = 0; i < NSEED; i++) {
-                    uint64_t wi = 0;
-                    bm[i] = 0;
-                    if (bit(act, i)) bloom_word(skey[i], k, a.bloom_lg, wi, bm[i]);
-                    bw[i] = a.bloom[wi];  // (outside the branch: the loads issue together; word 0 for the others)
-                }
-#pragma unroll
-                for (int i = 0; i < NSEED; i++)
-                    if ((bw[i] & bm[i]) != bm[i]) act &= ~(1u << i);
-            }
-#endif
+            act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 14) act = 0;  // timing dissection: one seed round
 #endif
@@ -476,8 +523,10 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
         // the reverse complements of the outer seeds -- R' windows 0 and W - 1
         // of the read's reverse complement R' -- for k_rc_seeds (S.P[0] / S.P[1]:
         // walk fields, unused by such a read)
-        S.P[0] = rc_key(skey[NSEED - 1], k);
-        S.P[1] = rc_key(skey[0], k);
+        if constexpr (NW == 1) {
+            S.P[0] = rc_key(skey[NSEED - 1], k);
+            S.P[1] = rc_key(skey[0], k);
+        }
         return (void)LANE_HARD_WHY(3);
     }
     S.anc = stp[0] | ((uint64_t)sw(0) << 40);
@@ -592,7 +641,7 @@ __device__ __forceinline__ void shifted_planes(const uint64_t (&p)[NM + 1], uint
 // others are left in S.P for the cooperative probes.  The 150-bp shape (NM =
 // 2) in named words: the NM-general form (lane_walk_long) needs ~10 more
 // VGPRs here, and the kernel then spills at 4 waves per SIMD.
-template <bool WIN_Q, bool MG>
+template <bool WIN_Q, bool MG, int NW = 1>
 __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t *row, LaneRead<2> &S) {
     const int k = a.k;
     const uint32_t W = S.W, len = S.len;
@@ -694,8 +743,13 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
             // (one 8-B load either way, 4-B aligned, no branch: the 12-B form's
             // 32-bit words loaded under a branch waited one by one)
             uint64_t v8;
-            __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
-            nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
+            if constexpr (NW == 2) {  // (two-word keys: 64-bit words of present neighbours, k <= 63 windows)
+                v8 = ((const uint64_t *)a.tile_nb)[ni];
+                nv[u] = v8;
+            } else {
+                __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
+                nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
+            }
             if (MG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
                 const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
                 ng[u] = a.tile_nbbig ? gv : 0u;
@@ -708,11 +762,23 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
         for (int u = 0; u < 4; u++) {
             if (sf[u] == 1000) continue;
             // present, present and specific (the 32-bit form: present only)
+            const int32_t sft = sf[u];
+            if constexpr (NW == 2) {  // (present only; up to 63 windows: bits reach the second word from any sft > 0)
+                const uint64_t nbw = nv[u];
+                if (sft >= 0) {
+                    NP0 |= sft < 64 ? nbw << sft : 0ull;
+                    NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 0 ? nbw >> (64 - sft) : 0ull);
+                } else {
+                    NP0 |= nbw >> (-sft);
+                }
+                NS0 = NP0;
+                NS1 = NP1;
+                continue;
+            }
             const uint64_t nbw = nv[u] & 0xFFFFFFFFull, nbs = a.nb_spec ? nv[u] >> 32 : nbw, nbg = ng[u];
 #ifdef PA_STATS
             atomicAdd(&a.dbg[16], 1ull);
 #endif
-            const int32_t sft = sf[u];
             if (sft >= 0) {
                 NP0 |= sft < 64 ? nbw << sft : 0ull;
                 NP1 |= sft >= 64 ? nbw << (sft - 64) : (sft > 32 ? nbw >> (64 - sft) : 0ull);
@@ -1032,7 +1098,7 @@ __device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_
 
 // Phase 3 (whole wave): probe windows Q of the walking lanes; `reset`
 // clears the lanes' outcomes first (LW.flags / hr / cand accumulate otherwise).
-template <int NM>
+template <int NM, int NW = 1>
 __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM> &LW, const LaneRead<NM> &S,
                                                 const uint64_t (&Qin)[NM], bool reset) {
     const int lane = lane_id();
@@ -1085,21 +1151,27 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
         wave_sync();
         const uint32_t cnt = min(total - base, (uint32_t)kPassEntries);
         constexpr int NPR = PA_LANE_PROBES;
-        uint64_t key4[NPR];
+        uint64_t key4[NW == 1 ? NPR : 1];  // (single-word keys)
+        Key<NW> kk4[NW == 1 ? 1 : NPR];    // (two-word keys)
         uint32_t tag4[NPR], act = 0;
         // entry 64 i + lane: with fewer than 64 (NPR - 1) entries the last keys
         // of every lane are idle, and their hashing and probing is skipped
 #pragma unroll
         for (int i = 0; i < NPR; i++) {
             const uint32_t e = 64 * i + lane;
-            key4[i] = 0;
+            if constexpr (NW == 1) key4[i] = 0;
+            else kk4[i].w[0] = kk4[i].w[1] = 0;
             tag4[i] = 0;
             if (e < cnt) {
                 const uint32_t t = LW.list[e];
                 const uint64_t *row = LW.R[t >> 8];
-                const uint32_t o = 2 * (t & 255), q = o >> 6, rr = o & 63;
-                const uint64_t hi64 = row[q] << rr;
-                key4[i] = (rr ? (hi64 | (row[q + 1] >> (64 - rr))) : hi64) >> sh;
+                if constexpr (NW == 1) {
+                    const uint32_t o = 2 * (t & 255), q = o >> 6, rr = o & 63;
+                    const uint64_t hi64 = row[q] << rr;
+                    key4[i] = (rr ? (hi64 | (row[q + 1] >> (64 - rr))) : hi64) >> sh;
+                } else {
+                    kk4[i] = row_key<NW>(row, t & 255, a.k);
+                }
                 tag4[i] = t;
                 act |= 1u << i;
             }
@@ -1112,7 +1184,10 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
                 bm[i] = 0;
                 if (64u * i < cnt) {  // (uniform)
                     uint64_t wi;
-                    bloom_word(key4[i], a.k, a.bloom_lg, wi, bm[i]);
+                    if constexpr (NW == 1)
+                        bloom_word(key4[i], a.k, a.bloom_lg, wi, bm[i]);
+                    else
+                        bloom_word2(kk4[i], a.bloom_lg, wi, bm[i]);
                     bw[i] = a.bloom[bit(act, i) ? wi : 0ull];  // (no branch around the load: they issue together)
                     if (!bit(act, i)) bm[i] = 0;
                 }
@@ -1125,7 +1200,10 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
 #endif
         }
         uint32_t f, c4[NPR], t4[NPR];
-        lane_probe<NPR, PA_LANE_SLOTS>(a, key4, act, f, c4, t4);
+        if constexpr (NW == 1)
+            lane_probe<NPR, PA_LANE_SLOTS>(a, key4, act, f, c4, t4);
+        else
+            lane_probe_k<NPR, PA_LANE_SLOTS, NW>(a, kk4, act, f, c4, t4);
 #pragma unroll
         for (int i = 0; i < NPR; i++) {
             if (!bit(f, i)) continue;
@@ -1162,9 +1240,9 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
 #ifndef PA_LANE_WAVES_LONG
 #define PA_LANE_WAVES_LONG 3  // the 250-bp shape (NM = 4: ~191-210 VGPRs; it spills 104-228 B/lane, but runs 1.15x faster than at 2 waves)
 #endif
-template <bool NEED_Q, bool WIN_Q, bool MG, int NM = 2>
+template <bool NEED_Q, bool WIN_Q, bool MG, int NM = 2, int NW = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
-    NM == 4 ? PA_LANE_WAVES_LONG : ((WIN_Q || MG) ? PA_LANE_WAVES_Q : PA_LANE_WAVES))))
+    NM == 4 ? PA_LANE_WAVES_LONG : ((WIN_Q || MG || NW == 2) ? PA_LANE_WAVES_Q : PA_LANE_WAVES))))
 void k_align_lane(AlignArgs a) {
     using LW_t = LaneWave<NM>;
     constexpr int NWD = LaneShape<NM>::NWD;
@@ -1221,7 +1299,7 @@ void k_align_lane(AlignArgs a) {
         LaneRead<NM> S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows (and the taken list entries) are done with
-        if (r != ~0u) lane_prep<NM, NEED_Q, WIN_Q>(a, r, cd, LW.R[lane], S);
+        if (r != ~0u) lane_prep<NM, NEED_Q, WIN_Q, true, NW>(a, r, cd, LW.R[lane], S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
@@ -1229,7 +1307,7 @@ void k_align_lane(AlignArgs a) {
         for (int attempt = again_batch ? 1 : 0; attempt < 2; attempt++) {
             if (S.kind == LANE_WALK) {
                 if constexpr (NM == 2)
-                    lane_walk_150<WIN_Q, MG>(a, LW.R[lane], S);
+                    lane_walk_150<WIN_Q, MG, NW>(a, LW.R[lane], S);
                 else
                     lane_walk_long<NM, WIN_Q, MG>(a, LW.R[lane], S);
             }
@@ -1264,7 +1342,7 @@ void k_align_lane(AlignArgs a) {
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
             }
-            lane_probe_wave<NM>(a, LW, S, S.P, true);
+            lane_probe_wave<NM, NW>(a, LW, S, S.P, true);
             if (S.kind == LANE_WALK) {
                 const uint32_t fl = LW.flags[lane];
                 if (fl & 1u) {  // a specific k-mer off the walk: walk again from it (once)

@@ -254,7 +254,7 @@ def test_fast_kernel_vs_oracle(cfg):
                                         mkq=full["mkq"], mg=full["mg"]), idents, full["mrq"], full["mkq"], full["mg"])
 
 
-NO_NB = [c for c in SYNTH if c[4] <= 31 and c[0] in (12, 25, 500, 70)]
+NO_NB = [c for c in SYNTH if c[4] <= 63 and c[0] in (12, 25, 500, 70, 5)]
 
 
 @pytest.mark.parametrize("cfg", NO_NB, ids=[f"G{c[0]}_k{c[4]}_L{c[6]}" for c in NO_NB])
@@ -722,7 +722,7 @@ def test_reverse_strand_walk_vs_oracle(ps, rcwalk, monkeypatch):
     assert o.stats[2] > 10000  # mostly unmapped reverse-strand reads: the case under test
 
 
-@pytest.mark.parametrize("k", [3, 4, 5, 8, 11, 16, 21, 28, 31])
+@pytest.mark.parametrize("k", [3, 4, 5, 8, 11, 16, 21, 28, 31, 32, 33, 40, 47, 63])
 def test_quality_masks_every_k_vs_oracle(k):
     """k_quality_masks (the lane kernels' --min-read-quality / --min-kmer-quality
     pre-pass: 16-B chunks realigned to the read, the bytes k earlier by a second
