@@ -136,12 +136,24 @@ __device__ __forceinline__ uint64_t window_bits(const uint64_t *bm, uint32_t w, 
 }
 
 // Where a key starts probing: multiply-high range reduction of its hash over
-// the table's capacity.  (A minimizer-region variant -- keys of one super-k-mer
-// homed in one region -- measured 1.7-3x slower on C2 and was removed; the
-// genome walk of pa_fast.h / pa_lane.h gets the locality instead.)
+// the table's capacity.  PA_HOME_ALIGN = 4 homes every key at the start of its
+// aligned 4-slot group (the probes read whole groups, so a search then never
+// wastes the slots before its home): modelled to cut a wave's seed round trips
+// from ~1.9 to ~1.03 at C2's load (scripts/probe_model.py), measured on MI355X
+// 1-3 % SLOWER on C2 / c2mix / C4 / C5 (profiles/r04/ab_home_align.txt) -- the
+// lanes' extra round trips are hidden by the other waves, while bucketed homes
+// crowd the probes of a group -- so homes stay slot-granular.  (A
+// minimizer-region variant -- keys of one super-k-mer homed in one region --
+// measured 1.7-3x slower on C2 and was removed; the genome walk of pa_fast.h /
+// pa_lane.h gets the locality instead.)
+#ifndef PA_HOME_ALIGN
+#define PA_HOME_ALIGN 1
+#endif
+constexpr uint64_t kHomeAlign = PA_HOME_ALIGN;
+static_assert(kHomeAlign == 1 || kHomeAlign == 2 || kHomeAlign == 4, "tables are whole 4-slot groups");
 template <int NW>
 __device__ __forceinline__ uint64_t home_of(const Key<NW> &, uint64_t h, const HomeCfg &c) {
-    return home_slot(h, c.cap);
+    return home_slot(h, c.cap / kHomeAlign) * kHomeAlign;
 }
 
 // Read-only probe from a home slot (tables are immutable once built).
