@@ -491,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
             if (!clean) continue;
             uint64_t slot;
             uint32_t cls, tpos;
-            if (!table_find<NW>(table, a.cap, key, home_of(key, key_hash(key), a.home), slot, cls, tpos)) continue;
+            if (!table_find<NW, true>(table, a.cap, key, home_of(key, key_hash(key), a.home), slot, cls, tpos)) continue;
             if (has_mg && (int64_t)class_size_of(cls, G, a.class_genomes) > (int64_t)a.prm.mg) {
                 hr++;
                 continue;

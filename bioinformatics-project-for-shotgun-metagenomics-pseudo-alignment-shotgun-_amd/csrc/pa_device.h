@@ -156,8 +156,44 @@ __device__ __forceinline__ uint64_t home_of(const Key<NW> &, uint64_t h, const H
     return home_slot(h, c.cap / kHomeAlign) * kHomeAlign;
 }
 
-// Read-only probe from a home slot (tables are immutable once built).
+// Ordered clusters.  Once built, every run of occupied slots is put in the
+// order of its keys' homes (k_table_order, pa_index.hip): the layout linear
+// probing gives when the keys arrive in home order -- the same occupied slots,
+// every key at or after its home with no EMPTY slot between.  A search for a
+// key homed at h then also ends at the first slot j holding a key that is less
+// displaced than the searched one would be there (homed after h, counted
+// cyclically): the key cannot lie further.  Absent keys no longer run to the
+// end of their cluster, which at C5's load (0.48) cuts a wave's probe rounds
+// from ~4.5 to ~2.1 (scripts/probe_model.py: the slowest of a wave's ~128
+// probes sets the wave's pace).  The probes test the LAST slot of each group
+// they read (the cluster's homes rise along it), only on the path that would
+// read another group.  PA_TABLE_ORDER=0 builds tables without the pass, and
+// no probe may then use the test.
+#ifndef PA_TABLE_ORDER
+#define PA_TABLE_ORDER 1
+#endif
+constexpr bool kTableOrdered = PA_TABLE_ORDER != 0;
+
 template <int NW>
+__device__ __forceinline__ bool probe_past_key(const Key<NW> &rk, const Key<NW> &me, uint64_t j, const HomeCfg &hc) {
+    if constexpr (!kTableOrdered) return false;
+    const uint64_t hr = home_of<NW>(rk, key_hash(rk), hc), hm = home_of<NW>(me, key_hash(me), hc);
+    const uint64_t dr = j >= hr ? j - hr : j + hc.cap - hr;
+    const uint64_t dm = j >= hm ? j - hm : j + hc.cap - hm;
+    return dr < dm;
+}
+template <int NW>
+__device__ __forceinline__ bool probe_past(const Slot<NW> &r, const Key<NW> &me, uint64_t j, const HomeCfg &hc) {
+    Key<NW> rk;
+#pragma unroll
+    for (int t = 0; t < NW; t++) rk.w[t] = r.key[t];
+    return probe_past_key<NW>(rk, me, j, hc);
+}
+
+// Read-only probe from a home slot (tables are immutable once built).  ORD:
+// the table's clusters are ordered (every probe after the build; the build's
+// own passes before k_table_order run with ORD = false).
+template <int NW, bool ORD = false>
 __device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint64_t cap, const Key<NW> &k,
                                            uint64_t home, uint64_t &slot, uint32_t &cls, uint32_t &tpos) {
     uint64_t pos = home;
@@ -172,6 +208,13 @@ __device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint6
             cls = s.cls;
             tpos = s.tpos;
             return true;
+        }
+        if constexpr (ORD && kTableOrdered) {
+            Key<NW> rk;
+#pragma unroll
+            for (int j = 0; j < NW; j++) rk.w[j] = s.key[j];
+            const uint64_t hr = home_of<NW>(rk, key_hash(rk), HomeCfg{cap});
+            if ((pos >= hr ? pos - hr : pos + cap - hr) < (pos >= home ? pos - home : pos + cap - home)) return false;
         }
         pos = (pos + 1 == cap) ? 0 : pos + 1;
     }
@@ -218,6 +261,11 @@ __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, c
                     found |= 1u << i;
                     cls[i] = s[i][h].cls;
                 }
+            }
+            if (!done) {
+                Key<1> kk;
+                kk.w[0] = key[i];
+                done = probe_past<1>(s[i][3], kk, b + 3, hc);
             }
             if (done) act &= ~(1u << i);
             pos[i] = (b + 4 == hc.cap) ? 0 : b + 4;

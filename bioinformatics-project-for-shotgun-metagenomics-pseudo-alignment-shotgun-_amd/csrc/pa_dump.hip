@@ -88,7 +88,7 @@ __global__ void k_dump_first(const uint8_t *__restrict__ codes, uint64_t gstart,
         if (run < k) continue;  // (N windows are not indexed, src/kmer.py:145)
         uint64_t slot;
         uint32_t cls, tpos;
-        if (!table_find<NW>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) continue;
+        if (!table_find<NW, true>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) continue;
         const unsigned long long t = gstart + w;
         if (fp[slot] > t) atomicMin(&fp[slot], t);  // (a stale plain load only costs an atomic)
     }
@@ -120,7 +120,7 @@ __global__ void k_dump_keys(const uint8_t *__restrict__ codes, uint64_t gstart, 
             if (run < k) continue;
             uint64_t slot;
             uint32_t cls, tpos;
-            if (!table_find<NW>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) continue;
+            if (!table_find<NW, true>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) continue;
             K[gstart + w] = (T)fp[slot];
             cnt++;
         }

@@ -544,6 +544,8 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
                     tp[j] = s[j].tpos;
                     if constexpr (NW > 1) S.slot[j] = pos[j];
                     resolve(j, s[j].cls);
+                } else if (probe_past<NW>(s[j], S.key[j], pos[j], a.home)) {
+                    m &= ~(1u << j);  // ordered clusters: homed after this key, so it is absent
                 } else {
                     pos[j] = (pos[j] + 1 == a.cap) ? 0 : pos[j] + 1;
                 }
@@ -582,6 +584,7 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
                             tpos = s[i].tpos;
                         }
                     }
+                    if (!done) done = probe_past<1>(s[3], key, base + 3, a.home);
                     act = !done;
                     pos = (base + 4 == a.cap) ? 0 : base + 4;
                 }

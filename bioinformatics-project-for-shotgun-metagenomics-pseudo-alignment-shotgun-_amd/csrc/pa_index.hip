@@ -505,7 +505,7 @@ __global__ void k_lookup(const Slot<NW> *table, HomeCfg hc, const uint8_t *kmers
     }
     uint64_t slot;
     uint32_t cls = 0, tpos = 0;
-    if (ok && table_find<NW>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) {
+    if (ok && table_find<NW, true>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) {
         cls_out[i] = cls;
         size_out[i] = class_size_of(cls, G, class_genomes);
     } else {
@@ -571,7 +571,7 @@ __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, u
         if (run < k) continue;
         uint64_t slot;
         uint32_t cls, tpos;
-        if (table_find<NW>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) {
+        if (table_find<NW, true>(table, hc.cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) {
             tile_cls[gstart + w] = cls;
             if (local) {
                 const uint32_t fg = cls < G ? cls : class_genomes[cls - G + 1];
@@ -665,7 +665,7 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
         kk.w[0] = K;
         uint64_t slot;
         uint32_t cls, tpos;
-        if (!table_find<1>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos)) continue;
+        if (!table_find<1, true>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos)) continue;
         const uint64_t fo = first_pos(cls, tpos, G, class_genomes, goff, local != 0);
         if ((fo == t) != (pass == 0)) continue;
         if (pass == 1) {  // copy the first occurrence's bits of this window
@@ -750,7 +750,7 @@ __global__ void k_nb_build2(const uint64_t *__restrict__ pk, const uint32_t *__r
         K.w[0] = hb ? get64_at(pk, 2 * t) >> (64 - hb) : 0ull;
         uint64_t slot;
         uint32_t cls, tpos;
-        if (!table_find<2>(table, hc.cap, K, home_of<2>(K, key_hash(K), hc), slot, cls, tpos)) continue;
+        if (!table_find<2, true>(table, hc.cap, K, home_of<2>(K, key_hash(K), hc), slot, cls, tpos)) continue;
         const uint64_t fo = first_pos(cls, tpos, G, class_genomes, goff, local != 0);
         if ((fo == t) != (pass == 0)) continue;
         if (pass == 1) {  // copy the first occurrence's bits of this window
@@ -776,7 +776,7 @@ __global__ void k_nb_build2(const uint64_t *__restrict__ pk, const uint32_t *__r
                 }
                 uint64_t s2;
                 uint32_t c2, p2;
-                if (table_find<2>(table, hc.cap, N, home_of<2>(N, key_hash(N), hc), s2, c2, p2))
+                if (table_find<2, true>(table, hc.cap, N, home_of<2>(N, key_hash(N), hc), s2, c2, p2))
                     atomicOr(&nb[3 * (t + j) + b], 1ull << (k - 1 - j));
             }
         }
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) void k_tile_rcp(const uint32_t *__restrict__ t
             }
             uint64_t slot;
             uint32_t cls, tpos;
-            if (maybe) maybe = table_find<1>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos);
+            if (maybe) maybe = table_find<1, true>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos);
         }
         const uint64_t b = __ballot(maybe);
         if (lane == 0) rcp[j] = b;
@@ -866,6 +866,46 @@ __global__ __launch_bounds__(256) void k_tile_walk(const uint32_t *__restrict__ 
                              : lane == 1 ? (64 * j + 32 < n ? pk[2 * j + 1] : 0ull)
                              : lane == 2 ? a : b;
             lw[4 * j + lane] = w;
+        }
+    }
+}
+
+// ---- ordered clusters (see probe_past, pa_device.h) --------------------------
+// The last pass of a build: every cluster (maximal run of occupied slots,
+// cyclic) put in the order of its keys' homes counted from its first slot, by
+// one thread per cluster (the slot after an EMPTY one), an insertion sort in
+// place.  Only slots move (key, class and first position together); the
+// occupied slots stay the same, every key stays at or after its home with no
+// EMPTY slot between, so every search finds what it found before.  A key only
+// moves back past keys homed after it, which lie inside its own probe span, so
+// the work is the sum of the displacements, not the square of a cluster's
+// length.  C5's 87 GB table: one read of its slots.
+template <int NW>
+__global__ void k_table_order(Slot<NW> *table, HomeCfg hc) {
+    const uint64_t cap = hc.cap;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (; i < cap; i += stride) {
+        if (table[i].key[0] == EMPTY || table[i == 0 ? cap - 1 : i - 1].key[0] != EMPTY) continue;
+        auto at = [&](uint64_t t) { return i + t >= cap ? i + t - cap : i + t; };
+        auto rel = [&](const Slot<NW> &s) {  // home, counted from the cluster's first slot
+            Key<NW> kk;
+#pragma unroll
+            for (int j = 0; j < NW; j++) kk.w[j] = s.key[j];
+            const uint64_t h = home_of<NW>(kk, key_hash(kk), hc);
+            return h >= i ? h - i : h + cap - i;
+        };
+        for (uint64_t t = 1;; t++) {
+            const Slot<NW> x = table[at(t)];
+            if (x.key[0] == EMPTY) break;
+            const uint64_t hx = rel(x);
+            uint64_t q = t;
+            for (; q > 0; q--) {
+                const Slot<NW> y = table[at(q - 1)];
+                if (rel(y) <= hx) break;
+                table[at(q)] = y;
+            }
+            if (q != t) table[at(q)] = x;
         }
     }
 }
@@ -1129,6 +1169,16 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         idx->n_multi = n_cls;
         idx->class_entries = entries;
         idx->device_bytes += n_cls * 12 + std::max<uint64_t>(entries, 1) * 4;
+    }
+    if (kTableOrdered && idx->n_kmers > 0) {
+        if (idx->n_kmers >= cap) {  // (the sizing keeps the load <= 0.7: never)
+            pa::set_error("index build: hash table full (internal error)");
+            cleanup();
+            return PA_EINTERNAL;
+        }
+        hipLaunchKernelGGL(k_table_order<NW>, dim3(grid_for(cap) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0, st,
+                           table, idx->home);
+        B_HIP(hipGetLastError());
     }
     if (idx->tile_n > 0 && (uint64_t)G + idx->class_entries >= PA_TILE_REP) idx->tile_n = 0;  // ids need bit 31
     idx->tiles_pending = idx->tile_n > 0 ? 1 : 0;  // made by build_tiles_nw (index_prepare)

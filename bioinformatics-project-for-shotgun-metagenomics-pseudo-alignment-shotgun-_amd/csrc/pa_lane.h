@@ -138,8 +138,16 @@ __device__ __forceinline__ uint32_t genome_of(const uint64_t *goff, const uint32
 }
 
 // Up to NP table probes of one lane in flight together, NS slots (an aligned
-// NS x 16-B group) per step; linear-probing order is kept exactly.
-template <int NP, int NS = 2>
+// NS x 16-B group) per step; linear-probing order is kept exactly.  ORD: end a
+// search at a key homed after the searched one (probe_past) -- off in the lane
+// kernels (PA_LANE_ORD=1 turns it on for the cooperative probes): its hashes
+// cost the 128-VGPR plain variant 200 B/lane of scratch.  The ordered table
+// still shortens their searches of present keys.
+#ifndef PA_LANE_ORD
+#define PA_LANE_ORD 0
+#endif
+constexpr bool kLaneOrd = PA_LANE_ORD != 0 && kTableOrdered;
+template <int NP, int NS = 2, bool ORD = false>
 __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&key)[NP], uint32_t act,
                                            uint32_t &found, uint32_t (&cls)[NP], uint32_t (&tpos)[NP]) {
     const Slot<1> *table = (const Slot<1> *)a.table;
@@ -156,6 +164,7 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
     found = 0;
     while (act) {
         Slot<1> s[NP][NS];
+        uint64_t last[NP];
 #pragma unroll
         for (int i = 0; i < NP; i++)
             if (bit(act, i)) {
@@ -181,13 +190,24 @@ __device__ __forceinline__ void lane_probe(const AlignArgs &a, const uint64_t (&
                 }
             }
             if (done) act &= ~(1u << i);
+            if (ORD && !done) last[i] = s[i][NS - 1].key[0];
             pos[i] = (b + NS == a.cap) ? 0 : b + NS;
+        }
+        if constexpr (ORD) {  // ordered clusters: a key homed after this one ends its search
+#pragma unroll
+            for (int i = 0; i < NP; i++)
+                if (bit(act, i)) {
+                    Key<1> r, me;
+                    r.w[0] = last[i];
+                    me.w[0] = key[i];
+                    if (probe_past_key<1>(r, me, pos[i] == 0 ? a.cap - 1 : pos[i] - 1, a.home)) act &= ~(1u << i);
+                }
         }
     }
 }
 
 // The same for keys of NW words (the lane path of 31 < k <= 63: NW = 2).
-template <int NP, int NS, int NW>
+template <int NP, int NS, int NW, bool ORD = false>
 __device__ __forceinline__ void lane_probe_k(const AlignArgs &a, const Key<NW> (&key)[NP], uint32_t act,
                                              uint32_t &found, uint32_t (&cls)[NP], uint32_t (&tpos)[NP]) {
     const Slot<NW> *table = (const Slot<NW> *)a.table;
@@ -197,6 +217,7 @@ __device__ __forceinline__ void lane_probe_k(const AlignArgs &a, const Key<NW> (
     found = 0;
     while (act) {
         Slot<NW> s[NP][NS];
+        Key<NW> last[NP];
 #pragma unroll
         for (int i = 0; i < NP; i++)
             if (bit(act, i)) {
@@ -227,7 +248,16 @@ __device__ __forceinline__ void lane_probe_k(const AlignArgs &a, const Key<NW> (
                 }
             }
             if (done) act &= ~(1u << i);
+            if (ORD && !done)
+#pragma unroll
+                for (int j = 0; j < NW; j++) last[i].w[j] = s[i][NS - 1].key[j];
             pos[i] = (b + NS == a.cap) ? 0 : b + NS;
+        }
+        if constexpr (ORD) {
+#pragma unroll
+            for (int i = 0; i < NP; i++)
+                if (bit(act, i) && probe_past_key<NW>(last[i], key[i], pos[i] == 0 ? a.cap - 1 : pos[i] - 1, a.home))
+                    act &= ~(1u << i);
         }
     }
 }
@@ -1201,9 +1231,9 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
         }
         uint32_t f, c4[NPR], t4[NPR];
         if constexpr (NW == 1)
-            lane_probe<NPR, PA_LANE_SLOTS>(a, key4, act, f, c4, t4);
+            lane_probe<NPR, PA_LANE_SLOTS, kLaneOrd>(a, key4, act, f, c4, t4);
         else
-            lane_probe_k<NPR, PA_LANE_SLOTS, NW>(a, kk4, act, f, c4, t4);
+            lane_probe_k<NPR, PA_LANE_SLOTS, NW, kLaneOrd>(a, kk4, act, f, c4, t4);
 #pragma unroll
         for (int i = 0; i < NPR; i++) {
             if (!bit(f, i)) continue;

@@ -85,6 +85,9 @@ def _check(case, ps, base=0):
     return stats
 
 
+_LIVE = []  # cases still holding device memory (module fixtures end only with the module)
+
+
 class _Full:
     """A device index of a packed reference, `n_reads` synthesized reads (the
     bench's, seed 2) and the restricted oracle over their k-mers."""
@@ -102,11 +105,15 @@ class _Full:
         s, _, off = self.host
         self.oix = O.OracleIndex.restricted(packed, K, (s, off), threads=THREADS)
         _say(f"restricted oracle {time.perf_counter() - t0:.1f} s: {self.oix.n_kmers} read k-mers in the reference")
+        _LIVE.append(self)
 
     def close(self):
+        if self.index is None:
+            return
         self.reads.close()
         self.index.close()
-        self.oix = None
+        self.reads = self.index = self.oix = None
+        _LIVE.remove(self)
 
 
 # ---- C4: 500 x 2 Mbp ----------------------------------------------------------------
@@ -141,6 +148,8 @@ C5_ROWS = list(range(0, 10)) + list(range(1995, 2000)) + [1000, 1503]  # familie
 @pytest.fixture(scope="module")
 def c5_full():
     import kmer
+    for case in list(_LIVE):  # C4's index (~100 GB) would leave C5's build too little HBM
+        case.close()
     t0 = time.perf_counter()
     gens = synth.family_genomes_fast(2000, 4_000_000, seed=1, family_size=5, sub_rate=0.01, conserved_len=5000,
                                      n_rate=1e-4, n_run=10, near_dup_every=2)  # bench.py CONFIGS["c5"]
