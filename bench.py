@@ -505,9 +505,8 @@ def main():
     if args.kept_file:  # traffic child: the parent's EXTSIM outcome
         with open(args.kept_file) as f:
             kept_idx = json.load(f)
-        index.close()
         genomes = [genomes[i] for i in kept_idx]
-        index = N.Index(genomes, cfg["k"], device=local, stream=stream, defer_tiles=True)
+        index.reduce(kept_idx, stream)
         torch.cuda.synchronize(dev)
     elif cfg.get("extsim") is not None:
         # EXTSIM (src/kmer.py:152-263): GPU statistics + the greedy pass; a
@@ -519,10 +518,9 @@ def main():
         stats_s = time.perf_counter() - t0
         kept_idx = [j for j, i in enumerate(idents) if i in keep]
         t1 = time.perf_counter()
-        if len(keep) != len(idents):
-            index.close()
+        if len(keep) != len(idents):  # the kept genomes' index, from their codes on the device
             genomes = [genomes[j] for j in kept_idx]
-            index = N.Index(genomes, cfg["k"], device=local, stream=stream, defer_tiles=True)
+            index.reduce(kept_idx, stream)
             torch.cuda.synchronize(dev)
             build_bases += sum(len(g) for g in genomes)
         rebuild_s = time.perf_counter() - t1

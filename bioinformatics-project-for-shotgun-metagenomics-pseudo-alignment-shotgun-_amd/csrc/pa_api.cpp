@@ -145,6 +145,17 @@ pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t 
     return PA_OK;
 }
 
+pa_status pa_index_reduce(pa_index *idx, const uint32_t *keep, uint32_t n_keep, uint32_t flags, void *stream) {
+    PA_CHECK(idx != nullptr && (n_keep == 0 || keep != nullptr), PA_EINVAL, "NULL argument");
+    for (uint32_t i = 0; i < n_keep; i++) {
+        PA_CHECK(keep[i] < idx->n_genomes, PA_EINVAL, "genome number out of range");
+        PA_CHECK(i == 0 || keep[i] > keep[i - 1], PA_EINVAL, "genome numbers must be ascending");
+    }
+    PA_HIP(hipSetDevice(idx->device));
+    PA_TRY(pa::index_reduce(idx, keep, n_keep, as_stream(stream), (flags & PA_BUILD_DEFER_TILES) != 0));
+    return PA_OK;
+}
+
 pa_status pa_index_prepare(pa_index *idx, void *stream) {
     PA_CHECK(idx != nullptr, PA_EINVAL, "NULL argument");
     PA_HIP(hipSetDevice(idx->device));

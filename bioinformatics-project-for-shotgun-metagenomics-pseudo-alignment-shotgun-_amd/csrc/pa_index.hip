@@ -649,6 +649,10 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 // REVERSE COMPLEMENTS, for k_align_lane_rc's reverse-strand walk -- a read
 // window that is the reverse complement of the genome's k-mer but for one base
 // is then resolved by one bit, as a forward one by tile_nb.
+#ifndef PA_NB_CHUNK
+#define PA_NB_CHUNK 4
+#endif
+constexpr int kNbChunk = PA_NB_CHUNK;
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
                            const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
                            const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local,
@@ -683,34 +687,54 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
             }
             continue;
         }
-        for (int j = 0; j < k; j++) {
+        // kNbChunk positions at a time: their 3 kNbChunk Bloom words are loaded
+        // together (one round trip, not one per position), then the few
+        // neighbours the filter lets through are probed position by position
+        auto nkey = [&](int j, int b) {
             const int bs = 2 * (k - 1 - j);
             const uint64_t cj = (K >> bs) & 3;
-            uint64_t keys[3];
-            uint32_t cls3[3];
+            const uint64_t v = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
+            return rc ? rc_key(v, k) : v;  // (tile_rcnb: the neighbour's reverse complement)
+        };
+        for (int j0 = 0; j0 < k; j0 += kNbChunk) {
+            uint32_t pass_bits = ~0u;  // bit 3 jj + b: neighbour (j0 + jj, b) may be present
+            if (bloom) {  // surely absent neighbours are not probed
+                uint64_t wv[kNbChunk][3], bm[kNbChunk][3];
 #pragma unroll
-            for (int b = 0; b < 3; b++) {
-                keys[b] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
-                if (rc) keys[b] = rc_key(keys[b], k);  // (tile_rcnb: the neighbour's reverse complement)
+                for (int jj = 0; jj < kNbChunk; jj++)
+#pragma unroll
+                    for (int b = 0; b < 3; b++) {
+                        wv[jj][b] = 0, bm[jj][b] = 0;
+                        if (j0 + jj < k) {
+                            uint64_t wi;
+                            bloom_word(nkey(j0 + jj, b), k, bloom_lg, wi, bm[jj][b]);
+                            wv[jj][b] = bloom[wi];
+                        }
+                    }
+                pass_bits = 0;
+#pragma unroll
+                for (int jj = 0; jj < kNbChunk; jj++)
+#pragma unroll
+                    for (int b = 0; b < 3; b++)
+                        if (j0 + jj < k && (wv[jj][b] & bm[jj][b]) == bm[jj][b]) pass_bits |= 1u << (3 * jj + b);
             }
-            uint32_t act = 7u;
-            if (bloom) {  // surely absent neighbours are not probed; most share the window's Bloom line
+            for (int jj = 0; jj < kNbChunk && j0 + jj < k; jj++) {
+                const uint32_t act = (pass_bits >> (3 * jj)) & 7u;
+                if (!act) continue;
+                const int j = j0 + jj;
+                uint64_t keys[3];
+                uint32_t cls3[3];
+#pragma unroll
+                for (int b = 0; b < 3; b++) keys[b] = nkey(j, b);
+                const uint32_t f = probe_lines<3>(table, hc, keys, cls3, act);  // the substitutions together
 #pragma unroll
                 for (int b = 0; b < 3; b++) {
-                    uint64_t wi, bm;
-                    bloom_word(keys[b], k, bloom_lg, wi, bm);
-                    if ((bloom[wi] & bm) != bm) act &= ~(1u << b);
+                    if (!((f >> b) & 1u)) continue;
+                    if (full)
+                        atomicOr(&nb[3 * (t + j) + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                    else
+                        atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
                 }
-                if (!act) continue;
-            }
-            const uint32_t f = probe_lines<3>(table, hc, keys, cls3, act);  // the substitutions together
-#pragma unroll
-            for (int b = 0; b < 3; b++) {
-                if (!((f >> b) & 1u)) continue;
-                if (full)
-                    atomicOr(&nb[3 * (t + j) + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
-                else
-                    atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
             }
         }
     }
@@ -1587,7 +1611,7 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
 }
 
 pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
-                      hipStream_t st, bool defer_tiles) {
+                      hipStream_t st, bool defer_tiles, uint8_t *dev_codes) {
     PhaseTimer tm(st);
     PhaseScope ps(&tm);
     idx->k = k;
@@ -1617,12 +1641,15 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     if (const char *e = std::getenv("PA_LAYOUT")) idx->force_large = std::strcmp(e, "large") == 0;
     if (const char *e = std::getenv("PA_TPOS_LOCAL")) idx->tpos_local |= e[0] == '1';  // tests: the >= 4 Gbp layout
     idx->tpos_local |= idx->force_large;
-    PA_HIP(pa::dev_malloc(&idx->codes, std::max<uint64_t>(total, 1)));
+    if (dev_codes)
+        idx->codes = dev_codes;  // (index_reduce: the 2-bit codes are on the device already)
+    else
+        PA_HIP(pa::dev_malloc(&idx->codes, std::max<uint64_t>(total, 1)));
     PA_HIP(pa::dev_malloc(&idx->goff, (n + 1) * 8));
     PA_HIP(pa::dev_malloc(&idx->counters, 32 * 8));
     PA_HIP(hipMemsetAsync(idx->counters, 0, 32 * 8, st));
     PA_HIP(hipMemcpyAsync(idx->goff, idx->h_goff.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    if (total > 0) {
+    if (total > 0 && !dev_codes) {
         uint8_t *ascii = nullptr;  // ASCII staging buffer, freed before the table is allocated
         unsigned long long *bad = nullptr, h_bad = ~0ull;
         PA_HIP(pa::dev_malloc(&ascii, total));
@@ -1751,6 +1778,38 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     rc = index_prepare(idx, st);
     tm.mark("tiles");
     return rc;
+}
+
+// The index of some of its genomes, in place: their 2-bit codes gathered on
+// the device (one copy per run of consecutive kept genomes), everything else
+// released, then the build from those codes.  The EXTSIM rebuild
+// (KmerReference._filter_similar_genomes; the reference prunes its dict,
+// src/kmer.py:232-263) without concatenating and uploading the kept genomes
+// again: C5's 1200 of 2000 genomes, 4.8 GB.
+pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream_t st, bool defer_tiles) {
+    std::vector<uint64_t> goff(n + 1, 0);
+    for (uint32_t i = 0; i < n; i++) goff[i + 1] = goff[i] + (idx->h_goff[sel[i] + 1] - idx->h_goff[sel[i]]);
+    uint8_t *codes = nullptr;
+    PA_HIP(pa::dev_malloc(&codes, std::max<uint64_t>(goff[n], 1)));
+    hipError_t e = hipSuccess;
+    for (uint32_t i = 0; i < n && e == hipSuccess;) {
+        uint32_t j = i;
+        while (j + 1 < n && sel[j + 1] == sel[j] + 1) j++;
+        const uint64_t from = idx->h_goff[sel[i]], len = idx->h_goff[sel[j] + 1] - from;
+        if (len) e = hipMemcpyAsync(codes + goff[i], idx->codes + from, len, hipMemcpyDeviceToDevice, st);
+        i = j + 1;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        pa::dev_free(codes);
+        PA_HIP(e);
+    }
+    const int64_t k = idx->k;
+    const int device = idx->device;
+    index_release(idx);
+    *idx = pa_index();
+    idx->device = device;
+    return index_build(idx, nullptr, goff.data(), n, k, st, defer_tiles, codes);
 }
 
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,

@@ -170,7 +170,8 @@ struct pa_result {
 
 namespace pa {
 pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, uint32_t n, int64_t k,
-                      hipStream_t st, bool defer_tiles);
+                      hipStream_t st, bool defer_tiles, uint8_t *dev_codes = nullptr);
+pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream_t st, bool defer_tiles);
 // The tiles of a deferred build (no-op otherwise).  reads_hint: the reads the
 // caller expects to align with this index; below kNbReadsPerBase per genome
 // base the neighbour bits are left for later (index_note_reads makes them once

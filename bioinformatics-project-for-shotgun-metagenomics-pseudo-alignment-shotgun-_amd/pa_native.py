@@ -32,7 +32,7 @@ PA_POS_REVERSE, PA_POS_RC_BIT = 1, 0x80000000
 # every symbol declared in include/pa.h
 EXPORTS = (
     "pa_last_error", "pa_version", "pa_device_count", "pa_runtime_start",
-    "pa_index_build", "pa_index_build_ex", "pa_index_prepare", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
+    "pa_index_build", "pa_index_build_ex", "pa_index_reduce", "pa_index_prepare", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
     "pa_index_positions",
     "pa_index_extsim_stats", "pa_index_dumpref",
     "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_reads_download", "pa_reads_free",
@@ -111,6 +111,7 @@ def lib():
         "pa_runtime_start": (I32, [I32]),
         "pa_index_build": (I32, [I32, ctypes.c_char_p, P, U32, I64, P, PP]),
         "pa_index_build_ex": (I32, [I32, ctypes.c_char_p, P, U32, I64, U32, P, PP]),
+        "pa_index_reduce": (I32, [P, P, U32, U32, P]),
         "pa_index_prepare": (I32, [P, P]),
         "pa_index_free": (None, [P]),
         "pa_index_get_info": (I32, [P, ctypes.POINTER(IndexInfo)]),
@@ -337,11 +338,28 @@ def parse_text(kind: int, text, threads: Optional[int] = None, universal_newline
     return _seqset_columns(h, kind)
 
 
+def _contiguous_views(chunks) -> bool:
+    """uint8 arrays that are views of one C-contiguous buffer, back to back."""
+    base = chunks[0].base
+    if base is None or not isinstance(base, np.ndarray) or not base.flags.c_contiguous or base.dtype != np.uint8:
+        return False
+    at = chunks[0].ctypes.data
+    for c in chunks:
+        if c.base is not base or c.ctypes.data != at or not c.flags.c_contiguous:
+            return False
+        at += c.size
+    return True
+
+
 def concat(chunks: Sequence) -> Tuple[np.ndarray, np.ndarray]:
     """Concatenate str/bytes/uint8 chunks into (uint8 array, uint64 CSR offsets)."""
     if chunks and all(isinstance(c, np.ndarray) and c.dtype == np.uint8 and c.ndim == 1 for c in chunks):
         off = np.zeros(len(chunks) + 1, dtype=np.uint64)
         off[1:] = np.cumsum([c.size for c in chunks], dtype=np.uint64)
+        if _contiguous_views(chunks):  # consecutive views of one buffer: no copy
+            whole = chunks[0].base if chunks[0].base is not None else chunks[0]
+            start = chunks[0].ctypes.data - whole.ctypes.data
+            return whole.reshape(-1)[start:start + int(off[-1])], off
         return np.concatenate(chunks), off  # (one copy: multi-Gbp references, BASELINE config 5)
     bs = [c.encode() if isinstance(c, str) else (c.tobytes() if isinstance(c, np.ndarray) else bytes(c))
           for c in chunks]
@@ -379,6 +397,19 @@ class Index:
     @property
     def handle(self):
         return self._h
+
+    def reduce(self, keep: Sequence[int], stream=None, defer_tiles: bool = True) -> None:
+        """Rebuild this index over the genomes numbered ``keep`` (ascending), in
+        place, from their 2-bit codes already on the device (pa_index_reduce):
+        the EXTSIM rebuild without uploading the kept genomes again.  On an
+        error the index is left empty and closed."""
+        sel = np.ascontiguousarray(np.asarray(keep, dtype=np.uint32))
+        st = lib().pa_index_reduce(self._h, _ptr(sel), len(sel), PA_BUILD_DEFER_TILES if defer_tiles else 0,
+                                   _stream(stream))
+        if st != PA_OK and st != PA_EINVAL:
+            self.close()
+        _check(st)
+        self.n_genomes = len(sel)
 
     def prepare(self, stream=None) -> None:
         """Make a deferred build's align-side view now (pa_index_prepare)."""

@@ -37,10 +37,12 @@ def family_genomes(n_genomes: int, length: int, seed: int = 1, family_size: int 
     conserved = ACGT[rng.integers(0, 4, size=conserved_len)] if conserved_len > 0 else None
     out: List[np.ndarray] = []
     base = None
+    whole = np.empty(n_genomes * length, dtype=np.uint8)  # (views of one buffer, as family_genomes_fast)
     for g in range(n_genomes):
         if g % max(family_size, 1) == 0:
             base = ACGT[rng.integers(0, 4, size=length)]
-        seq = base.copy()
+        seq = whole[g * length:(g + 1) * length]
+        seq[:] = base
         if sub_rate > 0:
             hit = np.flatnonzero(rng.random(length) < sub_rate)
             # substitute with one of the three other bases
@@ -80,6 +82,9 @@ def family_genomes_fast(n_genomes: int, length: int, seed: int = 1, family_size:
     out: List[np.ndarray] = []
     base = None
     fam = max(family_size, 1)
+    # the genomes are views of one buffer, back to back (pa_native.concat then
+    # hands it to the index build without a copy)
+    whole = np.empty(n_genomes * length, dtype=np.uint8)
     for g in range(n_genomes):
         if g % fam == 0:
             base = rng.integers(0, 4, size=length, dtype=np.uint8)
@@ -89,7 +94,8 @@ def family_genomes_fast(n_genomes: int, length: int, seed: int = 1, family_size:
         if rate > 0:
             hit = rng.integers(0, length, size=int(rng.binomial(length, rate)))
             codes[hit] = (codes[hit] + rng.integers(1, 4, size=hit.size, dtype=np.uint8)) & 3
-        seq = ACGT[codes]
+        seq = whole[g * length:(g + 1) * length]
+        np.take(ACGT, codes, out=seq)
         if conserved is not None:
             at = int(rng.integers(0, length - conserved_len + 1))
             seq[at:at + conserved_len] = conserved

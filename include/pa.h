@@ -8,6 +8,7 @@
  *
  *   pa_index_build           KmerReference.__init__ / _build_kmer_mapping   src/kmer.py:113-150
  *   pa_index_build_ex        the same, the align-side view deferred        src/kmer.py:113-133
+ *   pa_index_reduce          KmerReference._filter_similar_genomes (pruning)  src/kmer.py:232-263
  *   pa_index_prepare         (the deferred view, before the first align)
  *   pa_index_lookup          KmerReference.get_kmer_references / __getitem__ src/kmer.py:284-298
  *   pa_index_class_genomes   (genome set of a k-mer, i.e. the keys of kmers[kmer]) src/kmer.py:130
@@ -154,6 +155,14 @@ pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *ge
 #define PA_BUILD_DEFER_TILES 1u
 pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t *genome_off, uint32_t n_genomes,
                             int64_t k, uint32_t flags, void *stream, pa_index **out);
+/* Rebuild an index over some of its own genomes, in place: their 2-bit codes
+ * are gathered on the device (nothing is concatenated or uploaded again), the
+ * rest of the index is released and built anew -- the EXTSIM rebuild of
+ * KmerReference(filter_similar=True), where the reference deletes the dropped
+ * genomes from its dict (src/kmer.py:232-263).  keep: n_keep ascending genome
+ * numbers (< n_genomes); flags as pa_index_build_ex.  On failure the index
+ * holds nothing and may only be freed. */
+pa_status pa_index_reduce(pa_index *idx, const uint32_t *keep, uint32_t n_keep, uint32_t flags, void *stream);
 /* Make a deferred build's align-side view now (no-op otherwise); returns when
  * it is done. */
 pa_status pa_index_prepare(pa_index *idx, void *stream);

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy one scripts/measure.sh result into profiles/r03/: the bench line, its
+"""Copy one scripts/measure.sh result into profiles/<round>/ (ROUND, default r04): the bench line, its
 counter pass (per-kernel fabric bytes and SQ shares, JSON) and the rocprofv3
 kernel summary of the same workload, stamped with the git commit measured.
 
@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main(tag: str, name: str) -> None:
     src = os.path.join(REPO, "gpurun_out", f"ms_{tag}")
-    dst = os.path.join(REPO, "profiles", "r03")
+    dst = os.path.join(REPO, "profiles", os.environ.get("ROUND", "r04"))
     os.makedirs(dst, exist_ok=True)
     head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True, text=True).stdout.strip()
     with open(os.path.join(src, "args")) as f:
