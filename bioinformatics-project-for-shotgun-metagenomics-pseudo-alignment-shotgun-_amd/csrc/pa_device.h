@@ -351,6 +351,32 @@ __device__ __forceinline__ void bloom_word(uint64_t key, int k, uint32_t lg, uin
     const uint32_t mn = k == 31 ? key_minimizer_c<31>(key) : key_minimizer(key, k);
     w = (bloom_block(mn, lg) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
 }
+// The build-time filter of k_nb_build / k_nb_first (its own filter, freed
+// after): blocked by a minimizer of a cheaper order -- the 15-mer XOR a fixed
+// random pattern, one VALU op instead of mm_order's four -- since those kernels
+// compute ~93 of them per window and are VALU-bound as much as memory-bound.
+constexpr uint32_t kNbOrderXor = 0x2B7E1516u & 0x3FFFFFFFu;
+__device__ __forceinline__ uint32_t key_minimizer_nb(uint64_t key, int k) {
+    const int mm = k < 15 ? k : 15;
+    const uint64_t mmask = (1ull << (2 * mm)) - 1;
+    const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+    uint32_t best = ~0u;
+    if (k == 31) {
+#pragma unroll
+        for (int i = 0; i < 17; i++) {
+            const uint32_t x = (2 * i < 32 ? __builtin_amdgcn_alignbit(hi, lo, 2 * i) : hi >> (2 * i - 32)) & 0x3FFFFFFFu;
+            best = min(best, x ^ kNbOrderXor);
+        }
+        return best ^ kNbOrderXor;
+    }
+    for (int i = 0; i + mm <= k; i++) best = min(best, (uint32_t)((key >> (2 * i)) & mmask) ^ kNbOrderXor);
+    return best ^ kNbOrderXor;
+}
+__device__ __forceinline__ void bloom_word_nb(uint64_t key, int k, uint32_t lg, uint64_t &w, uint64_t &m) {
+    const uint32_t h = bloom_key_mix(key);
+    m = bloom_bits(h);
+    w = (bloom_block(key_minimizer_nb(key, k), lg) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
+}
 // The Bloom word of a two-word key (31 < k <= 63, the lane path of long k):
 // the block by a hash of the key (no minimizer runs: a read's windows off the
 // walk are probed one by one), the bits by its mix as above.

@@ -649,10 +649,6 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 // REVERSE COMPLEMENTS, for k_align_lane_rc's reverse-strand walk -- a read
 // window that is the reverse complement of the genome's k-mer but for one base
 // is then resolved by one bit, as a forward one by tile_nb.
-#ifndef PA_NB_CHUNK
-#define PA_NB_CHUNK 4
-#endif
-constexpr int kNbChunk = PA_NB_CHUNK;
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
                            const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
                            const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local,
@@ -687,53 +683,140 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
             }
             continue;
         }
-        // kNbChunk positions at a time: their 3 kNbChunk Bloom words are loaded
-        // together (one round trip, not one per position), then the few
-        // neighbours the filter lets through are probed position by position
-        auto nkey = [&](int j, int b) {
+        for (int j = 0; j < k; j++) {
             const int bs = 2 * (k - 1 - j);
             const uint64_t cj = (K >> bs) & 3;
-            const uint64_t v = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
-            return rc ? rc_key(v, k) : v;  // (tile_rcnb: the neighbour's reverse complement)
-        };
-        for (int j0 = 0; j0 < k; j0 += kNbChunk) {
-            uint32_t pass_bits = ~0u;  // bit 3 jj + b: neighbour (j0 + jj, b) may be present
+            uint64_t keys[3];
+            uint32_t cls3[3];
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                keys[b] = K ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
+                if (rc) keys[b] = rc_key(keys[b], k);  // (tile_rcnb: the neighbour's reverse complement)
+            }
+            uint32_t act = 7u;
             if (bloom) {  // surely absent neighbours are not probed
-                uint64_t wv[kNbChunk][3], bm[kNbChunk][3];
 #pragma unroll
-                for (int jj = 0; jj < kNbChunk; jj++)
+                for (int b = 0; b < 3; b++) {
+                    uint64_t wi, bm;
+                    bloom_word_nb(keys[b], k, bloom_lg, wi, bm);
+                    if ((bloom[wi] & bm) != bm) act &= ~(1u << b);
+                }
+                if (!act) continue;
+            }
+            const uint32_t f = probe_lines<3>(table, hc, keys, cls3, act);  // the substitutions together
 #pragma unroll
-                    for (int b = 0; b < 3; b++) {
-                        wv[jj][b] = 0, bm[jj][b] = 0;
-                        if (j0 + jj < k) {
+            for (int b = 0; b < 3; b++) {
+                if (!((f >> b) & 1u)) continue;
+                if (full)
+                    atomicOr(&nb[3 * (t + j) + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                else
+                    atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
+            }
+        }
+    }
+}
+
+// Pass 0 of k_nb_build in POSITION order: a wave takes 64 consecutive windows
+// and walks their 64 k (window, substituted position) pairs ordered by the
+// substituted position p, 64 pairs per step, instead of one window per lane
+// and one offset j per step.  The neighbours of the windows around one p
+// mostly share their minimizer -- the Bloom blocks are chosen by it -- so one
+// memory instruction of the wave touches ~7 distinct Bloom blocks instead of
+// ~40 (scripts/nb_model.py).  The pair of lane l at step s is the entry
+// s 64 + l of the block's decode table (LDS, by p then window); the window's
+// key comes from the lane that owns it (a cross-lane read).  Same bits as
+// k_nb_build's pass 0, set by the same atomics.  C5: 4.21 -> 3.55 s -- the
+// pass is bound by the minimizers' VALU (93 per window) as much as by its
+// Bloom lines; listing the filter's positives in LDS and probing them in one
+// batch per tile (occupancy 3 instead of 4) measured 4.56 s.
+#ifndef PA_NB_FIRST_ORDER
+#define PA_NB_FIRST_ORDER 1  // 0: pass 0 by k_nb_build (one window per lane; A/B)
+#endif
+constexpr bool kNbFirstOrder = PA_NB_FIRST_ORDER != 0;
+constexpr int kNbFirstChunk = 2;  // steps whose Bloom words are in flight together
+__global__ __launch_bounds__(256) void k_nb_first(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls,
+                                                  uint64_t n, int k, const Slot<1> *__restrict__ table, HomeCfg hc,
+                                                  uint32_t G, void *nb_out, int full,
+                                                  const uint32_t *__restrict__ class_genomes,
+                                                  const uint64_t *__restrict__ goff, int local,
+                                                  const uint64_t *__restrict__ bloom, uint32_t bloom_lg, int rc) {
+    __shared__ uint16_t pair_of[64 * 31];  // (p - t0) << 6 | window lane, p-major
+    unsigned long long *nb = (unsigned long long *)nb_out;
+    uint32_t *nb32 = (uint32_t *)nb_out;
+    for (int q = threadIdx.x; q < 64 + k - 1; q += blockDim.x) {  // one thread per p: its windows
+        const int lo = q - k + 1 > 0 ? q - k + 1 : 0, hi = q < 63 ? q : 63;
+        int base = 0;  // pairs of the positions before q
+        for (int d = 0; d < q; d++) base += (d < 63 ? d : 63) - (d - k + 1 > 0 ? d - k + 1 : 0) + 1;
+        for (int l = lo; l <= hi; l++) pair_of[base + (l - lo)] = (uint16_t)((q << 6) | l);
+    }
+    __syncthreads();
+    const int sh = 64 - 2 * k;
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t t0 = wave * 64; t0 < n; t0 += n_waves * 64) {
+        const uint64_t t = t0 + lane;
+        uint64_t K = 0;
+        bool first = false;
+        if (t < n && tile_cls[t] != NONE) {
+            K = get64_at(pk, 2 * t) >> sh;
+            Key<1> kk;
+            kk.w[0] = K;
+            uint64_t slot;
+            uint32_t cls, tpos;
+            if (table_find<1, true>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos))
+                first = first_pos(cls, tpos, G, class_genomes, goff, local != 0) == t;
+        }
+        const uint64_t fm = __ballot(first);
+        if (!fm) continue;
+        for (int s0 = 0; s0 < k; s0 += kNbFirstChunk) {
+            uint64_t key[kNbFirstChunk][3], wv[kNbFirstChunk][3], bm[kNbFirstChunk][3];
+            uint32_t j_of[kNbFirstChunk], p_of[kNbFirstChunk], pass_bits = 0;
+#pragma unroll
+            for (int c = 0; c < kNbFirstChunk; c++) {
+                const int s = s0 + c;
+                const uint32_t e = s < k ? pair_of[s * 64 + lane] : 0u;
+                const uint32_t l = e & 63, dp = e >> 6;
+                const uint64_t Kw = (uint64_t)__shfl((unsigned long long)K, (int)l);  // (all lanes take part)
+                const bool a = s < k && ((fm >> l) & 1ull);
+                const int j = (int)dp - (int)l;
+                j_of[c] = (uint32_t)j, p_of[c] = a ? dp : ~0u;
+#pragma unroll
+                for (int b = 0; b < 3; b++) {
+                    wv[c][b] = 0, bm[c][b] = 0, key[c][b] = 0;
+                    if (a) {
+                        const int bs = 2 * (k - 1 - j);
+                        const uint64_t cj = (Kw >> bs) & 3;
+                        const uint64_t v = Kw ^ ((cj ^ ((cj + 1 + b) & 3)) << bs);
+                        key[c][b] = rc ? rc_key(v, k) : v;
+                        if (bloom) {
                             uint64_t wi;
-                            bloom_word(nkey(j0 + jj, b), k, bloom_lg, wi, bm[jj][b]);
-                            wv[jj][b] = bloom[wi];
+                            bloom_word_nb(key[c][b], k, bloom_lg, wi, bm[c][b]);
+                            wv[c][b] = bloom[wi];
                         }
                     }
-                pass_bits = 0;
-#pragma unroll
-                for (int jj = 0; jj < kNbChunk; jj++)
-#pragma unroll
-                    for (int b = 0; b < 3; b++)
-                        if (j0 + jj < k && (wv[jj][b] & bm[jj][b]) == bm[jj][b]) pass_bits |= 1u << (3 * jj + b);
+                }
             }
-            for (int jj = 0; jj < kNbChunk && j0 + jj < k; jj++) {
-                const uint32_t act = (pass_bits >> (3 * jj)) & 7u;
-                if (!act) continue;
-                const int j = j0 + jj;
-                uint64_t keys[3];
-                uint32_t cls3[3];
 #pragma unroll
-                for (int b = 0; b < 3; b++) keys[b] = nkey(j, b);
-                const uint32_t f = probe_lines<3>(table, hc, keys, cls3, act);  // the substitutions together
+            for (int c = 0; c < kNbFirstChunk; c++)
+#pragma unroll
+                for (int b = 0; b < 3; b++)
+                    if (p_of[c] != ~0u && (!bloom || (wv[c][b] & bm[c][b]) == bm[c][b])) pass_bits |= 1u << (3 * c + b);
+#pragma unroll
+            for (int c = 0; c < kNbFirstChunk; c++) {
+                const uint32_t act = (pass_bits >> (3 * c)) & 7u;
+                if (!act) continue;
+                uint32_t cls3[3];
+                const uint32_t f = probe_lines<3>(table, hc, key[c], cls3, act);
+                const uint64_t p = t0 + p_of[c];
+                const int j = (int)j_of[c];
 #pragma unroll
                 for (int b = 0; b < 3; b++) {
                     if (!((f >> b) & 1u)) continue;
                     if (full)
-                        atomicOr(&nb[3 * (t + j) + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                        atomicOr(&nb[3 * p + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
                     else
-                        atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
+                        atomicOr(&nb32[3 * p + b], 1u << (k - 1 - j));
                 }
             }
         }
@@ -809,13 +892,17 @@ __global__ void k_nb_build2(const uint64_t *__restrict__ pk, const uint32_t *__r
 
 // The Bloom filter of the table's keys (pa_device.h bloom_word): one pass over
 // the slots, an atomic OR per key.
+template <bool NB = false>  // NB: the neighbour-bit build's own filter (bloom_word_nb)
 __global__ void k_bloom_build(const Slot<1> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg, int k) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
         const uint64_t key = table[i].key[0];
         if (key == EMPTY) continue;
         uint64_t w, m;
-        bloom_word(key, k, lg, w, m);
+        if (NB)
+            bloom_word_nb(key, k, lg, w, m);
+        else
+            bloom_word(key, k, lg, w, m);
         atomicOr((unsigned long long *)&bloom[w], (unsigned long long)m);
     }
 }
@@ -1259,7 +1346,7 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                 if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && pa::dev_malloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
                     B_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
                     phase_mark(bb_lg >= 30 ? "nb: Bloom alloc (lg >= 30)" : "nb: Bloom alloc (lg < 30)");
-                    hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                    hipLaunchKernelGGL(k_bloom_build<true>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
                                        dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, bb, bb_lg, k);
                 } else {
                     bb = nullptr;
@@ -1267,10 +1354,16 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
             }
             phase_mark("nb: build Bloom");
             for (int pass = 0; pass < 2; pass++) {
-                hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
-                                   st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                   idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
-                                   pass, bb, bb_lg, 0);
+                if (pass == 0 && kNbFirstOrder)
+                    hipLaunchKernelGGL(k_nb_first, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
+                                       st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                       idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
+                                       bb, bb_lg, 0);
+                else
+                    hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
+                                       st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                       idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
+                                       pass, bb, bb_lg, 0);
                 phase_mark(pass == 0 ? "nb: first occurrences" : "nb: copies");
             }
             // the reverse-complement neighbour bits (tile_rcnb, 12 B per base)
@@ -1281,10 +1374,16 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                 n * 12 <= fr_b / 4 * 3 && pa::dev_malloc(&idx->tile_rcnb, n * 12 + 64) == hipSuccess) {
                 B_HIP(hipMemsetAsync(idx->tile_rcnb, 0, n * 12 + 64, st));
                 for (int pass = 0; pass < 2; pass++)
-                    hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
-                                       st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                       (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff, idx->tpos_local,
-                                       pass, bb, bb_lg, 1);
+                    if (pass == 0 && kNbFirstOrder)
+                        hipLaunchKernelGGL(k_nb_first, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock),
+                                           0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,
+                                           G, (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff,
+                                           idx->tpos_local, bb, bb_lg, 1);
+                    else
+                        hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock),
+                                           0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,
+                                           G, (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff,
+                                           idx->tpos_local, pass, bb, bb_lg, 1);
                 idx->device_bytes += n * 12;
                 phase_mark("nb: reverse complements");
             }
@@ -1442,7 +1541,7 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                     B_HIP(pa::dev_malloc(&idx->bloom, (1ull << lg) * 8));
                     B_HIP(hipMemsetAsync(idx->bloom, 0, (1ull << lg) * 8, st));
                     if (NW == 1)
-                        hipLaunchKernelGGL(k_bloom_build, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                        hipLaunchKernelGGL(k_bloom_build<false>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
                                            dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg, k);
                     else
                         hipLaunchKernelGGL(k_bloom_build2, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--reads-per-gpu", type=int, default=None)
     ap.add_argument("--out", required=True)
     ap.add_argument("--timeout", type=int, default=300)
+    ap.add_argument("--kernels", default=None, help="regex on kernel names (default: the align kernels)")
+    ap.add_argument("--bench-args", default="", help="extra bench.py arguments")
     ap.add_argument("counters", nargs="+")
     args = ap.parse_args()
     tmp = tempfile.mkdtemp(prefix="pa_pmc_", dir="/tmp")
@@ -39,6 +41,16 @@ def main():
            "--steps", "2", "--warmup", "1"]
     if args.reads_per_gpu:
         cmd += ["--reads-per-gpu", str(args.reads_per_gpu)]
+    cmd += args.bench_args.split()
+    import re
+    pat = re.compile(args.kernels) if args.kernels else None
+
+    def short(name):
+        if pat is None:
+            return kernel_short_name(name)
+        m = re.search(r"\d+(k_[A-Za-z0-9_]+)", name)
+        base = m.group(1) if m else name
+        return base if pat.search(base) else None
     r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.PIPE,
                        stderr=subprocess.PIPE, text=True, timeout=args.timeout)
     if r.returncode:
@@ -51,15 +63,16 @@ def main():
             "join rocpd_info_pmc i on e.pmc_id = i.id join rocpd_event ev on e.event_id = ev.id "
             "join rocpd_kernel_dispatch d on d.event_id = ev.id "
             "join rocpd_info_kernel_symbol s on d.kernel_id = s.id group by s.kernel_name, i.name"):
-        short = kernel_short_name(name)
-        if short:
-            per.setdefault(short, {})[cname] = [float(v), int(n)]
+        sh = short(name)
+        if sh:
+            per.setdefault(sh, {})[cname] = [float(v), int(n)]
     for name, avg_ns, n in c.execute(
             "select s.kernel_name, avg(d.end - d.start), count(*) from rocpd_kernel_dispatch d "
             "join rocpd_info_kernel_symbol s on d.kernel_id = s.id group by s.kernel_name"):
-        short = kernel_short_name(name)
-        if short and short in per:
-            per[short]["trace_avg_ms"] = float(avg_ns) / 1e6
+        sh = short(name)
+        if sh and sh in per:
+            per[sh]["trace_avg_ms"] = float(avg_ns) / 1e6
+            per[sh]["launches"] = int(n)
     shutil.rmtree(tmp, ignore_errors=True)
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, "w") as f:
