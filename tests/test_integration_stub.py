@@ -111,3 +111,23 @@ def test_stub_dumpref_matches_reference(tmp_path):
     text = out.read_text() + tail[tail.index('"Kmers": 0') + len('"Kmers": 0'):] + "\n"
     gold = json.load(open(os.path.join(GOLD, "dumpref_cases.json")))["config1"]["config1"]
     assert hashlib.sha256(text.encode()).hexdigest() == gold["sha256"]
+
+
+def test_gunzip_snippet_inflates_like_gzip(tmp_path):
+    """INTEGRATION.md's pa_gz_inflate_file snippet, as written (host threads only,
+    no device): one ordinary gzip member of a few MB inflates to its bytes."""
+    import gzip
+    import numpy as np
+    ns = _stub_namespace()
+    with open(os.path.join(REPO, "INTEGRATION.md")) as f:
+        text = f.read()
+    g = re.search(r"```python\n(_L\.pa_gz_inflate_file\.argtypes.*?)```", text, re.S)
+    assert g, "INTEGRATION.md gunzip snippet not found"
+    exec(compile(g.group(1), "INTEGRATION.md:gunzip", "exec"), ns)
+    data = np.random.default_rng(3).integers(0, 4, 6_000_000, dtype=np.uint8)
+    raw = np.frombuffer(b"ACGT", np.uint8)[data].tobytes()
+    path = tmp_path / "r.fq.gz"
+    with gzip.open(path, "wb", compresslevel=6) as f:
+        f.write(raw)
+    out = ns["gunzip"](str(path), len(raw) + 1024, threads=4)
+    assert out.tobytes() == raw
