@@ -716,6 +716,42 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
     }
 }
 
+// Pass 1 of k_nb_build on its own (the probe loop of pass 0 holds 108 VGPRs;
+// this copy needs a third of them, so twice the waves hide its latency):
+// every occurrence t of a k-mer other than its first copies the first
+// occurrence's bits, k consecutive words per substitution (bit k - 1 - j of
+// word 3 (fo + j) + b to the same bit of word 3 (t + j) + b).
+__global__ void k_nb_copy(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
+                          const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
+                          const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local) {
+    unsigned long long *nb = (unsigned long long *)nb_out;
+    uint32_t *nb32 = (uint32_t *)nb_out;
+    const int sh = 64 - 2 * k;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+        if (tile_cls[t] == NONE) continue;
+        Key<1> kk;
+        kk.w[0] = get64_at(pk, 2 * t) >> sh;
+        uint64_t slot;
+        uint32_t cls, tpos;
+        if (!table_find<1, true>(table, hc.cap, kk, home_of<1>(kk, key_hash(kk), hc), slot, cls, tpos)) continue;
+        const uint64_t fo = first_pos(cls, tpos, G, class_genomes, goff, local != 0);
+        if (fo == t) continue;
+        for (int j = 0; j < k; j++) {
+#pragma unroll
+            for (int b = 0; b < 3; b++) {
+                if (full) {
+                    const unsigned long long m = nb[3 * (fo + j) + b] & (0x100000001ull << (k - 1 - j));
+                    if (m) atomicOr(&nb[3 * (t + j) + b], m);
+                } else {
+                    const uint32_t m = nb32[3 * (fo + j) + b] & (1u << (k - 1 - j));
+                    if (m) atomicOr(&nb32[3 * (t + j) + b], m);
+                }
+            }
+        }
+    }
+}
+
 // Pass 0 of k_nb_build in POSITION order: a wave takes 64 consecutive windows
 // and walks their 64 k (window, substituted position) pairs ordered by the
 // substituted position p, 64 pairs per step, instead of one window per lane
@@ -1359,6 +1395,10 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                                        st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
                                        idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
                                        bb, bb_lg, 0);
+                else if (pass == 1)
+                    hipLaunchKernelGGL(k_nb_copy, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
+                                       st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
+                                       idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local);
                 else
                     hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
                                        st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
@@ -1379,6 +1419,11 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                                            0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,
                                            G, (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff,
                                            idx->tpos_local, bb, bb_lg, 1);
+                    else if (pass == 1)
+                        hipLaunchKernelGGL(k_nb_copy, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock),
+                                           0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,
+                                           G, (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff,
+                                           idx->tpos_local);
                     else
                         hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock),
                                            0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,

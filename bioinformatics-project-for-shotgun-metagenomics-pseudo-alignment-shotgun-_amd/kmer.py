@@ -223,8 +223,8 @@ class KmerReference:
         # the align-side view (tiles, neighbour bits) is made at the first align:
         # an index that EXTSIM then rebuilds from the kept genomes never needs it
         packed, self._packed = getattr(self, "_packed", None), None  # (only for the first build)
-        self._index = N.Index([g["genome"] for g in self.genomes], self.kmer_len, device=self._device,
-                              defer_tiles=True, packed=packed)
+        self._index = N.Index(None if packed is not None else [g["genome"] for g in self.genomes], self.kmer_len,
+                              device=self._device, defer_tiles=True, packed=packed)
         self._view: Optional[Dict[str, Dict[Record, Set[int]]]] = None
 
     @property

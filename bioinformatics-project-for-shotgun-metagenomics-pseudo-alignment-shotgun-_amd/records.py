@@ -60,6 +60,21 @@ class UnparsedDataError(Exception):
         super().__init__(message)
 
 
+class _LazyText:
+    """ASCII bytes of a section not yet decoded into a str (a slice of the
+    native parser's column): a genome is decoded on first access, so the
+    dumpalign CLI -- whose index is built from the parser's packed bytes --
+    never decodes 100 MB of genome text it does not read."""
+
+    __slots__ = ("buf", "lo", "hi")
+
+    def __init__(self, buf, lo: int, hi: int) -> None:
+        self.buf, self.lo, self.hi = buf, lo, hi
+
+    def text(self) -> str:
+        return self.buf[self.lo:self.hi].tobytes().decode("ascii")
+
+
 class Record:
     """A parsed record: ``identifier`` is the first section's data; sections by name."""
 
@@ -76,15 +91,23 @@ class Record:
             self._sections[s.name] = s.data
 
     def __getitem__(self, key: str) -> str:
-        return self._sections[key]
+        v = self._sections[key]
+        if type(v) is _LazyText:
+            v = self._sections[key] = v.text()
+        return v
+
+    def _materialize(self) -> Dict[str, str]:
+        for k in self._sections:
+            self[k]
+        return self._sections
 
     def __str__(self) -> str:
-        return "\n".join(f"{k}: {v}" for k, v in self._sections.items())
+        return "\n".join(f"{k}: {v}" for k, v in self._materialize().items())
 
     __repr__ = __str__
 
     def __getstate__(self):
-        return {"identifier": self.identifier, "sections": self._sections}
+        return {"identifier": self.identifier, "sections": self._materialize()}
 
     def __setstate__(self, state):
         if "_Record__sections" in state:  # pickled by the reference (src/records.py:74-90: name-mangled dict)
@@ -159,7 +182,7 @@ class FASTARecordContainer(RecordContainer):
         these records is built from them without concatenating again."""
         seq, off = cols.seq, cols.off
         for i, name in enumerate(cols.names):
-            genome = seq[int(off[i]):int(off[i + 1])].tobytes().decode("ascii")
+            genome = _LazyText(seq, int(off[i]), int(off[i + 1]))  # (decoded on first access)
             self._records.append(Record([Section("description", name), Section("genome", genome)]))
         self._packed = (seq, np.asarray(off, dtype=np.uint64), list(self._records))
 
