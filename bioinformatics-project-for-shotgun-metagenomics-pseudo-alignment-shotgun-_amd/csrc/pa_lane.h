@@ -686,16 +686,6 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
     const uint32_t gr = (uint32_t)(2 * Ac & 63);
     uint64_t gw[kLaneWords + 1], pa3[3], pb3[3];
     lane_blocks<true>(a, Ac, len, gw, pa3, pb3);
-    // --max-genomes >= 2: the plane "set size > mg" of this mg (k_tile_big),
-    // loaded with the walk blocks, not after the walk (one round trip less;
-    // the mg variant runs at 3 waves per SIMD and has the registers)
-    uint64_t bg3[3] = {0, 0, 0};
-    if constexpr (MG) {
-        if (a.prm.mg >= 2) {
-            const uint64_t *bp = a.tile_big + (Ac >> 6);
-            bg3[0] = bp[0], bg3[1] = bp[1], bg3[2] = bp[2];
-        }
-    }
     const uint32_t g = S.acls < a.G ? S.acls : genome_of(a.goff, a.gblk, atp);
     S.g = g;
     const uint64_t gs = a.goff[g], ge = a.goff[g + 1];
@@ -888,8 +878,9 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
         } else if (mg == 1) {
             big0 = walked0 & ~spec0;
             big1 = walked1 & ~spec1;
-        } else {  // the plane "set size > mg" of this mg (bg3, loaded with the walk blocks)
-            const uint64_t b0 = bg3[0], b1 = bg3[1], b2 = bg3[2];
+        } else {  // the plane "set size > mg" of this mg (k_tile_big)
+            const uint64_t *bp = a.tile_big + (Ac >> 6);
+            const uint64_t b0 = bp[0], b1 = bp[1], b2 = bp[2];
             big0 = walked0 & ~spec0 & (fr ? (b0 >> fr) | (b1 << (64 - fr)) : b0);
             big1 = walked1 & ~spec1 & (fr ? (b1 >> fr) | (b2 << (64 - fr)) : b1);
         }
