@@ -33,12 +33,50 @@ from typing import List, Optional
 
 _T0 = time.perf_counter()
 
+_EARLY_PREFETCH = None  # (path, native handle) of a FASTQ prefetch started at entry
+
+
+def _early_reads_path(argv: List[str]) -> Optional[str]:
+    """The --reads file of a `-t dumpalign` command line, read off argv before
+    argparse and the heavy imports (a guess: main() still validates everything
+    and ignores the early prefetch unless it names the same file)."""
+    task = reads = None
+    for i, a in enumerate(argv[:-1]):
+        if a in ("-t", "--task"):
+            task = argv[i + 1]
+        elif a == "--reads":
+            reads = argv[i + 1]
+    return reads if task == "dumpalign" else None
+
+
 if __name__ == "__main__":  # the HIP runtime starts on a native thread while the modules below import
     try:
         import ctypes
         _here = os.path.dirname(os.path.abspath(__file__))
-        ctypes.CDLL(os.environ.get("PA_LIBRARY", os.path.join(_here, "libpa.so"))).pa_runtime_start(
-            int(os.environ.get("PA_DEVICE", os.environ.get("LOCAL_RANK", "0"))))
+        _lib = ctypes.CDLL(os.environ.get("PA_LIBRARY", os.path.join(_here, "libpa.so")))
+        _dev = int(os.environ.get("PA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        _lib.pa_runtime_start(_dev)
+        # a plain FASTQ's copy into device memory starts now too (pa_fastq_prefetch_start
+        # makes no HIP call on this thread): it overlaps the imports, not only the build
+        _r = _early_reads_path(sys.argv[1:])
+        if (_r and not _r.endswith(".gz") and os.path.isfile(_r) and os.environ.get("PA_STREAM", "1") != "0"
+                and os.environ.get("PA_PREFETCH", "1") != "0" and os.environ.get("PA_EARLY_PREFETCH", "1") != "0"):
+            _n = len(os.sched_getaffinity(0))
+            _omp = os.environ.get("OMP_NUM_THREADS", "")
+            _thr = os.environ.get("PA_INGEST_THREADS", "")
+            _threads = int(_thr) if _thr.isdigit() and int(_thr) > 0 else \
+                max(1, min(min(_n, int(_omp)) if _omp.isdigit() and int(_omp) > 0 else _n, 16))
+            _h = ctypes.c_void_p()
+            _lib.pa_fastq_prefetch_start.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                                     ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+            if _lib.pa_fastq_prefetch_start(os.fsencode(_r), _dev, _threads, 0, ctypes.byref(_h)) == 0 and _h.value:
+                _EARLY_PREFETCH = (os.path.abspath(_r), _h)
+
+                def _free_early_prefetch():  # (an early exit: argument errors, another task)
+                    if _EARLY_PREFETCH is not None:
+                        _lib.pa_fastq_prefetch_free.argtypes = [ctypes.c_void_p]
+                        _lib.pa_fastq_prefetch_free(_EARLY_PREFETCH[1])
+                atexit.register(_free_early_prefetch)
     except (OSError, AttributeError, ValueError):
         pass  # (no library: pa_native raises at the first device call)
 
@@ -113,7 +151,13 @@ def _prefetch_reads(reads_file: str):
         return None
     try:
         import pa_native as N
-        pf = N.FastqPrefetch(reads_file)
+        global _EARLY_PREFETCH
+        early = _EARLY_PREFETCH
+        if early is not None and early[0] == os.path.abspath(reads_file):  # started at entry
+            _EARLY_PREFETCH = None  # (owned by pf from here on)
+            pf = N.FastqPrefetch.adopt(early[1], reads_file)
+        else:
+            pf = N.FastqPrefetch(reads_file)
     except Exception:  # (no device, unreadable file: the exact path reports it in the reference's order)
         return None
     atexit.register(pf.close)

@@ -742,6 +742,16 @@ class FastqPrefetch:
         _check(lib().pa_fastq_prefetch_start(os.fsencode(path), self.device, int(threads or ingest_threads()),
                                              int(window_bytes), ctypes.byref(self.handle)))
 
+    @classmethod
+    def adopt(cls, handle, path: str) -> "FastqPrefetch":
+        """A prefetch already started through the C ABI (main.py starts one at
+        entry, before the imports): this object owns and frees it."""
+        self = cls.__new__(cls)
+        self.handle = P(handle.value if hasattr(handle, "value") else handle)
+        self.path = path
+        self.device = default_device()
+        return self
+
     def close(self) -> None:
         if self.handle:
             lib().pa_fastq_prefetch_free(self.handle)
