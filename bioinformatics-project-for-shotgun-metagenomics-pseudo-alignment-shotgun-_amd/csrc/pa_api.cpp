@@ -78,7 +78,8 @@ pa_status pa_runtime_start(int32_t device) {
     if (g_runtime_starter.th.joinable()) return PA_OK;
     g_runtime_starter.th = std::thread([device] {
         const auto t0 = std::chrono::steady_clock::now();
-        if (hipSetDevice(device) == hipSuccess && hipFree(nullptr) == hipSuccess) {  // (creates the context)
+        const char *w = std::getenv("PA_RUNTIME_WARM");  // 0: the context only (A/B)
+        if (hipSetDevice(device) == hipSuccess && hipFree(nullptr) == hipSuccess && !(w && w[0] == '0')) {
             pa::warm_index(nullptr);  // the code objects too, not at the first real launch
             pa::warm_align(nullptr);
             pa::warm_fastq(nullptr);
