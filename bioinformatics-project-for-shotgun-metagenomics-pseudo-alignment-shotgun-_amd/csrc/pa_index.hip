@@ -540,20 +540,38 @@ __global__ void k_tile_pack(const uint8_t *__restrict__ codes, uint64_t n, uint6
     }
 }
 
-// Class of the k-mer starting at every window of one genome (tile_cls is
+// Class of the k-mer starting at every genome window (tile_cls is
 // pre-filled with NONE, which stays at windows with non-ACGT bases), and the
 // key's first occurrence: slot.tpos = the smallest position of the key inside
 // its first genome (FASTA order: the specific genome, or the first of its set),
 // concatenated while the reference is < 2^32 bases, else genome-local so that
 // references of any total length tile (the concatenated position is then
 // goff[first genome] + tpos; pad::first_pos).
+// Tile classes and first occurrences (k_tile_cls_all), every genome in ONE
+// launch (they do not depend on the genomes' order): thread T takes chunk T -
+// tstart[g] of genome g, the last genome with tstart[g] <= T (tstart: the
+// genomes' first chunks, prefix sums of ceil(windows / wpt)); windows never
+// cross genomes.  C5's 1200 launches of 0.23 ms became one.
 template <int NW>
-__global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, uint64_t nwin, int k, uint64_t mask0,
-                           Slot<NW> *table, HomeCfg hc, uint32_t *tile_cls, uint32_t g, uint32_t G,
-                           const uint32_t *__restrict__ class_genomes, int local, int wpt) {
-    uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
+__global__ void k_tile_cls_all(const uint8_t *__restrict__ codes, const uint64_t *__restrict__ goff,
+                               const uint64_t *__restrict__ tstart, uint32_t G, int k, uint64_t mask0,
+                               Slot<NW> *table, HomeCfg hc, uint32_t *tile_cls,
+                               const uint32_t *__restrict__ class_genomes, int local, int wpt) {
+    const uint64_t T = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (T >= tstart[G]) return;
+    uint32_t lo = 0, hi = G;  // tstart[lo] <= T < tstart[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tstart[mid] <= T)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    const uint32_t g = lo;
+    const uint64_t gstart = goff[g], nwin = goff[g + 1] - gstart - (uint64_t)k + 1;
+    const uint64_t w0 = (T - tstart[g]) * (uint64_t)wpt;
     if (w0 >= nwin) return;
-    uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
+    const uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
     const uint8_t *s = codes + gstart + w0;
     Key<NW> key;
 #pragma unroll
@@ -575,7 +593,7 @@ __global__ void k_tile_cls(const uint8_t *__restrict__ codes, uint64_t gstart, u
             tile_cls[gstart + w] = cls;
             if (local) {
                 const uint32_t fg = cls < G ? cls : class_genomes[cls - G + 1];
-                if (fg == g && tpos > (uint32_t)w) atomicMin(&table[slot].tpos, (uint32_t)w);  // (stale: an extra atomic)
+                if (fg == g && tpos > (uint32_t)w) atomicMin(&table[slot].tpos, (uint32_t)w);
             } else if (tpos > (uint32_t)(gstart + w)) {
                 atomicMin(&table[slot].tpos, (uint32_t)(gstart + w));
             }
@@ -1508,13 +1526,24 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
         B_HIP(hipMemsetAsync(idx->tile_cls, 0xFF, n * 4, st));
         hipLaunchKernelGGL(k_tile_pack, dim3(grid_for(nwords) > 65536 ? 65536 : grid_for(nwords)), dim3(kBlock), 0, st,
                            idx->codes, n, idx->tile_pk, nwords);
-        for (uint32_t g = 0; g < G; g++) {
-            uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
-            if ((uint64_t)k > len) continue;
-            uint64_t nwin = len - k + 1;
-            hipLaunchKernelGGL(k_tile_cls<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
-                               idx->codes, idx->h_goff[g], nwin, k, mask0, table, idx->home, idx->tile_cls, g, G,
-                               idx->class_genomes, idx->tpos_local, wpt);
+        {  // every genome's chunks in one launch (k_tile_cls_all)
+            std::vector<uint64_t> ts(G + 1, 0);
+            for (uint32_t g = 0; g < G; g++) {
+                const uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
+                ts[g + 1] = ts[g] + ((uint64_t)k > len ? 0 : (len - k + 1 + wpt - 1) / wpt);
+            }
+            uint64_t *d_ts = nullptr;
+            B_HIP(pa::dev_malloc(&d_ts, (G + 1) * 8));
+            hipError_t e = hipMemcpyAsync(d_ts, ts.data(), (G + 1) * 8, hipMemcpyHostToDevice, st);
+            if (e == hipSuccess && ts[G] > 0) {
+                hipLaunchKernelGGL(k_tile_cls_all<NW>, dim3(grid_for(ts[G])), dim3(kBlock), 0, st, idx->codes, idx->goff,
+                                   d_ts, G, k, mask0, table, idx->home, idx->tile_cls, idx->class_genomes,
+                                   idx->tpos_local, wpt);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipStreamSynchronize(st);  // (d_ts is freed below)
+            pa::dev_free(d_ts);
+            B_HIP(e);
         }
         phase_mark("tile classes");
         {  // genome of every 2^16-th position: genome_of is then one or two goff steps
