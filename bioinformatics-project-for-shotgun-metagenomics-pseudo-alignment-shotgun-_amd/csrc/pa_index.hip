@@ -1959,29 +1959,75 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
 // (KmerReference._filter_similar_genomes; the reference prunes its dict,
 // src/kmer.py:232-263) without concatenating and uploading the kept genomes
 // again: C5's 1200 of 2000 genomes, 4.8 GB.
+// The kept genomes' codes are gathered into a fresh buffer while the old index
+// is still whole (an error leaves it usable); when that buffer does not fit
+// beside the old index, they are compacted inside the old codes buffer instead
+// (sel ascending: every run moves towards the front), through a small bounce
+// buffer where a run's source and destination overlap, so the peak is never
+// above the old index.
 pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream_t st, bool defer_tiles) {
     std::vector<uint64_t> goff(n + 1, 0);
     for (uint32_t i = 0; i < n; i++) goff[i + 1] = goff[i] + (idx->h_goff[sel[i] + 1] - idx->h_goff[sel[i]]);
-    uint8_t *codes = nullptr;
-    PA_HIP(pa::dev_malloc(&codes, std::max<uint64_t>(goff[n], 1)));
-    hipError_t e = hipSuccess;
-    for (uint32_t i = 0; i < n && e == hipSuccess;) {
+    // runs of consecutive kept genomes: (destination, source, length)
+    struct Run {
+        uint64_t to, from, len;
+    };
+    std::vector<Run> runs;
+    for (uint32_t i = 0; i < n;) {
         uint32_t j = i;
         while (j + 1 < n && sel[j + 1] == sel[j] + 1) j++;
         const uint64_t from = idx->h_goff[sel[i]], len = idx->h_goff[sel[j] + 1] - from;
-        if (len) e = hipMemcpyAsync(codes + goff[i], idx->codes + from, len, hipMemcpyDeviceToDevice, st);
+        if (len) runs.push_back({goff[i], from, len});
         i = j + 1;
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) {
+    uint8_t *codes = nullptr;
+    hipError_t e = pa::dev_malloc(&codes, std::max<uint64_t>(goff[n], 1));
+    const char *inplace = std::getenv("PA_REDUCE_INPLACE");  // tests: force the in-place path
+    if (e == hipSuccess && inplace && inplace[0] == '1') {
         pa::dev_free(codes);
+        codes = nullptr;
+        e = hipErrorOutOfMemory;
+    }
+    if (e == hipSuccess) {
+        for (size_t r = 0; r < runs.size() && e == hipSuccess; r++)
+            e = hipMemcpyAsync(codes + runs[r].to, idx->codes + runs[r].from, runs[r].len, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            pa::dev_free(codes);
+            PA_HIP(e);
+        }
+    } else if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        codes = idx->codes;
+        constexpr uint64_t kBounce = 64ull << 20;
+        uint8_t *bounce = nullptr;
+        for (size_t r = 0; r < runs.size(); r++) {
+            const Run &u = runs[r];
+            if (u.to == u.from) continue;
+            if (u.to + u.len <= u.from) {  // no overlap: one copy
+                PA_HIP(hipMemcpyAsync(codes + u.to, codes + u.from, u.len, hipMemcpyDeviceToDevice, st));
+                continue;
+            }
+            if (!bounce) PA_HIP(pa::dev_malloc(&bounce, kBounce));
+            for (uint64_t o = 0; o < u.len; o += kBounce) {  // front to back: a chunk's source is read before it is overwritten
+                const uint64_t c = std::min(kBounce, u.len - o);
+                PA_HIP(hipMemcpyAsync(bounce, codes + u.from + o, c, hipMemcpyDeviceToDevice, st));
+                PA_HIP(hipMemcpyAsync(codes + u.to + o, bounce, c, hipMemcpyDeviceToDevice, st));
+            }
+        }
+        PA_HIP(hipStreamSynchronize(st));
+        pa::dev_free(bounce);
+        idx->codes = nullptr;  // (kept: the rebuild's codes)
+    } else {
         PA_HIP(e);
     }
     const int64_t k = idx->k;
     const int device = idx->device;
+    const bool profile = idx->profile;  // (set through the C ABI: kept across the rebuild)
     index_release(idx);
     *idx = pa_index();
     idx->device = device;
+    idx->profile = profile;
     return index_build(idx, nullptr, goff.data(), n, k, st, defer_tiles, codes);
 }
 

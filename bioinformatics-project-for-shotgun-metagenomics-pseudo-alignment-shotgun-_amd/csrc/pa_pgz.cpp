@@ -700,8 +700,10 @@ void pgz_close(Pgz *g) { delete g; }
 
 }  // namespace pa
 
-// Test / measurement entry (not part of include/pa.h): inflate a whole gzip
-// file with `threads` threads into dst (cap bytes); the text length in *n.
+// pa_gz_inflate_file (include/pa.h): inflate a whole gzip file with `threads`
+// threads into dst (cap bytes); the text length in *n.  A text of exactly cap
+// bytes fits: at tot == cap one more read into a scratch byte tells the end
+// from more text (the zlib path sets its end flag only after a read of 0 bytes).
 extern "C" pa_status pa_gz_inflate_file(const char *path, int threads, uint8_t *dst, uint64_t cap, uint64_t *n) {
     pa::Gz *g = nullptr;
     const pa_status s = pa::gz_open(path, threads, &g);
@@ -711,6 +713,14 @@ extern "C" pa_status pa_gz_inflate_file(const char *path, int threads, uint8_t *
     while (!eof) {
         uint64_t got = 0;
         if (tot >= cap) {
+            uint8_t probe = 0;
+            // (BGZF refuses a 1-byte window while a member is left: PA_EINVAL, more text)
+            const pa_status r = pa::gz_read(g, &probe, 1, &got, &eof);
+            if (r != PA_OK && r != PA_EINVAL) {
+                pa::gz_close(g);
+                return r;
+            }
+            if (r == PA_OK && got == 0 && eof) break;
             pa::gz_close(g);
             pa::set_error("pa_gz_inflate_file: buffer too small");
             return PA_EINVAL;

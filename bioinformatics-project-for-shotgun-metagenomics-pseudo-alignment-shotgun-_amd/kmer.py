@@ -242,12 +242,13 @@ class KmerReference:
         keep, info = extsim_filter(self._index, [g.identifier for g in self.genomes],
                                    [len(g["genome"]) for g in self.genomes], similarity_threshold)
         if len(keep) != len({g.identifier for g in self.genomes}):
-            self._all_genomes = self.genomes
             sel = [i for i, g in enumerate(self.genomes) if g.identifier in keep]
-            self.genomes = [self.genomes[i] for i in sel]
             # pruning dropped genomes == building from the kept ones: in place,
-            # from their codes already on the device (pa_index_reduce)
+            # from their codes already on the device (pa_index_reduce); the
+            # genome lists change only once that succeeded
             self._index.reduce(sel)
+            self._all_genomes = self.genomes
+            self.genomes = [self.genomes[i] for i in sel]
             self._view = None
         self.similarity_info = info
 

@@ -36,17 +36,45 @@ _T0 = time.perf_counter()
 _EARLY_PREFETCH = None  # (path, native handle) of a FASTQ prefetch started at entry
 
 
+_FQ_PLAIN_EXT = ".fq"  # (FASTAQFile.EXTENSIONS without ".fq.gz": the file types the prefetch takes)
+
+
 def _early_reads_path(argv: List[str]) -> Optional[str]:
     """The --reads file of a `-t dumpalign` command line, read off argv before
-    argparse and the heavy imports (a guess: main() still validates everything
-    and ignores the early prefetch unless it names the same file)."""
+    argparse and the heavy imports (every spelling argparse accepts: `-t X`,
+    `-tX`, `--task X`, `--task=X`, `--reads X`, `--reads=X`), when it is a file
+    the later prefetch would take too (_prefetch_reads: a plain `.fq`, streaming
+    and prefetch on).  A guess: main() still validates everything and ignores
+    the early prefetch unless it names the same file."""
     task = reads = None
-    for i, a in enumerate(argv[:-1]):
+    i = 0
+    while i < len(argv):
+        a = argv[i]
+        nxt = argv[i + 1] if i + 1 < len(argv) else None
         if a in ("-t", "--task"):
-            task = argv[i + 1]
-        elif a == "--reads":
-            reads = argv[i + 1]
-    return reads if task == "dumpalign" else None
+            task, i = nxt, i + 2
+            continue
+        if a == "--reads":
+            reads, i = nxt, i + 2
+            continue
+        if a.startswith("--task="):
+            task = a.split("=", 1)[1]
+        elif a.startswith("-t") and not a.startswith("--") and len(a) > 2:
+            task = a[2:]
+        elif a.startswith("--reads="):
+            reads = a.split("=", 1)[1]
+        i += 1
+    if task != "dumpalign" or not reads or not reads.endswith(_FQ_PLAIN_EXT):
+        return None
+    if os.environ.get("PA_STREAM", "1") == "0" or os.environ.get("PA_PREFETCH", "1") == "0":
+        return None
+    return reads
+
+
+def _stream_window() -> int:
+    """PA_STREAM_WINDOW (bytes; 0: the library's default), as pa_native reads it."""
+    env = os.environ.get("PA_STREAM_WINDOW")
+    return int(env) if env and env.isdigit() else 0
 
 
 if __name__ == "__main__":  # the HIP runtime starts on a native thread while the modules below import
@@ -59,8 +87,7 @@ if __name__ == "__main__":  # the HIP runtime starts on a native thread while th
         # a plain FASTQ's copy into device memory starts now too (pa_fastq_prefetch_start
         # makes no HIP call on this thread): it overlaps the imports, not only the build
         _r = _early_reads_path(sys.argv[1:])
-        if (_r and not _r.endswith(".gz") and os.path.isfile(_r) and os.environ.get("PA_STREAM", "1") != "0"
-                and os.environ.get("PA_PREFETCH", "1") != "0" and os.environ.get("PA_EARLY_PREFETCH", "1") != "0"):
+        if _r and os.path.isfile(_r) and os.environ.get("PA_EARLY_PREFETCH", "1") != "0":
             _n = len(os.sched_getaffinity(0))
             _omp = os.environ.get("OMP_NUM_THREADS", "")
             _thr = os.environ.get("PA_INGEST_THREADS", "")
@@ -69,7 +96,8 @@ if __name__ == "__main__":  # the HIP runtime starts on a native thread while th
             _h = ctypes.c_void_p()
             _lib.pa_fastq_prefetch_start.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
                                                      ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
-            if _lib.pa_fastq_prefetch_start(os.fsencode(_r), _dev, _threads, 0, ctypes.byref(_h)) == 0 and _h.value:
+            if (_lib.pa_fastq_prefetch_start(os.fsencode(_r), _dev, _threads, _stream_window(), ctypes.byref(_h)) == 0
+                    and _h.value):
                 _EARLY_PREFETCH = (os.path.abspath(_r), _h)
 
                 def _free_early_prefetch():  # (an early exit: argument errors, another task)
@@ -252,8 +280,11 @@ def _run(args: argparse.Namespace) -> None:
         else:
             validate_file_readable(args.genomefile, "Genome FASTA")
             ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
-            if args.referencefile:
-                ref.save(args.referencefile)
+            # saved unconditionally, as src/main.py:370 does: without -r that is
+            # gzip.open(None), a TypeError the reference does not catch
+            # (src/main.py:401), so the command ends with a traceback and exit
+            # status 1 before any alignment is written -- reproduced, not fixed
+            ref.save(args.referencefile)
         create_alignment_from_reference(ref, args.reads, *filt, per_read=True).save(args.alignfile)
     elif args.task == "dumpalign":
         if args.referencefile and args.reads:

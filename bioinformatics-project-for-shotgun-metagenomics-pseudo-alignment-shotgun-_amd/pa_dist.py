@@ -35,6 +35,12 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def default_backend(cuda_available: bool) -> str:
+    """The backend of a multi-rank job: "nccl" (RCCL over xGMI on ROCm) on a
+    GPU node, "gloo" for CPU rehearsals."""
+    return "nccl" if cuda_available else "gloo"
+
+
 def init_process_group(backend: Optional[str] = None):
     """Initialise torch.distributed from the torchrun environment (127.0.0.1 rendezvous)."""
     import torch
@@ -43,7 +49,7 @@ def init_process_group(backend: Optional[str] = None):
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = default_backend(torch.cuda.is_available())
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world)

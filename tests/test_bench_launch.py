@@ -106,6 +106,44 @@ def test_default_is_the_north_star_job():
     assert sum(n for _, n in (bench.rank_reads(cfg, r, 8) for r in range(8))) == 500_000_000
 
 
+def test_eight_gpu_plan_is_the_north_star_over_rccl():
+    """`bench.py --gpus 8` with the default config plans the north-star job:
+    8 ranks x 62.5M reads (500M, contiguous global ranges), the torch
+    reduction, and the nccl (RCCL) backend on a GPU node -- checked through the
+    same job_plan the bench runs, and through `--plan` (no device call)."""
+    sys.path.insert(0, REPO)
+    import bench
+    p = bench.job_plan("c4", 8, "torch", cuda_available=True)
+    assert p["world"] == 8 and p["reduce"] == "torch" and p["backend"] == "nccl"
+    assert [r["n"] for r in p["rank_reads"]] == [62_500_000] * 8
+    assert [r["first"] for r in p["rank_reads"]] == [62_500_000 * i for i in range(8)]
+    assert p["job_reads_per_step"] == 500_000_000
+    assert bench.job_plan("c4", 2, "torch", cuda_available=False)["backend"] == "gloo"
+    assert bench.job_plan("c4", 1, "torch", cuda_available=True)["backend"] is None
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--plan"], env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    q = json.loads(r.stdout.strip().splitlines()[-1])
+    assert q["world"] == 8 and q["config"] == "c4" and q["job_reads_per_step"] == 500_000_000
+    assert q["reduce"] == "torch" and q["backend"] in ("nccl", "gloo")  # (gloo here: this container has no GPU)
+
+
+def test_counter_child_error_lines():
+    """The counter child's failure keeps its own message: the profiler's log
+    lines after it are dropped (a child's error was lost)."""
+    sys.path.insert(0, REPO)
+    import bench
+    err = ("Traceback (most recent call last):\n  File \"bench.py\", line 1, in <module>\n"
+           "pa_native.PaError: out of device memory (table)\n"
+           "W20261017 12:53:42.739491 130735486295552 simple_timer.cpp:55] [rocprofv3] output generation :: 1.7 sec\n"
+           "I20261017 12:53:42.739556 130735486295552 simple_timer.cpp:55] [rocprofv3] tool finalization :: 1.7 sec\n")
+    s = bench.child_error_lines(err)
+    assert "out of device memory" in s and "rocprofv3" not in s and "Traceback" in s
+
+
 def test_kernel_short_names():
     """Counter rows are matched to kernels by their own mangled names (the
     length prefix keeps k_align_lane apart from k_align_lane_na)."""

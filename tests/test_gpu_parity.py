@@ -157,6 +157,26 @@ def test_config1_cli_stdout():
         assert r.stdout == case["stdout"], case["flags"]
 
 
+def test_align_without_reference_file_fails_like_the_reference(tmp_path):
+    """`-t align -g -k --reads -a` without -r: the reference saves its k-mer
+    reference to None (src/main.py:366-372), gzip.open raises a TypeError the
+    CLI does not catch (src/main.py:401), and the process exits with status 1
+    and a traceback before the alignment file is written."""
+    aln = tmp_path / "out.aln"
+    cmd = [sys.executable, os.path.join(PKG, "main.py"), "-t", "align", "-g", os.path.join(GOLD, "config1.fa"),
+           "-k", "21", "--reads", os.path.join(GOLD, "config1.fq"), "-a", str(aln)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 1, r.stderr
+    assert "Traceback" in r.stderr and "TypeError" in r.stderr
+    assert not aln.exists()
+    # with -r the same command writes both files
+    kdb = tmp_path / "ref.kdb"
+    r = subprocess.run(cmd + ["-r", str(kdb)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert aln.exists() and kdb.exists()
+
+
 @pytest.mark.parametrize("case", load("extsim_cases.json"), ids=lambda c: c["name"])
 def test_extsim_golden(case):
     from kmer import KmerReference, PseudoAlignment

@@ -20,8 +20,13 @@ def _fetch(index, reads, prm):
     return out
 
 
-@pytest.mark.parametrize("k", [31, 45, 75])
-def test_reduce_equals_build_of_kept(k):
+@pytest.mark.parametrize("k,inplace", [(31, False), (45, False), (75, False), (31, True)])
+def test_reduce_equals_build_of_kept(k, inplace, monkeypatch):
+    """inplace: the path taken when the gathered codes do not fit beside the
+    old index (PA_REDUCE_INPLACE=1 forces it): the kept runs compacted inside
+    the old codes buffer, overlapping ones through a bounce buffer."""
+    if inplace:
+        monkeypatch.setenv("PA_REDUCE_INPLACE", "1")
     gens = synth.family_genomes(12, 60_000, seed=5, family_size=4, sub_rate=0.01, conserved_len=800)
     sel = [0, 1, 3, 4, 5, 8, 11]
     red = N.Index(gens, k, defer_tiles=True)

@@ -81,3 +81,17 @@ def test_not_gzip_refused(tmp_path):
     p.write_bytes(b"@r\nACGT\n+\nIIII\n")
     with pytest.raises(N.PaError):
         N.gz_inflate_file(str(p), 1 << 20, threads=4)
+
+
+@pytest.mark.parametrize("pgz", ["1", "0"])
+def test_exact_capacity(tmp_path, monkeypatch, pgz):
+    """A text of exactly `cap` bytes fits (the zlib path knows its end only
+    after one more read), one byte more is refused as too large -- parallel
+    (PA_PGZ=1) and zlib (PA_PGZ=0) paths alike."""
+    monkeypatch.setenv("PA_PGZ", pgz)
+    t = _fastq(3000, 9)
+    p = tmp_path / "x.gz"
+    p.write_bytes(gzip.compress(t, 6))
+    assert N.gz_inflate_file(str(p), len(t), threads=4) == t
+    with pytest.raises((N.PaError, ValueError)):
+        N.gz_inflate_file(str(p), len(t) - 1, threads=4)

@@ -363,3 +363,27 @@ def test_native_parse_file_bgzf(tmp_path):
         assert N.parse_file(N.PA_FASTQ, str(tmp_path / name)) is None, name
         with pytest.raises(Exception):
             FASTAQFile(str(tmp_path / name))
+
+
+def test_early_prefetch_sniffing_matches_the_prefetch_conditions(monkeypatch):
+    """The CLI's entry-time FASTQ prefetch (main._early_reads_path) takes exactly
+    the files the later prefetch would: every argparse spelling of the task and
+    the reads, plain `.fq` only, not with streaming or prefetch turned off
+    (a second, never-adopted prefetch otherwise held device memory)."""
+    import main
+    for v in ("PA_STREAM", "PA_PREFETCH"):
+        monkeypatch.delenv(v, raising=False)
+    f = main._early_reads_path
+    assert f(["-t", "dumpalign", "-g", "g.fa", "-k", "31", "--reads", "r.fq"]) == "r.fq"
+    assert f(["-tdumpalign", "--reads=r.fq"]) == "r.fq"
+    assert f(["--task=dumpalign", "--reads", "r.fq"]) == "r.fq"
+    assert f(["--task", "dumpalign", "--reads=x/r.fq"]) == "x/r.fq"
+    assert f(["-t", "align", "--reads", "r.fq"]) is None
+    assert f(["-t", "dumpalign", "--reads", "r.fq.gz"]) is None
+    assert f(["-t", "dumpalign", "--reads", "r.fastq"]) is None
+    assert f(["-t", "dumpalign"]) is None
+    monkeypatch.setenv("PA_PREFETCH", "0")
+    assert f(["-t", "dumpalign", "--reads", "r.fq"]) is None
+    monkeypatch.setenv("PA_PREFETCH", "1")
+    monkeypatch.setenv("PA_STREAM_WINDOW", "1048576")
+    assert main._stream_window() == 1048576
