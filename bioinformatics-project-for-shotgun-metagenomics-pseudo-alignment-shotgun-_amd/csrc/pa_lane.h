@@ -80,11 +80,15 @@ constexpr uint32_t kLaneMaxMis = PA_LANE_MAXMIS;  // mismatching bases against t
 #define PA_LANE_SLOTS 1   // table slots per probe step in the cooperative passes
 #endif
 constexpr int kPassEntries = 64 * PA_LANE_PROBES;
-// Per-workgroup LDS unique counters up to this many genomes (12 B each); above
-// it the lane kernel counts in global memory (one atomic per unique read), so
-// that the counters do not cost occupancy.
+// Per-workgroup LDS unique counters up to this many genomes (8 B each: the
+// count and the smallest batch-local read index, < 2^32); above it the lane
+// kernel counts in global memory (two device-scope atomics per unique read, on
+// the same G lines from every CU).  1792: a block's counters and its four
+// waves' LaneWave<2> (26 KB) fit 40 KB, four blocks per CU in 160 KB -- the
+// 4 waves per SIMD of the plain variant.  (Round 4 kept 512 at 12 B each: C5's
+// 1200 kept genomes counted in global memory.)
 #ifndef PA_LANE_LDS_GENOMES
-#define PA_LANE_LDS_GENOMES 512
+#define PA_LANE_LDS_GENOMES 1792
 #endif
 constexpr uint32_t kLaneLdsGenomeCap = PA_LANE_LDS_GENOMES;
 
@@ -1280,14 +1284,14 @@ void k_align_lane(AlignArgs a) {
     const uint32_t G = a.G;
     const int lane = lane_id();
     const bool lds = G <= kLaneLdsGenomeCap;
-    const size_t cnt_bytes = lds ? ((size_t)G * 12 + 15) / 16 * 16 : 0;
-    unsigned long long *first = (unsigned long long *)smem;
-    uint32_t *uniq = (uint32_t *)(first + (lds ? G : 0));
+    const size_t cnt_bytes = lds ? ((size_t)G * 8 + 15) / 16 * 16 : 0;
+    uint32_t *first = (uint32_t *)smem;  // the smallest batch-local index of a unique read of g (first_key rank 0)
+    uint32_t *uniq = first + (lds ? G : 0);
     // (the wave's index read from lane 0: the LDS base is then a scalar, not a VGPR held all kernel long)
     LW_t &LW = ((LW_t *)(smem + cnt_bytes))[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     if (lds) {
         for (uint32_t i = threadIdx.x; i < G; i += kBlock) {
-            first[i] = (unsigned long long)PA_NO_FIRST_KEY;
+            first[i] = ~0u;
             uniq[i] = 0;
         }
         __syncthreads();
@@ -1453,13 +1457,12 @@ void k_align_lane(AlignArgs a) {
             n_again += (uint32_t)__popcll(ab);
         }
         if (S.kind == LANE_UNIQUE) {
-            const uint64_t key = first_key(a.base + r, 0);
             if (lds) {
                 atomicAdd(&uniq[S.g], 1u);
-                if (key < first[S.g]) atomicMin(&first[S.g], (unsigned long long)key);
+                if (r < first[S.g]) atomicMin(&first[S.g], r);
             } else {
                 atomicAdd(&a.uniq[S.g], 1ull);
-                atomicMin(&a.first[S.g], (unsigned long long)key);
+                atomicMin(&a.first[S.g], (unsigned long long)first_key(a.base + r, 0));
             }
         }
         n_uniq += (uint32_t)__popcll(__ballot(S.kind == LANE_UNIQUE));
@@ -1482,13 +1485,13 @@ void k_align_lane(AlignArgs a) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < G; i += kBlock) {
             if (uniq[i]) atomicAdd(&a.uniq[i], (unsigned long long)uniq[i]);
-            if (first[i] != (unsigned long long)PA_NO_FIRST_KEY) atomicMin(&a.first[i], first[i]);
+            if (first[i] != ~0u) atomicMin(&a.first[i], (unsigned long long)first_key(a.base + first[i], 0));
         }
     }
 }
 
 constexpr size_t lane_lds_bytes(uint32_t G, int NM = 2) {
-    return (G <= kLaneLdsGenomeCap ? ((size_t)G * 12 + 15) / 16 * 16 : 0) +
+    return (G <= kLaneLdsGenomeCap ? ((size_t)G * 8 + 15) / 16 * 16 : 0) +
            (size_t)kWaves * (NM == 4 ? sizeof(LaneWave<4>) : sizeof(LaneWave<2>));
 }
 
