@@ -497,7 +497,7 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
                 continue;
             }
             ws.wslot[w] = slot;
-            ws.wcls[w] = cls;
+            ws.wcls[w] = cls_of(cls);
             any = 1;
             uint32_t p = (uint32_t)(fmix64(slot) & (x.dh - 1));
             for (;;) {

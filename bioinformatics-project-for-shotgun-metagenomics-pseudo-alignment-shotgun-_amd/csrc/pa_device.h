@@ -38,18 +38,30 @@ struct Slot {
     uint32_t tpos;
 };
 
+// Class ids are < 2^31 (the build refuses more genome-set entries), so bit 31
+// of a slot's cls is free: for references of 2^32 .. 2^33 bases it holds bit
+// 32 of the key's concatenated first position (k_tpos_concat), whose low bits
+// are slot.tpos.  Every use of a slot's class goes through cls_of.
+constexpr uint32_t kClsMask = 0x7FFFFFFFu;
+__device__ __forceinline__ uint32_t cls_of(uint32_t cls) { return cls & kClsMask; }
+
 // Number of genomes of a class: cls < G is a singleton, otherwise the class id
 // is G + the offset of its [size, genomes...] record.
 __device__ __forceinline__ uint32_t class_size_of(uint32_t cls, uint32_t G, const uint32_t *class_genomes) {
+    cls = cls_of(cls);
     return cls < G ? 1u : class_genomes[cls - G];
 }
 
-// Concatenated-genome position of a key's first occurrence: slot.tpos is
-// genome-local, in the key's first genome (its specific genome, or the first of
-// its genome set: records are [size, ascending genomes...]).
+// Concatenated-genome position of a key's first occurrence from its slot's
+// (raw) cls and tpos: with `local` (references of >= 2^33 bases, or
+// PA_TPOS_HI=0) tpos is genome-local, in the key's first genome (its specific
+// genome, or the first of its genome set: records are [size, ascending
+// genomes...]), which costs the caller two dependent loads; otherwise tpos is
+// the position's low 32 bits and bit 31 of cls its bit 32.
 __device__ __forceinline__ uint64_t first_pos(uint32_t cls, uint32_t tpos, uint32_t G, const uint32_t *class_genomes,
                                               const uint64_t *goff, bool local) {
-    if (!local) return tpos;  // references below 2^32 bases: tpos is concatenated already
+    if (!local) return ((uint64_t)(cls >> 31) << 32) | tpos;
+    cls = cls_of(cls);
     const uint32_t g = cls < G ? cls : class_genomes[cls - G + 1];
     return goff[g] + tpos;
 }
@@ -224,7 +236,7 @@ __device__ __forceinline__ bool table_find(const Slot<NW> *__restrict__ t, uint6
 // step: tables are whole lines (cap % 4 == 0), so a search costs ~1-2 round
 // trips even at a high load factor, where slot-by-slot probing (table_find)
 // pays one dependent load per slot.  Bit i of `found` / cls[i]: key i's result
-// (keys outside `act` are not looked up).
+// (keys outside `act` are not looked up; classes without the position bit).
 template <int NP>
 __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, const HomeCfg &hc,
                                                 const uint64_t (&key)[NP], uint32_t (&cls)[NP],
@@ -259,7 +271,7 @@ __device__ __forceinline__ uint32_t probe_lines(const Slot<1> *__restrict__ t, c
                 } else if (s[i][h].key[0] == key[i]) {
                     done = true;
                     found |= 1u << i;
-                    cls[i] = s[i][h].cls;
+                    cls[i] = cls_of(s[i][h].cls);
                 }
             }
             if (!done) {

@@ -506,6 +506,7 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
     const Slot<NW> *table = (const Slot<NW> *)a.table;
     // a window whose k-mer is in the index: --max-genomes gate, else included
     auto resolve = [&](int j, uint32_t c) {
+        c = cls_of(c);  // (a slot's raw class: without its position bit)
         S.cls[j] = c;
         if ((flags & F_MG) && (int64_t)class_size_of(c, a.G, a.class_genomes) > (int64_t)a.prm.mg)
             S.hr++;  // highly redundant k-mer (src/kmer.py:425-427)
@@ -629,10 +630,10 @@ __device__ __forceinline__ void resolve_read(const AlignArgs &a, WaveLds<WPL> &L
 #endif
             const bool sf = probe_one(lane < 3, sw, scls, stp) && stp != NONE;
             // anchor: a specific seed (its genome is the read's), else any found one
-            const uint64_t b1 = __ballot(sf && scls < a.G), b2 = __ballot(sf);
+            const uint64_t b1 = __ballot(sf && cls_of(scls) < a.G), b2 = __ballot(sf);
             if (!b2) continue;
             const int l = (int)__builtin_ctzll(b1 ? b1 : b2);
-            const uint32_t ga = b1 ? __builtin_amdgcn_readlane(scls, l) : NONE;
+            const uint32_t ga = b1 ? cls_of(__builtin_amdgcn_readlane(scls, l)) : NONE;
             const uint32_t lcls = __builtin_amdgcn_readlane(scls, l), ltp = __builtin_amdgcn_readlane(stp, l);
             const int64_t A = (int64_t)first_pos(lcls, ltp, a.G, a.class_genomes, a.goff, a.tpos_local) -
                               (int64_t)__builtin_amdgcn_readlane(sw, l);

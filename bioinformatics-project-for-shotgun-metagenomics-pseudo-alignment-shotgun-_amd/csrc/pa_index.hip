@@ -506,7 +506,7 @@ __global__ void k_lookup(const Slot<NW> *table, HomeCfg hc, const uint8_t *kmers
     uint64_t slot;
     uint32_t cls = 0, tpos = 0;
     if (ok && table_find<NW, true>(table, cap, key, home_of(key, key_hash(key), hc), slot, cls, tpos)) {
-        cls_out[i] = cls;
+        cls_out[i] = cls_of(cls);
         size_out[i] = class_size_of(cls, G, class_genomes);
     } else {
         cls_out[i] = -1;
@@ -598,6 +598,24 @@ __global__ void k_tile_cls_all(const uint8_t *__restrict__ codes, const uint64_t
                 atomicMin(&table[slot].tpos, (uint32_t)(gstart + w));
             }
         }
+    }
+}
+
+// First occurrences as concatenated positions for references of 2^32 .. 2^33
+// bases (tiled with genome-local tpos, k_tile_cls_all): tpos = the low 32
+// bits, bit 31 of cls = bit 32 (pad::first_pos).  The lane kernels' anchors
+// then need no class-record and goff loads (C4 laid out genome-locally ran
+// 5 % slower: profiles/r05/ab_tpos_local.txt).  One pass over the slots.
+template <int NW>
+__global__ void k_tpos_concat(Slot<NW> *table, uint64_t cap, uint32_t G, const uint32_t *__restrict__ class_genomes,
+                              const uint64_t *__restrict__ goff) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+        Slot<NW> &s = table[i];
+        if (s.key[0] == EMPTY || s.tpos == NONE) continue;
+        const uint64_t fo = first_pos(s.cls, s.tpos, G, class_genomes, goff, true);
+        s.tpos = (uint32_t)fo;
+        s.cls |= (uint32_t)(fo >> 32) << 31;
     }
 }
 
@@ -1090,7 +1108,7 @@ __global__ void k_extsim_slots(const Slot<NW> *table, uint64_t cap, uint32_t n_g
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; s < cap; s += stride) {
         if (table[s].key[0] == EMPTY) continue;
-        uint32_t c = table[s].cls;
+        uint32_t c = cls_of(table[s].cls);
         if (c < n_genomes) {
             uint32_t a = group_of[c];
             if (use_lds)
@@ -1307,8 +1325,8 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         B_HIP(hipMemcpyAsync(h_cnt, cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
         B_HIP(hipStreamSynchronize(st));
         const uint64_t n_cls = h_cnt[3], entries = h_cnt[4];
-        if ((uint64_t)G + entries >= 0xFFFFFFFFull) {
-            pa::set_error("index build: too many distinct genome sets for 32-bit class ids");
+        if ((uint64_t)G + entries >= (uint64_t)PA_TILE_REP) {  // (bit 31 of a class id is the position bit, cls_of)
+            pa::set_error("index build: too many distinct genome-set entries for 31-bit class ids");
             cleanup();
             return PA_EUNSUPPORTED;
         }
@@ -1546,6 +1564,16 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             B_HIP(e);
         }
         phase_mark("tile classes");
+        // below 2^33 bases: first occurrences as 33-bit concatenated positions
+        // (PA_TPOS_HI=0 keeps them genome-local: tests of that layout)
+        const char *thi = std::getenv("PA_TPOS_HI");
+        if (idx->tpos_local && idx->h_goff[G] < (1ull << 33) && !(thi && thi[0] == '0')) {
+            hipLaunchKernelGGL(k_tpos_concat<NW>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                               dim3(kBlock), 0, st, table, idx->cap, G, idx->class_genomes, idx->goff);
+            B_HIP(hipGetLastError());
+            idx->tpos_local = 0;
+            phase_mark("first occurrences concatenated");
+        }
         {  // genome of every 2^16-th position: genome_of is then one or two goff steps
             const uint64_t nb_ = (n >> 16) + 2;
             std::vector<uint32_t> gb(nb_);

@@ -531,7 +531,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             sfound |= f;
             bool spec = false;
 #pragma unroll
-            for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && scls[i] < a.G && stp32[i] != NONE;
+            for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && cls_of(scls[i]) < a.G && stp32[i] != NONE;
             act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 14) act = 0;  // timing dissection: one seed round
@@ -543,9 +543,11 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     }
     uint64_t stp[NSEED];  // first occurrences, concatenated positions (NONE64: none)
 #pragma unroll
-    for (int i = 0; i < NSEED; i++)
+    for (int i = 0; i < NSEED; i++) {
         stp[i] = bit(sfound, i) && stp32[i] != NONE ? first_pos(scls[i], stp32[i], a.G, a.class_genomes, a.goff, a.tpos_local)
                                                      : ~0ull;
+        scls[i] = cls_of(scls[i]);  // (the position bit used)
+    }
     int at = -1;
 #pragma unroll
     for (int pass = 0; pass < 2; pass++)
@@ -1242,15 +1244,15 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
         for (int i = 0; i < NPR; i++) {
             if (!bit(f, i)) continue;
             const uint32_t o = tag4[i] >> 8, w = tag4[i] & 255;
-            const uint32_t cl = c4[i];
+            const uint32_t cl = cls_of(c4[i]);
             if ((a.prm.flags & F_MG) && (int64_t)class_size_of(cl, a.G, a.class_genomes) > (int64_t)a.prm.mg) {
                 atomicAdd(&LW.hr[o], 1u);  // highly redundant: counted, never included
             } else if (cl >= a.G) {
                 atomicAdd(&LW.flags[o], 4u);  // unspecific: counted in bits 2..
             } else {
                 atomicOr(&LW.flags[o], 1u);
-                atomicMin(&LW.cand[o], ((unsigned long long)w << 40) | first_pos(cl, t4[i], a.G, a.class_genomes, a.goff,
-                                                                               a.tpos_local));
+                atomicMin(&LW.cand[o], ((unsigned long long)w << 40) | first_pos(c4[i], t4[i], a.G, a.class_genomes,
+                                                                               a.goff, a.tpos_local));
             }
         }
         wave_sync();  // the list is rewritten by the next pass
@@ -1835,7 +1837,7 @@ __device__ __forceinline__ void na_probe_rest(const AlignArgs &a, const uint64_t
         for (int j = 0; j < NPB; j++) {
             if (!bit(f, j)) continue;
             if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
-            else if (cl[j] >= a.G) noff++;
+            else if (cls_of(cl[j]) >= a.G) noff++;
             else spec = true;
         }
     }

@@ -561,17 +561,22 @@ def test_full_size_shards_equal_one_pass():
 
 
 @pytest.mark.gpu
-def test_large_reference_layout(monkeypatch):
+@pytest.mark.parametrize("tpos_hi", ["1", "0"])
+def test_large_reference_layout(monkeypatch, tpos_hi):
     """The layout of references too large for the default one (C5: 8 Gbp):
     table sized on the HyperLogLog distinct estimate at 1.43 slots per k-mer
-    (load ~0.7, long probe chains), genome-local first occurrences (first_pos)
-    and present-only neighbour bits, no Bloom filter -- same index, same results
-    as the oracle, the lane kernel on."""
+    (load ~0.7, long probe chains), first occurrences as 33-bit concatenated
+    positions (tpos_hi 1: bit 32 in the class word, C5's kept 4.8 Gbp) or
+    genome-local (tpos_hi 0: references of >= 2^33 bases; first_pos) and
+    present-only neighbour bits, no Bloom filter -- same index, same results as
+    the oracle, the lane kernel on."""
     gens, s, q, off = _synthetic_case(20, 30000, 5, 0.01, 31, 8000, 150, 0.01, seed=4242)
     oix = O.OracleIndex(gens, 31)
     monkeypatch.setenv("PA_LAYOUT", "large")  # every choice the build makes for an 8 Gbp reference
+    monkeypatch.setenv("PA_TPOS_HI", tpos_hi)
     index = N.Index(gens, 31)
     monkeypatch.delenv("PA_LAYOUT")
+    monkeypatch.delenv("PA_TPOS_HI")
     info = index.info()
     assert index.n_kmers == oix.n_kmers
     assert info.table_slots < 2 * index.n_kmers  # sized on the estimate (default: 4 x windows)
