@@ -411,12 +411,14 @@ __device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t *red) {
     return s;
 }
 
+constexpr uint32_t kRankLds = 2048;  // genomes of a read's list ranked in LDS (16 KB); more: over the scratch
 template <int NW>
 __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
     const AlignArgs &a = x.a;
     __shared__ uint32_t red[kWaves];
     __shared__ unsigned long long red64[kWaves];
-    __shared__ uint32_t n_touched, n_cls;
+    __shared__ uint32_t n_touched, n_cls, n_rank;
+    __shared__ uint64_t rank_key[kRankLds];  // the listed genomes' order keys (ranks of genomes_mapped_to)
     const uint32_t G = a.G;
     const int k = a.k;
     const uint64_t mask0 = k > 0 ? mask0_of(k, NW) : 0;
@@ -616,9 +618,21 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
                     }
                 }
             } else if (unique && demote) {
+                // the listed genomes' order keys (first window << 32 | genome)
+                // staged in LDS once, so that each one's rank is counted over
+                // LDS rather than over the scratch in global memory (2 nt loads
+                // per genome: ~1 ms for the reads of C5's families)
+                if (threadIdx.x == 0) n_rank = 0;
+                __syncthreads();
                 uint32_t nq = 0;
-                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) nq += ld_agent(&ws.g_tot[ws.touched[t]]) >= tstar;
-                nq = block_sum(nq, red);
+                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                    const uint32_t g = ws.touched[t];
+                    if (ld_agent(&ws.g_tot[g]) < tstar) continue;
+                    nq++;
+                    const uint32_t i = atomicAdd(&n_rank, 1u);
+                    if (i < kRankLds) rank_key[i] = ((uint64_t)ld_agent(&ws.g_totmin[g]) << 32) | g;
+                }
+                nq = block_sum(nq, red);  // (its barriers also publish rank_key)
                 list_len = 1 + nq;
                 for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
                     const uint32_t g = ws.touched[t];
@@ -626,11 +640,15 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
                     if (tg < tstar) continue;
                     const uint64_t me = ((uint64_t)ld_agent(&ws.g_totmin[g]) << 32) | g;
                     uint32_t rank = 1;
-                    for (uint32_t u = 0; u < nt; u++) {
-                        const uint32_t h = ws.touched[u];
-                        if (ld_agent(&ws.g_tot[h]) >= tstar &&
-                            (((uint64_t)ld_agent(&ws.g_totmin[h]) << 32) | h) < me)
-                            rank++;
+                    if (nq <= kRankLds) {
+                        for (uint32_t u = 0; u < nq; u++) rank += rank_key[u] < me;
+                    } else {
+                        for (uint32_t u = 0; u < nt; u++) {
+                            const uint32_t h = ws.touched[u];
+                            if (ld_agent(&ws.g_tot[h]) >= tstar &&
+                                (((uint64_t)ld_agent(&ws.g_totmin[h]) << 32) | h) < me)
+                                rank++;
+                        }
                     }
                     if (x.detail == 2) x.lists[x.list_off[r] + rank] = g;
                     if (!x.detail) {
@@ -641,14 +659,28 @@ __global__ __launch_bounds__(kBlock) void k_align_exact(ExactArgs x) {
                 if (threadIdx.x == 0 && x.detail == 2) x.lists[x.list_off[r]] = gstar;
             } else if (nspec > 0) {
                 list_len = nspec;
+                // (the genomes with specific k-mers: their first windows staged in LDS, as above)
+                if (threadIdx.x == 0) n_rank = 0;
+                __syncthreads();
+                for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
+                    const uint32_t g = ws.touched[t];
+                    if (ld_agent(&ws.g_spec[g]) == 0) continue;
+                    const uint32_t i = atomicAdd(&n_rank, 1u);
+                    if (i < kRankLds) rank_key[i] = ld_agent(&ws.g_specmin[g]);
+                }
+                __syncthreads();
                 for (uint32_t t = threadIdx.x; t < nt; t += kBlock) {
                     const uint32_t g = ws.touched[t];
                     if (ld_agent(&ws.g_spec[g]) == 0) continue;
                     const uint32_t mw = ld_agent(&ws.g_specmin[g]);
                     uint32_t rank = 0;
-                    for (uint32_t u = 0; u < nt; u++) {
-                        const uint32_t h = ws.touched[u];
-                        if (ld_agent(&ws.g_spec[h]) > 0 && ld_agent(&ws.g_specmin[h]) < mw) rank++;
+                    if (nspec <= kRankLds) {
+                        for (uint32_t u = 0; u < nspec; u++) rank += rank_key[u] < mw;
+                    } else {
+                        for (uint32_t u = 0; u < nt; u++) {
+                            const uint32_t h = ws.touched[u];
+                            if (ld_agent(&ws.g_spec[h]) > 0 && ld_agent(&ws.g_specmin[h]) < mw) rank++;
+                        }
                     }
                     if (x.detail == 2) x.lists[x.list_off[r] + rank] = g;
                     if (!x.detail) {
