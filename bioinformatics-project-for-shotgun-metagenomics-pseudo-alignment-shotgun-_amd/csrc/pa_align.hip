@@ -199,7 +199,7 @@ __device__ __forceinline__ void quality_read(const uint8_t *__restrict__ qual, u
     // E bit i: the window ending at byte i fails (its sum < T); bytes i - k
     // from rk (0 before the read)
     const uint32_t kb = 8 * ((uint32_t)k & 3);
-    uint32_t E[kQmDwords / 8 + 1] = {};
+    uint32_t E[kQmDwords / 8 + 3] = {};  // (+2 zero words: the shift by up to k - 1 = 94 bits below)
     uint32_t run = 0;
 #pragma unroll
     for (int j = 0; j < kQmDwords; j++) {
@@ -218,11 +218,12 @@ __device__ __forceinline__ void quality_read(const uint8_t *__restrict__ qual, u
         const int32_t hi = (int32_t)len - 32 * d;
         E[d] &= hi >= 32 ? ~0u : hi <= 0 ? 0u : (1u << hi) - 1;
     }
-    const uint32_t sh = (uint32_t)k - 1, shb = sh & 31;  // (k <= 63: a shift of up to one word and 31 bits)
-    const bool w1 = sh >= 32;
+    const uint32_t sh = (uint32_t)k - 1, shb = sh & 31, q = sh >> 5;  // (k <= 95: up to two words and 30 bits)
     uint32_t F[4];
 #pragma unroll
-    for (int d = 0; d < 4; d++) F[d] = __builtin_amdgcn_alignbit(w1 ? E[d + 2] : E[d + 1], w1 ? E[d + 1] : E[d], shb);
+    for (int d = 0; d < 4; d++)
+        F[d] = __builtin_amdgcn_alignbit(q >= 2 ? E[d + 3] : q == 1 ? E[d + 2] : E[d + 1],
+                                         q >= 2 ? E[d + 2] : q == 1 ? E[d + 1] : E[d], shb);
     mask = make_uint4(F[0], F[1], F[2], F[3]);
 }
 
@@ -246,12 +247,29 @@ __device__ __forceinline__ void quality_reads(const uint8_t *__restrict__ qual, 
     }
 }
 
+// LONG: k > 63 (three-word keys), a kernel of its own so that the longer
+// realignments do not raise the registers of the k <= 63 one
+template <bool LONG = false>
 __global__ __launch_bounds__(256) void k_quality_masks(const uint8_t *__restrict__ qual, const uint64_t *__restrict__ off,
                                                        uint64_t n, int k, int64_t mrq, int64_t mkq, uint32_t flags,
                                                        uint4 *__restrict__ qmask, uint8_t *__restrict__ qdrop) {
     const int64_t T64 = mkq * (int64_t)k;
     const uint32_t T = T64 <= 0 ? 0u : (T64 > (1 << 24) ? (1u << 24) : (uint32_t)T64);
-    switch (k >> 2) {  // (k <= 63 on the lane path; uniform)
+    if (LONG) {
+        switch (k >> 2) {
+            case 16: quality_reads<16>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            case 17: quality_reads<17>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            case 18: quality_reads<18>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            case 19: quality_reads<19>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            case 20: quality_reads<20>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            case 21: quality_reads<21>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            case 22: quality_reads<22>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            case 23: quality_reads<23>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
+            default: break;  // (unreachable: 63 < k <= 95)
+        }
+        return;
+    }
+    switch (k >> 2) {  // (k <= 63 here; uniform)
         case 0: quality_reads<0>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 1: quality_reads<1>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 2: quality_reads<2>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
@@ -268,7 +286,7 @@ __global__ __launch_bounds__(256) void k_quality_masks(const uint8_t *__restrict
         case 13: quality_reads<13>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 14: quality_reads<14>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
         case 15: quality_reads<15>(qual, off, n, k, T, mrq, flags, qmask, qdrop); break;
-        default: break;  // (unreachable: the launch requires k <= 63)
+        default: break;  // (unreachable: k > 63 takes the LONG kernel)
     }
 }
 
@@ -768,8 +786,8 @@ struct KernelTimer {
 // bases): the 250-bp shape (NM = 4, <= 272 bases, <= 256 windows) walks them,
 // unless --min-kmer-quality is set (its window masks cover 128 windows: such
 // reads then go to the wave kernel).
-// nw: key words (2: 31 < k <= 63 -- the 150-bp shape, no reverse-strand path:
-// reads without a seed go to the wave kernel).
+// nw: key words (2: 31 < k <= 63, 3: 63 < k <= 95 -- the 150-bp shape, no
+// reverse-strand path: reads without a seed go to the wave kernel).
 pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr, bool long_reads = false,
                       int nw = 1) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
@@ -777,7 +795,11 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
     const bool mg = (a.prm.flags & F_MG) != 0;
     const bool nm4 = long_reads && !win_q && nw == 1;
     const size_t shm = lane_lds_bytes(a.G, nm4 ? 4 : 2);
-    auto kern = nw == 2
+    auto kern = nw == 3
+                    ? (win_q ? (mg ? k_align_lane<true, true, true, 2, 3> : k_align_lane<true, true, false, 2, 3>)
+                       : need_q ? (mg ? k_align_lane<true, false, true, 2, 3> : k_align_lane<true, false, false, 2, 3>)
+                                : (mg ? k_align_lane<false, false, true, 2, 3> : k_align_lane<false, false, false, 2, 3>))
+              : nw == 2
                     ? (win_q ? (mg ? k_align_lane<true, true, true, 2, 2> : k_align_lane<true, true, false, 2, 2>)
                        : need_q ? (mg ? k_align_lane<true, false, true, 2, 2> : k_align_lane<true, false, false, 2, 2>)
                                 : (mg ? k_align_lane<false, false, true, 2, 2> : k_align_lane<false, false, false, 2, 2>))
@@ -1085,7 +1107,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
     const bool fast_ok = idx->k > 0 && idx->nw <= 4 && idx->n_kmers > 0;  // (k <= 127: the wave kernel's keys)
     // the lane kernel first (single-word keys on a tiled index); PA_NO_LANE=1 skips it
     const char *no_lane = std::getenv("PA_NO_LANE");
-    const bool lane_ok = fast_ok && idx->nw <= 2 && a.tile_n > 0 && a.tile_lw && !(no_lane && no_lane[0] == '1');
+    const bool lane_ok = fast_ok && idx->nw <= 3 && a.tile_n > 0 && a.tile_lw && !(no_lane && no_lane[0] == '1');
     if (fast_ok) {
         const uint32_t wmax = r->max_len >= idx->k ? (uint32_t)(r->max_len - idx->k + 1) : 0;
         const int wpl = wmax <= 64 ? 1 : wmax <= 128 ? 2 : 4;  // longer reads are deferred by WPL=4
@@ -1138,13 +1160,13 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.queue_hard_count = (unsigned long long *)idx->counters + 3;
             PA_HIP(hipMemsetAsync(idx->counters + 3, 0, 8, st));
             if (a.prm.flags & (F_MRQ | F_MKQ)) {  // the quality filters of every read, up front
-                if (idx->k > 63) {  // (k_quality_masks realigns by k >> 2 <= 15: lane_ok implies k <= 63)
-                    set_error("internal: quality pre-pass for k > 63");
+                if (idx->k > 95) {  // (k_quality_masks realigns by k >> 2 <= 23: lane_ok implies k <= 95)
+                    set_error("internal: quality pre-pass for k > 95");
                     return PA_EINTERNAL;
                 }
                 PA_TRY(ensure_qmask(idx, r->n));
                 KernelTimer kt(idx, st, PA_PROF_QUALITY);
-                hipLaunchKernelGGL(k_quality_masks, dim3((unsigned)std::min<uint64_t>((r->n + 255) / 256, 65536)),
+                hipLaunchKernelGGL(idx->k > 63 ? k_quality_masks<true> : k_quality_masks<false>, dim3((unsigned)std::min<uint64_t>((r->n + 255) / 256, 65536)),
                                    dim3(256), 0, st, r->qual, r->off, r->n, (int)idx->k, (int64_t)a.prm.mrq,
                                    (int64_t)a.prm.mkq, a.prm.flags & (F_MRQ | F_MKQ), idx->qmask, idx->qdrop);
                 PA_HIP(hipGetLastError());

@@ -398,6 +398,43 @@ __device__ __forceinline__ void bloom_word2(const Key<2> &key, uint32_t lg, uint
     const uint64_t b = fmix64(key.w[1] ^ (key.w[0] * 0xC2B2AE3D27D4EB4Full) ^ 0x5851F42D4C957F2Dull);
     w = ((b >> (64 - (lg - kBloomLgBW))) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
 }
+// The same for a three-word key (63 < k <= 95: the lane path of the
+// reference's demo k = 75, src/RUN_LOG:28-61).
+__device__ __forceinline__ void bloom_word3(const Key<3> &key, uint32_t lg, uint64_t &w, uint64_t &m) {
+    const uint64_t x = key.w[2] ^ (key.w[1] * 0x9E3779B97F4A7C15ull) ^ (key.w[0] * 0xD6E8FEB86659FD93ull);
+    const uint32_t h = bloom_key_mix(x);
+    m = bloom_bits(h);
+    const uint64_t b = fmix64(x ^ (key.w[1] * 0xC2B2AE3D27D4EB4Full) ^ 0x5851F42D4C957F2Dull);
+    w = ((b >> (64 - (lg - kBloomLgBW))) << kBloomLgBW) | (h >> (32 - kBloomLgBW));
+}
+// The key of the genome window at 2-bit position t (the words key_push leaves:
+// the last 32 bases in w[NW - 1], the first 2k - 64 (NW - 1) bits in w[0]).
+template <int NW>
+__device__ __forceinline__ Key<NW> genome_key(const uint64_t *pk, uint64_t t, int k) {
+    Key<NW> K;
+    const int hb = 2 * k - 64 * (NW - 1);
+#pragma unroll
+    for (int j = 1; j < NW; j++) K.w[j] = get64_at(pk, 2 * t + 2 * k - 64 * (NW - j));
+    K.w[0] = NW == 1 ? (get64_at(pk, 2 * t) >> (64 - 2 * k)) : (hb ? get64_at(pk, 2 * t) >> (64 - hb) : 0ull);
+    return K;
+}
+// The key with base j of its window (0: the first) replaced by its b-th other
+// base ((base + 1 + b) & 3).
+template <int NW>
+__device__ __forceinline__ Key<NW> key_sub(Key<NW> K, int j, int k, int b) {
+    const int bs = 2 * (k - 1 - j);  // the base's bit offset from the key's end
+    const int wi = NW - 1 - bs / 64, bo = bs % 64;
+    uint64_t c = 0;
+#pragma unroll
+    for (int q = 0; q < NW; q++)
+        if (q == wi) c = (K.w[q] >> bo) & 3;
+    const uint64_t x = (c ^ ((c + 1 + (uint64_t)b) & 3)) << bo;
+#pragma unroll
+    for (int q = 0; q < NW; q++)
+        if (q == wi) K.w[q] ^= x;
+    return K;
+}
+
 // Minimizer presence bitmap (mm_bits, 2^lg bits): bit mm_bit(mn) is set for
 // the minimizer of every key (k_mm_build) -- a prefilter small enough to stay
 // in the L2 that answers a whole minimizer run of absent windows.

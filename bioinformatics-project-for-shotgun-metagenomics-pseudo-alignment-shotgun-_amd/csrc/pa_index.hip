@@ -626,7 +626,7 @@ __global__ void k_tpos_concat(Slot<NW> *table, uint64_t cap, uint32_t G, const u
 // < kTileRepDist apart), which the lane kernel (pa_lane.h) tests instead of
 // deduplicating.  One block per 256 positions, keys staged in LDS.
 constexpr int kTileRepDist = 255;  // (>= the lane kernels' longest span of windows: 256 windows, pa_lane.h)
-template <int NW>  // (1: k <= 31, 2: k <= 63 -- the key words compared)
+template <int NW>  // (1: k <= 31, 2: k <= 63, 3: k <= 95 -- the key words compared)
 __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ pk, uint32_t *tile_cls, uint64_t n,
                                                   int k) {
     __shared__ uint64_t keys[NW][256 + kTileRepDist];
@@ -641,8 +641,9 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
             if (NW == 1) {
                 keys[0][i] = ok ? (get64_at(pk, 2 * t) >> sh) : 0;
             } else {  // the key's words (pa_lane.h row_key)
-                keys[NW - 1][i] = ok ? get64_at(pk, 2 * t + 2 * k - 64) : 0;
-                keys[0][i] = ok && hb ? get64_at(pk, 2 * t) >> (64 - hb) : 0;
+                const Key<NW> K = ok ? genome_key<NW>(pk, t, k) : Key<NW>{};
+#pragma unroll
+                for (int j = 0; j < NW; j++) keys[j][i] = K.w[j];
             }
         }
         __syncthreads();
@@ -895,18 +896,59 @@ __global__ __launch_bounds__(256) void k_nb_first(const uint64_t *__restrict__ p
     }
 }
 
-// The same for two-word keys (31 < k <= 63: pa_device.h bloom_word2).
-__global__ void k_bloom_build2(const Slot<2> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg) {
+// The same for two- and three-word keys (31 < k <= 95: pa_device.h
+// bloom_word2 / bloom_word3).
+template <int NW = 2>
+__global__ void k_bloom_build2(const Slot<NW> *__restrict__ table, uint64_t cap, uint64_t *bloom, uint32_t lg) {
+    static_assert(NW == 2 || NW == 3, "two- or three-word keys");
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
-        const Slot<2> s = table[i];
+        const Slot<NW> s = table[i];
         if (s.key[0] == EMPTY) continue;
-        Key<2> kk;
-        kk.w[0] = s.key[0];
-        kk.w[1] = s.key[1];
+        Key<NW> kk;
+#pragma unroll
+        for (int j = 0; j < NW; j++) kk.w[j] = s.key[j];
         uint64_t w, m;
-        bloom_word2(kk, lg, w, m);
+        if constexpr (NW == 2)
+            bloom_word2(kk, lg, w, m);
+        else
+            bloom_word3(kk, lg, w, m);
         atomicOr((unsigned long long *)&bloom[w], (unsigned long long)m);
+    }
+}
+
+// Neighbour summaries of three-word keys (63 < k <= 95): nbs holds 4 bits per
+// genome position p (8 positions per 32-bit word), bit b set when SOME indexed
+// window holding p is, with its base at p replaced by the b-th other base,
+// a key of the index.  A k-window word of bits as for k <= 63 would take 48 B
+// per base; the summary takes 0.5, and a read window with one mismatch at p
+// whose summary bit is clear is absent (the lane walk, pa_lane.h) -- on a
+// random or family reference almost every such bit is clear, a set one only
+// makes the walk probe that mismatch's windows.  Every indexed window probes
+// its 3k neighbours, the build-time Bloom filter (bloom_word3) first.
+__global__ void k_nb_sum3(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
+                          const Slot<3> *__restrict__ table, HomeCfg hc, uint32_t *nbs,
+                          const uint64_t *__restrict__ bloom, uint32_t bloom_lg) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+        if (tile_cls[t] == NONE) continue;
+        const Key<3> K = genome_key<3>(pk, t, k);
+        for (int j = 0; j < k; j++) {
+            const uint64_t p = t + j;
+            uint32_t have = 0;
+            for (int b = 0; b < 3; b++) {
+                const Key<3> N = key_sub<3>(K, j, k, b);
+                if (bloom) {
+                    uint64_t w, m;
+                    bloom_word3(N, bloom_lg, w, m);
+                    if ((bloom[w] & m) != m) continue;
+                }
+                uint64_t s2;
+                uint32_t c2, p2;
+                if (table_find<3, true>(table, hc.cap, N, home_of<3>(N, key_hash(N), hc), s2, c2, p2)) have |= 1u << b;
+            }
+            if (have) atomicOr(&nbs[p >> 3], have << (4 * (p & 7)));
+        }
     }
 }
 
@@ -1381,8 +1423,11 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
 // allocation) -- they repay themselves after ~4 reads per genome base.
 pa_status build_nb2(pa_index *idx, hipStream_t st);
 
+pa_status build_nb3(pa_index *idx, hipStream_t st);
+
 pa_status build_nb(pa_index *idx, hipStream_t st) {
     if (idx->nw == 2) return build_nb2(idx, st);
+    if (idx->nw == 3) return build_nb3(idx, st);
     const uint64_t n = idx->tile_n;
     const int k = (int)idx->k;
     const uint32_t G = idx->n_genomes;
@@ -1501,7 +1546,7 @@ pa_status build_nb2(pa_index *idx, hipStream_t st) {
             while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
             if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && pa::dev_malloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
                 PA_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
-                hipLaunchKernelGGL(k_bloom_build2, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                hipLaunchKernelGGL(k_bloom_build2<2>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
                                    dim3(kBlock), 0, st, (const Slot<2> *)idx->table, idx->cap, bb, bb_lg);
             } else {
                 bb = nullptr;
@@ -1520,6 +1565,46 @@ pa_status build_nb2(pa_index *idx, hipStream_t st) {
         idx->nb_spec = 0;
         idx->device_bytes += n * 24;
         phase_mark("nb: two-word keys");
+    }
+    idx->nb_pending = 0;
+    return PA_OK;
+}
+
+// Neighbour summaries of three-word keys (k_nb_sum3): 0.5 B per base.
+pa_status build_nb3(pa_index *idx, hipStream_t st) {
+    const uint64_t n = idx->tile_n;
+    const char *no_nb = std::getenv("PA_NO_NB");
+    const uint64_t bytes = (n / 8 + 64) * 4;
+    size_t free_b = 0, total_b = 0;
+    if (!(no_nb && no_nb[0] == '1') && pa::dev_mem_info(&free_b, &total_b) == hipSuccess && bytes <= free_b / 4) {
+        PA_HIP(pa::dev_malloc(&idx->tile_nb, bytes));
+        PA_HIP(hipMemsetAsync(idx->tile_nb, 0, bytes, st));
+        uint64_t *bb = nullptr;  // the build-time Bloom filter, 16 bits per key (freed below)
+        uint32_t bb_lg = 6;
+        if (idx->n_kmers > 0) {
+            while (bb_lg < 33 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;
+            size_t fb = 0, tb = 0;
+            if (pa::dev_mem_info(&fb, &tb) != hipSuccess) fb = 0;
+            while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
+            if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && pa::dev_malloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
+                PA_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
+                hipLaunchKernelGGL(k_bloom_build2<3>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                   dim3(kBlock), 0, st, (const Slot<3> *)idx->table, idx->cap, bb, bb_lg);
+            } else {
+                bb = nullptr;
+            }
+        }
+        hipLaunchKernelGGL(k_nb_sum3, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
+                           idx->tile_pk, idx->tile_cls, n, (int)idx->k, (const Slot<3> *)idx->table, idx->home,
+                           (uint32_t *)idx->tile_nb, bb, bb_lg);
+        PA_HIP(hipGetLastError());
+        if (bb) {
+            PA_HIP(hipStreamSynchronize(st));
+            pa::dev_free(bb);
+        }
+        idx->nb_spec = 0;
+        idx->device_bytes += bytes;
+        phase_mark("nb: three-word summaries");
     }
     idx->nb_pending = 0;
     return PA_OK;
@@ -1590,9 +1675,9 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
             idx->device_bytes += nb_ * 4;
         }
         // the lane kernels' view: keys of one word (k <= 31) or two (k <= 63)
-        const bool lane_view = NW <= 2 && k <= 32 * NW - 1;
+        const bool lane_view = NW <= 3 && k <= 32 * NW - 1;
         if (lane_view)
-            hipLaunchKernelGGL(k_tile_rep<NW <= 2 ? NW : 1>, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)),
+            hipLaunchKernelGGL(k_tile_rep<NW <= 3 ? NW : 1>, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1u << 20)),
                                dim3(256), 0, st, idx->tile_pk, idx->tile_cls, n, k);
         if (lane_view) {
             const uint64_t n_blocks = n / 64 + 8;  // padded: the 250-bp walk reads six blocks from any position
@@ -1645,9 +1730,12 @@ pa_status build_tiles_nw(pa_index *idx, hipStream_t st) {
                     if (NW == 1)
                         hipLaunchKernelGGL(k_bloom_build<false>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
                                            dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, idx->bloom, lg, k);
-                    else
-                        hipLaunchKernelGGL(k_bloom_build2, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                    else if (NW == 2)
+                        hipLaunchKernelGGL(k_bloom_build2<2>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
                                            dim3(kBlock), 0, st, (const Slot<2> *)table, idx->cap, idx->bloom, lg);
+                    else
+                        hipLaunchKernelGGL(k_bloom_build2<3>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                                           dim3(kBlock), 0, st, (const Slot<3> *)table, idx->cap, idx->bloom, lg);
                     idx->bloom_lg = lg;
                     idx->device_bytes += (1ull << lg) * 8;
                 }
@@ -1797,7 +1885,9 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
     PhaseScope ps(t_phase ? t_phase : own.get());
     const uint64_t bases = idx->h_goff.empty() ? 0 : idx->h_goff.back();
     idx->nb_skip = reads_hint != ~0ull && reads_hint < kNbReadsPerBase * bases;
-    pa_status rc = idx->nw == 2 ? build_tiles_nw<2>(idx, st) : build_tiles_nw<1>(idx, st);  // (one- or two-word keys)
+    pa_status rc = idx->nw == 3   ? build_tiles_nw<3>(idx, st)
+                   : idx->nw == 2 ? build_tiles_nw<2>(idx, st)
+                                  : build_tiles_nw<1>(idx, st);  // (keys of one to three words)
     idx->nb_skip = 0;
     if (rc != PA_OK) {  // the index stays usable without its align-side view
         pa::dev_free(idx->tile_cls); pa::dev_free(idx->tile_pk); pa::dev_free(idx->tile_lw); pa::dev_free(idx->tile_nb);
@@ -1832,7 +1922,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     const char *no_tile = std::getenv("PA_NO_TILE");
     uint64_t max_glen = 0;
     for (uint32_t g = 0; g < n; g++) max_glen = std::max<uint64_t>(max_glen, goff[g + 1] - goff[g]);
-    idx->tile_n = (idx->nw <= 2 && k > 0 && total > 0 && max_glen < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
+    idx->tile_n = (idx->nw <= 3 && k > 0 && total > 0 && max_glen < 0xFFFFFFFFull && !(no_tile && no_tile[0] == '1'))
                       ? total : 0;
     idx->tpos_local = total >= 0xFFFFFFFFull ? 1 : 0;
     // PA_LAYOUT=large (tests): every choice the build makes for a reference too

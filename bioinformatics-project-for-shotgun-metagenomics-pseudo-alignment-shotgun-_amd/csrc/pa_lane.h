@@ -298,17 +298,18 @@ __device__ __forceinline__ uint64_t row_bits(const uint64_t *row, uint32_t o) {
 }
 
 // The key of window w of a packed row: k bases from bit 2 w, laid out as
-// key_push builds them (the last 32 bases in the low word; for NW = 2 the
-// first k - 32 in the top one, zero at k = 32).
+// key_push builds them (the last 32 bases in the low word; for NW >= 2 the
+// first k - 32 (NW - 1) in the top one, zero at k = 32 (NW - 1)).
 template <int NW>
 __device__ __forceinline__ Key<NW> row_key(const uint64_t *row, uint32_t w, int k) {
     Key<NW> K;
     if constexpr (NW == 1) {
         K.w[0] = row_bits(row, 2 * w) >> (64 - 2 * k);
     } else {
-        static_assert(NW == 2, "lane-path keys: one or two words");
-        K.w[1] = row_bits(row, 2 * w + 2 * k - 64);
-        const int hb = 2 * k - 64;
+        static_assert(NW == 2 || NW == 3, "lane-path keys: one to three words");
+#pragma unroll
+        for (int j = 1; j < NW; j++) K.w[j] = row_bits(row, 2 * w + 2 * k - 64 * (NW - j));
+        const int hb = 2 * k - 64 * (NW - 1);
         K.w[0] = hb ? row_bits(row, 2 * w) >> (64 - hb) : 0ull;
     }
     return K;
@@ -499,7 +500,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
     // (seed i's window, recomputed where needed rather than kept in registers)
     auto sw = [W](int i) { return (uint32_t)(((uint64_t)(W - 1) * (uint32_t)i) / (NSEED - 1)); };
     uint64_t skey[NW == 1 ? NSEED : 1];  // (single-word keys)
-    Key<NW> skk[NW == 1 ? 1 : NSEED];    // (two-word keys, 31 < k <= 63)
+    Key<NW> skk[NW == 1 ? 1 : NSEED];    // (two- and three-word keys, 31 < k <= 95)
     if constexpr (NW == 1) {
 #pragma unroll
         for (int i = 0; i < NSEED; i++) skey[i] = row_bits(row, 2 * sw(i)) >> sh;
@@ -527,7 +528,7 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             if constexpr (NW == 1)
                 lane_probe<NSEED, PA_SEED_SLOTS>(a, skey, act, f, scls, stp32);
             else
-                lane_probe_k<NSEED, PA_SEED_SLOTS, NW>(a, skk, act, f, scls, stp32);
+                lane_probe_k<NSEED, NW == 3 ? 1 : PA_SEED_SLOTS, NW>(a, skk, act, f, scls, stp32);  // (NW 3: registers)
             sfound |= f;
             bool spec = false;
 #pragma unroll
@@ -779,7 +780,11 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
             // (one 8-B load either way, 4-B aligned, no branch: the 12-B form's
             // 32-bit words loaded under a branch waited one by one)
             uint64_t v8;
-            if constexpr (NW == 2) {  // (two-word keys: 64-bit words of present neighbours, k <= 63 windows)
+            if constexpr (NW == 3) {  // (three-word keys: the position's summary bit of this substitution)
+                const uint64_t p = (uint64_t)A + e;
+                v8 = (((const uint32_t *)a.tile_nb)[p >> 3] >> (4 * (p & 7) + c)) & 1u;
+                nv[u] = v8;
+            } else if constexpr (NW == 2) {  // (two-word keys: 64-bit words of present neighbours, k <= 63 windows)
                 v8 = ((const uint64_t *)a.tile_nb)[ni];
                 nv[u] = v8;
             } else {
@@ -799,6 +804,20 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
             if (sf[u] == 1000) continue;
             // present, present and specific (the 32-bit form: present only)
             const int32_t sft = sf[u];
+            if constexpr (NW == 3) {  // (a set summary bit: every window holding the mismatch may be present)
+                if (nv[u]) {
+                    const int32_t lo = sft < 0 ? 0 : sft, hi = sft + k - 1 < (int32_t)W - 1 ? sft + k - 1 : (int32_t)W - 1;
+                    if (lo <= hi) {
+                        NP0 |= lo < 64 ? ((~0ull << lo) & (hi >= 63 ? ~0ull : ((2ull << hi) - 1))) : 0ull;
+                        NP1 |= hi >= 64 ? ((lo <= 64 ? ~0ull : (~0ull << (lo - 64))) &
+                                           (hi >= 127 ? ~0ull : ((2ull << (hi - 64)) - 1)))
+                                        : 0ull;
+                    }
+                }
+                NS0 = NP0;
+                NS1 = NP1;
+                continue;
+            }
             if constexpr (NW == 2) {  // (present only; up to 63 windows: bits reach the second word from any sft > 0)
                 const uint64_t nbw = nv[u];
                 if (sft >= 0) {
@@ -1196,7 +1215,7 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
         for (int i = 0; i < NPR; i++) {
             const uint32_t e = 64 * i + lane;
             if constexpr (NW == 1) key4[i] = 0;
-            else kk4[i].w[0] = kk4[i].w[1] = 0;
+            else kk4[i] = Key<NW>{};
             tag4[i] = 0;
             if (e < cnt) {
                 const uint32_t t = LW.list[e];
@@ -1222,8 +1241,10 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
                     uint64_t wi;
                     if constexpr (NW == 1)
                         bloom_word(key4[i], a.k, a.bloom_lg, wi, bm[i]);
-                    else
+                    else if constexpr (NW == 2)
                         bloom_word2(kk4[i], a.bloom_lg, wi, bm[i]);
+                    else
+                        bloom_word3(kk4[i], a.bloom_lg, wi, bm[i]);
                     bw[i] = a.bloom[bit(act, i) ? wi : 0ull];  // (no branch around the load: they issue together)
                     if (!bit(act, i)) bm[i] = 0;
                 }
@@ -1278,7 +1299,7 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
 #endif
 template <bool NEED_Q, bool WIN_Q, bool MG, int NM = 2, int NW = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
-    NM == 4 ? PA_LANE_WAVES_LONG : ((WIN_Q || MG || NW == 2) ? PA_LANE_WAVES_Q : PA_LANE_WAVES))))
+    NM == 4 ? PA_LANE_WAVES_LONG : ((WIN_Q || MG || NW >= 2) ? PA_LANE_WAVES_Q : PA_LANE_WAVES))))
 void k_align_lane(AlignArgs a) {
     using LW_t = LaneWave<NM>;
     constexpr int NWD = LaneShape<NM>::NWD;

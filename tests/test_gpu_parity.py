@@ -213,6 +213,10 @@ SYNTH = [
     (4, 6000, 2, 0.02, 75, 1000, 150, 0.005, [dict(), dict(m=0, p=0), dict(mkq=58, mg=1)]),
     (4, 6000, 2, 0.02, 100, 1000, 150, 0.005, [dict(), dict(m=0, p=0)]),
     (4, 6000, 2, 0.02, 75, 800, 250, 0.005, [dict(), dict(m=0, p=0), dict(mrq=57, mkq=58, mg=1)]),  # 250 bp
+    # three-word keys on the lane kernel (63 < k <= 95: neighbour summaries, sibling walks)
+    (25, 40000, 5, 0.01, 75, 8000, 150, 0.015, [dict(), dict(m=0, p=0), dict(mg=2), dict(m=2, p=0), dict(mg=1),
+                                                 dict(mrq=58, mkq=59, mg=2), dict(mkq=60)]),
+    (12, 20000, 4, 0.02, 95, 3000, 150, 0.01, [dict(), dict(m=0, p=-1), dict(mg=3), dict(mkq=59)]),
     (3, 4000, 1, 0.0, 17, 1500, 40, 0.02, [dict(), dict(mkq=55)]),
     (70, 3000, 10, 0.01, 15, 3000, 80, 0.01, [dict(), dict(m=0, p=0)]),  # many genomes per class
     # families (1% apart) and 1.5% read errors: off-walk k-mers, sibling walks,
@@ -270,7 +274,7 @@ def test_fast_kernel_vs_oracle(cfg):
                                         mkq=full["mkq"], mg=full["mg"]), idents, full["mrq"], full["mkq"], full["mg"])
 
 
-NO_NB = [c for c in SYNTH if c[4] <= 63 and c[0] in (12, 25, 500, 70, 5)]
+NO_NB = [c for c in SYNTH if c[4] <= 95 and c[0] in (12, 25, 500, 70, 5)]
 
 
 @pytest.mark.parametrize("cfg", NO_NB, ids=[f"G{c[0]}_k{c[4]}_L{c[6]}" for c in NO_NB])
@@ -743,7 +747,7 @@ def test_reverse_strand_walk_vs_oracle(ps, rcwalk, monkeypatch):
     assert o.stats[2] > 10000  # mostly unmapped reverse-strand reads: the case under test
 
 
-@pytest.mark.parametrize("k", [3, 4, 5, 8, 11, 16, 21, 28, 31, 32, 33, 40, 47, 63])
+@pytest.mark.parametrize("k", [3, 4, 5, 8, 11, 16, 21, 28, 31, 32, 33, 40, 47, 63, 64, 67, 75, 90, 95])
 def test_quality_masks_every_k_vs_oracle(k):
     """k_quality_masks (the lane kernels' --min-read-quality / --min-kmer-quality
     pre-pass: 16-B chunks realigned to the read, the bytes k earlier by a second
