@@ -844,7 +844,13 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
             b.queue_na = a.queue_na2;
             b.queue_na_count = a.queue_na2_count;
         }
-        auto na = win_q ? (mg ? k_align_lane_na<true, true, true> : k_align_lane_na<true, true, false>)
+        auto na = nw == 3 ? (win_q ? (mg ? k_align_lane_naw<true, true, true, 3> : k_align_lane_naw<true, true, false, 3>)
+                             : need_q ? (mg ? k_align_lane_naw<true, false, true, 3> : k_align_lane_naw<true, false, false, 3>)
+                                      : (mg ? k_align_lane_naw<false, false, true, 3> : k_align_lane_naw<false, false, false, 3>))
+                : nw == 2 ? (win_q ? (mg ? k_align_lane_naw<true, true, true, 2> : k_align_lane_naw<true, true, false, 2>)
+                             : need_q ? (mg ? k_align_lane_naw<true, false, true, 2> : k_align_lane_naw<true, false, false, 2>)
+                                      : (mg ? k_align_lane_naw<false, false, true, 2> : k_align_lane_naw<false, false, false, 2>))
+                : win_q ? (mg ? k_align_lane_na<true, true, true> : k_align_lane_na<true, true, false>)
                 : need_q ? (mg ? k_align_lane_na<true, false, true> : k_align_lane_na<true, false, false>)
                          : (mg ? k_align_lane_na<false, false, true> : k_align_lane_na<false, false, false>);
         int na_cu = 0;
@@ -1176,7 +1182,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             // reads without a seed in the index: k_align_lane_na (with a Bloom filter; PA_LANE_NOANCHOR=0/1)
             bool na = a.bloom != nullptr;
             if (const char *e = std::getenv("PA_LANE_NOANCHOR")) na = e[0] == '1';
-            if (idx->nw != 1) na = false;  // (the reverse-strand / Bloom-group kernels take single-word keys)
+            if (idx->nw > 3) na = false;  // (two- and three-word keys: k_align_lane_naw)
             a.queue_na = na ? idx->queue_na : nullptr;
             a.queue_na_count = idx->na_count;
             // their reverse-complement seeds (k_rc_seeds -> k_align_lane_rc):

@@ -1959,6 +1959,128 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
     }
 }
 
+// k_align_lane_naw: k_align_lane_na for keys of two and three words (31 < k
+// <= 95): the reads none of whose seeds is in the index -- at k = 75 with 150-bp
+// reads 7 % of them at 0.5 % errors, since an error in windows 56 .. 74 and
+// another past 74 leave no seed (often no window at all) clean.  Every window
+// (but those failing --min-kmer-quality) is tested against the Bloom filter,
+// eight loads in flight (a window's word is chosen by its key's hash:
+// bloom_word2 / bloom_word3), then the table for the few it lets through;
+// nothing found: UNMAPPED, only multi-genome k-mers: AMBIGUOUS with an empty
+// list, a specific one: the wave kernel (src/kmer.py:410-461).
+template <bool NEED_Q, bool WIN_Q, bool MG, int NW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WAVES))) void k_align_lane_naw(AlignArgs a) {
+    static_assert(NW == 2 || NW == 3, "multi-word keys");
+    __shared__ uint64_t rows[kBlock][kLaneWords + 1];
+    rows[threadIdx.x][kLaneWords] = 0;
+    const int lane = lane_id();
+    const uint64_t n = *a.queue_na_count;
+    const bool forward = n < a.na_min;  // (few such reads: on to the wave kernel, as k_align_lane_na)
+    uint32_t n_amb = 0, n_unm = 0;
+    uint32_t hr_sum = 0, qf_sum = 0;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); c0 < n;
+         c0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i = c0 + lane;
+        LaneRead<2> S;
+        S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
+        uint32_t r = 0;
+        if (i < n) {
+            r = a.queue_na[i];
+            if (forward) S.kind = LANE_HARD;
+            else lane_prep<2, NEED_Q, WIN_Q, false, NW>(a, r, ~0ull, rows[threadIdx.x], S);
+        }
+        if (S.kind == LANE_WALK) {
+            const uint64_t *row = rows[threadIdx.x];
+            const uint32_t W = S.W;
+            uint64_t pm0 = 0, pm1 = 0;  // windows the filter lets through
+            if (!a.bloom) {  // (no filter, PA_LANE_NOANCHOR=1 forced: every window is looked up)
+                pm0 = W >= 64 ? ~0ull : ((1ull << W) - 1);
+                pm1 = W <= 64 ? 0ull : (W >= 128 ? ~0ull : ((1ull << (W - 64)) - 1));
+                if (WIN_Q) {
+                    pm0 &= ~S.F[0];
+                    pm1 &= ~S.F[1];
+                }
+            }
+#pragma unroll 1
+            for (uint32_t w0 = 0; a.bloom && w0 < W; w0 += 8) {
+                uint64_t bw[8], bm[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t w = w0 + j;
+                    const bool filt = WIN_Q && (((w < 64 ? S.F[0] >> w : S.F[1] >> (w - 64)) & 1ull) != 0);
+                    bm[j] = 0;
+                    uint64_t wi = 0;
+                    if (w < W && !filt) {
+                        const Key<NW> K = row_key<NW>(row, w, a.k);
+                        if constexpr (NW == 2)
+                            bloom_word2(K, a.bloom_lg, wi, bm[j]);
+                        else
+                            bloom_word3(K, a.bloom_lg, wi, bm[j]);
+                    }
+                    bw[j] = a.bloom[wi];  // (every load issued before any is tested)
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t w = w0 + j;
+                    if (bm[j] && (bw[j] & bm[j]) == bm[j]) {
+                        if (w < 64) pm0 |= 1ull << w;
+                        else pm1 |= 1ull << (w - 64);
+                    }
+                }
+            }
+            bool spec = false;
+            uint32_t noff = 0, hr = 0;
+#pragma unroll 1
+            while ((pm0 | pm1) && !spec) {
+                Key<NW> key[4];
+                uint32_t act4 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const bool lo = pm0 != 0;
+                    const uint64_t m = lo ? pm0 : pm1;
+                    const uint32_t w = (lo ? 0u : 64u) + (uint32_t)__builtin_ctzll(m | (1ull << 63));
+                    act4 |= m ? 1u << j : 0u;
+                    key[j] = m ? row_key<NW>(row, w, a.k) : Key<NW>{};
+                    if (lo) pm0 &= pm0 - 1;
+                    else pm1 &= pm1 - 1;
+                }
+                uint32_t f, cl[4], tp[4];
+                lane_probe_k<4, 1, NW>(a, key, act4, f, cl, tp);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (!bit(f, j)) continue;
+                    if (MG && (int64_t)class_size_of(cl[j], a.G, a.class_genomes) > (int64_t)a.prm.mg) hr++;
+                    else if (cls_of(cl[j]) >= a.G) noff++;
+                    else spec = true;
+                }
+            }
+            S.kind = spec ? LANE_HARD : (noff ? LANE_AMB : LANE_UNMAPPED);
+            if (!spec) {
+                hr_sum += hr;
+                qf_sum += S.qf;
+            }
+        }
+        const bool hard = S.kind == LANE_HARD;
+        const uint64_t hb = __ballot(hard);
+        if (hb) {
+            uint64_t qbase = 0;
+            if (lane == __builtin_ctzll(hb)) qbase = atomicAdd(a.queue_hard_count, (unsigned long long)__popcll(hb));
+            qbase = shfl64(qbase, __builtin_ctzll(hb));
+            if (hard) a.queue_hard[qbase + lanes_below(hb)] = r;
+        }
+        n_amb += (uint32_t)__popcll(__ballot(S.kind == LANE_AMB));
+        n_unm += (uint32_t)__popcll(__ballot(S.kind == LANE_UNMAPPED));
+    }
+    const uint32_t hr_w = wave_sum(hr_sum);
+    const uint32_t qf_w = WIN_Q ? wave_sum(qf_sum) : 0u;
+    if (lane == 0) {
+        if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
+        if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
+        if (MG && hr_w) atomicAdd(&a.stats[5], (unsigned long long)hr_w);
+        if (WIN_Q && qf_w) atomicAdd(&a.stats[4], (unsigned long long)qf_w);
+    }
+}
+
 // k_rc_seeds: the reverse-complement seeds of the reads k_align_lane found no
 // seed for (their keys come with the queue: a.queue_na_keys, made while the
 // read was packed), kSeedReads reads per thread: a read with one

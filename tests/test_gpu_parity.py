@@ -671,12 +671,14 @@ def test_quality_thresholds_no_read_can_fail(mrq, mkq, monkeypatch):
     assert out[0] == [o.stats.tolist(), o.unique.tolist(), o.ambiguous.tolist(), ofk.tolist()]
 
 
+@pytest.mark.parametrize("k", [31, 45, 75])
 @pytest.mark.parametrize("noanchor", ["1", "0", "1-nobloom"])
 @pytest.mark.parametrize("ps", [dict(), dict(m=0, p=0), dict(mg=2), dict(mrq=58, mkq=60, mg=5), dict(p=-1)])
-def test_unanchored_reads_vs_oracle(ps, noanchor, monkeypatch):
+def test_unanchored_reads_vs_oracle(ps, noanchor, k, monkeypatch):
     """Reads with no seed in the index -- reverse-complemented reads (forward-only
     lookups) and reads of an unindexed organism, 1.5 % substitutions -- checked
-    window by window by k_align_lane_na (PA_LANE_NOANCHOR=1, the default with a
+    window by window by k_align_lane_na (k = 31) / k_align_lane_naw (two- and
+    three-word keys, k = 45 / 75) (PA_LANE_NOANCHOR=1, the default with a
     Bloom filter; PA_NA_MIN=0 so that it takes them however few) or left to the
     wave kernel (0): both equal the oracle, with and without the Bloom filter."""
     monkeypatch.setenv("PA_LANE_NOANCHOR", noanchor[0])
@@ -685,8 +687,8 @@ def test_unanchored_reads_vs_oracle(ps, noanchor, monkeypatch):
         monkeypatch.setenv("PA_BLOOM_MB", "0")
     gens = synth.family_genomes(12, 30000, seed=61, family_size=4, sub_rate=0.01, conserved_len=800,
                                 n_rate=2e-4, n_run=8)
-    index = N.Index(gens, 31)
-    oix = O.OracleIndex(gens, 31)
+    index = N.Index(gens, k)
+    oix = O.OracleIndex(gens, k)
     reads = N.Reads.synthesize(index, 20000, 150, first_read=0, seed=62, sub_rate=0.015, rc_rate=0.3,
                                foreign_rate=0.3)
     s, q, off = reads.download()
