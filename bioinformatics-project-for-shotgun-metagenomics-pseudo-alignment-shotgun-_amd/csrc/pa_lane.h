@@ -927,8 +927,47 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
     }
 }
 
+// Phase 2 for the 250-bp shape as two walks of the 150-bp shape: windows 0 ..
+// 127 (bases 0 .. 126 + k) from the anchor's genome position A, then windows
+// 128 .. W - 1 (bases 128 ..) from A + 128, each with lane_walk_150's
+// registers (the NM-general walk below held ~40 more and spilled 68-76
+// B/lane).  The halves' walked windows are distinct k-mers exactly as one
+// walk's are: a window whose k-mer starts again within 255 positions -- any
+// other window of the read -- carries the local-repeat flag and sends the read
+// to the wave kernel; so their counts add, and their unwalked windows are the
+// read's (P words 0-1 and 2-3).  Both halves are placed in the anchor's genome.
+#ifndef PA_LANE_HALVES
+#define PA_LANE_HALVES 1
+#endif
+template <bool MG>
+__device__ __forceinline__ void lane_walk_halves(const AlignArgs &a, const uint64_t *row, LaneRead<4> &S) {
+    LaneRead<2> H;
+    H.kind = LANE_WALK;
+    H.len = S.W > 128 ? 127 + (uint32_t)a.k : S.len;
+    H.W = S.W > 128 ? 128u : S.W;
+    H.anc = S.anc;
+    H.acls = S.acls;
+    H.F[0] = H.F[1] = 0;
+    lane_walk_150<false, MG, 1>(a, row, H);
+    S.g = H.g;
+    S.kind = H.kind;
+    S.nspec = H.nspec, S.nincl = H.nincl, S.hr = H.hr, S.uoff = H.uoff;
+    S.P[0] = H.P[0], S.P[1] = H.P[1], S.P[2] = S.P[3] = 0;
+    if (S.kind != LANE_WALK || S.W <= 128) return;
+    const int64_t A = (int64_t)(S.anc & kPosMask) - (int64_t)(S.anc >> 40);  // genome position of window 0
+    H.len = S.len - 128;
+    H.W = S.W - 128;
+    H.anc = (uint64_t)(A + 128);  // (window 0 of the second half at A + 128; A >= 0: the first half checked it)
+    H.acls = S.g;                 // (the first half's genome: a genome id < G)
+    lane_walk_150<false, MG, 1>(a, row + 4, H);
+    S.kind = H.kind;
+    S.nspec += H.nspec, S.nincl += H.nincl, S.hr += H.hr, S.uoff += H.uoff;
+    S.P[2] = H.P[0], S.P[3] = H.P[1];
+}
+
 // Phase 2 for the 250-bp shape (NM = 4; lane_walk_150 below states the steps):
-// the same walk over NM-word window masks.
+// the same walk over NM-word window masks (PA_LANE_HALVES=0; else
+// lane_walk_halves).
 template <int NM, bool WIN_Q, bool MG>
 __device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_t *row, LaneRead<NM> &S) {
     using SH = LaneShape<NM>;
@@ -1366,7 +1405,10 @@ void k_align_lane(AlignArgs a) {
                 if constexpr (NM == 2)
                     lane_walk_150<WIN_Q, MG, NW>(a, LW.R[lane], S);
                 else
-                    lane_walk_long<NM, WIN_Q, MG>(a, LW.R[lane], S);
+                    if constexpr (NM == 4 && !WIN_Q && NW == 1 && PA_LANE_HALVES)
+                        lane_walk_halves<MG>(a, LW.R[lane], S);
+                    else
+                        lane_walk_long<NM, WIN_Q, MG>(a, LW.R[lane], S);
             }
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
