@@ -941,28 +941,39 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
 #endif
 template <bool MG>
 __device__ __forceinline__ void lane_walk_halves(const AlignArgs &a, const uint64_t *row, LaneRead<4> &S) {
-    LaneRead<2> H;
-    H.kind = LANE_WALK;
-    H.len = S.W > 128 ? 127 + (uint32_t)a.k : S.len;
-    H.W = S.W > 128 ? 128u : S.W;
-    H.anc = S.anc;
-    H.acls = S.acls;
-    H.F[0] = H.F[1] = 0;
-    lane_walk_150<false, MG, 1>(a, row, H);
-    S.g = H.g;
-    S.kind = H.kind;
-    S.nspec = H.nspec, S.nincl = H.nincl, S.hr = H.hr, S.uoff = H.uoff;
-    S.P[0] = H.P[0], S.P[1] = H.P[1], S.P[2] = S.P[3] = 0;
-    if (S.kind != LANE_WALK || S.W <= 128) return;
     const int64_t A = (int64_t)(S.anc & kPosMask) - (int64_t)(S.anc >> 40);  // genome position of window 0
-    H.len = S.len - 128;
-    H.W = S.W - 128;
-    H.anc = (uint64_t)(A + 128);  // (window 0 of the second half at A + 128; A >= 0: the first half checked it)
-    H.acls = S.g;                 // (the first half's genome: a genome id < G)
-    lane_walk_150<false, MG, 1>(a, row + 4, H);
-    S.kind = H.kind;
-    S.nspec += H.nspec, S.nincl += H.nincl, S.hr += H.hr, S.uoff += H.uoff;
-    S.P[2] = H.P[0], S.P[3] = H.P[1];
+    const uint32_t len = S.len, W = S.W;
+    S.nspec = S.nincl = S.hr = S.uoff = 0;
+    S.P[2] = S.P[3] = 0;
+    // (one copy of the walk in a loop, not two inlined ones: the copies' loop
+    // invariants were hoisted side by side and spilled)
+#pragma unroll 1
+    for (uint32_t h = 0; h < 2; h++) {
+        LaneRead<2> H;
+        H.kind = LANE_WALK;
+        H.F[0] = H.F[1] = 0;
+        if (h == 0) {
+            H.len = W > 128 ? 127 + (uint32_t)a.k : len;
+            H.W = W > 128 ? 128u : W;
+            H.anc = S.anc;
+            H.acls = S.acls;
+        } else {
+            H.len = len - 128;
+            H.W = W - 128;
+            H.anc = (uint64_t)(A + 128);  // (window 0 of the second half at A + 128; A >= 0: the first half checked it)
+            H.acls = S.g;                 // (the first half's genome: a genome id < G)
+        }
+        lane_walk_150<false, MG, 1>(a, row + 4 * h, H);
+        if (h == 0) S.g = H.g;
+        S.kind = H.kind;
+        S.nspec += H.nspec, S.nincl += H.nincl, S.hr += H.hr, S.uoff += H.uoff;
+        if (h == 0) {
+            S.P[0] = H.P[0], S.P[1] = H.P[1];
+        } else {
+            S.P[2] = H.P[0], S.P[3] = H.P[1];
+        }
+        if (S.kind != LANE_WALK || W <= 128) break;
+    }
 }
 
 // Phase 2 for the 250-bp shape (NM = 4; lane_walk_150 below states the steps):
@@ -1334,7 +1345,7 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
 #define PA_LANE_WAVES_Q 3
 #endif
 #ifndef PA_LANE_WAVES_LONG
-#define PA_LANE_WAVES_LONG 3  // the 250-bp shape (NM = 4: ~191-210 VGPRs; it spills 104-228 B/lane, but runs 1.15x faster than at 2 waves)
+#define PA_LANE_WAVES_LONG 4  // the 250-bp shape (NM = 4, two 150-bp walks: 128 VGPRs, no scratch; c2l250 1.57 vs 1.45 G reads/s at 3 waves)
 #endif
 template <bool NEED_Q, bool WIN_Q, bool MG, int NM = 2, int NW = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
