@@ -681,7 +681,11 @@ __device__ __forceinline__ void shifted_planes(const uint64_t (&p)[NM + 1], uint
 template <bool WIN_Q, bool MG, int NW = 1>
 __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t *row, LaneRead<2> &S) {
     const int k = a.k;
-    const uint32_t W = S.W, len = S.len;
+    uint32_t W = S.W, len = S.len;
+    // (opaque here: the masks made from len and W -- per-word tails, window
+    // ranges -- are then made in each walk, not hoisted out of the kernel's
+    // read loop and kept, spilled, through the probe phases)
+    asm volatile("" : "+v"(W), "+v"(len));
     const uint64_t atp = S.anc & kPosMask;
     const int64_t A = (int64_t)atp - (int64_t)(S.anc >> 40);  // genome position of window 0
     const bool in_tile = A >= 0 && (uint64_t)A + W <= a.tile_n;
@@ -1342,14 +1346,21 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
 #endif
 
 #ifndef PA_LANE_WAVES_Q
-#define PA_LANE_WAVES_Q 3
+#define PA_LANE_WAVES_Q 4  // (--min-kmer-quality: 128 VGPRs, 12 B/lane of scratch; c3raw +1 % vs 3 waves at 140 VGPRs)
 #endif
 #ifndef PA_LANE_WAVES_LONG
 #define PA_LANE_WAVES_LONG 4  // the 250-bp shape (NM = 4, two 150-bp walks: 128 VGPRs, no scratch; c2l250 1.57 vs 1.45 G reads/s at 3 waves)
 #endif
+#ifndef PA_LANE_WAVES_MG
+#define PA_LANE_WAVES_MG 4  // --max-genomes (C3): 128 VGPRs, no scratch once the walk's len / W are opaque (round 4: 146-151 at 3)
+#endif
+#ifndef PA_LANE_WAVES_W
+#define PA_LANE_WAVES_W 3  // two- and three-word keys (~168 VGPRs; at 4 they spill 84-180 B/lane)
+#endif
 template <bool NEED_Q, bool WIN_Q, bool MG, int NM = 2, int NW = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
-    NM == 4 ? PA_LANE_WAVES_LONG : ((WIN_Q || MG || NW >= 2) ? PA_LANE_WAVES_Q : PA_LANE_WAVES))))
+    NM == 4 ? PA_LANE_WAVES_LONG
+            : (NW >= 2 ? PA_LANE_WAVES_W : (WIN_Q ? PA_LANE_WAVES_Q : (MG ? PA_LANE_WAVES_MG : PA_LANE_WAVES))))))
 void k_align_lane(AlignArgs a) {
     using LW_t = LaneWave<NM>;
     constexpr int NWD = LaneShape<NM>::NWD;
