@@ -70,6 +70,7 @@ struct AlignArgs {
     const void *tile_nb;            // one-substitution neighbour bits (null: none)
     int nb_spec;                    //   1: 64-bit present | specific << 32, 0: 32-bit present
     const uint32_t *tile_nbbig;     // --max-genomes >= 2: neighbour present with a set > mg (k_nb_big; null: none)
+    const uint4 *tile_nbm;          //   the same interleaved with tile_nb's words (k_nb_merge; null: none)
     int mg_nb;                      // --max-genomes: the neighbour bits tell every present neighbour's set vs mg
     const uint32_t *gblk;           // the genome holding position j << 16 (tiled indexes)
     const uint64_t *bloom;          // Bloom filter of the keys (null: none), 2^bloom_lg words
@@ -310,6 +311,18 @@ __global__ __launch_bounds__(256) void k_tile_big(const uint32_t *__restrict__ t
     }
 }
 
+
+// tile_nb's 64-bit words and tile_nbbig's 32-bit ones interleaved as one 16-B
+// record per (position, substitution), for the walks under --max-genomes: a
+// mismatch then costs the walk one line instead of one in each array.
+__global__ __launch_bounds__(256) void k_nb_merge(const uint64_t *__restrict__ nb, const uint32_t *__restrict__ nbbig,
+                                                  uint64_t n_words, uint4 *__restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_words; i += stride) {
+        const uint64_t v = nb[i];
+        out[i] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), nbbig[i], 0u);
+    }
+}
 
 // The neighbour bits' "set size > mg" half for one --max-genomes value mg >= 2
 // (cached in the index like tile_big): bit i of nbbig[3 p + b] is set when the
@@ -1157,6 +1170,26 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
                         idx->tile_nbbig_mg = a.prm.mg;
                     }
                     a.tile_nbbig = idx->tile_nbbig;
+                    // interleaved with the neighbour words (48 B per base, when it fits; PA_NO_NBM=1: none)
+                    if (idx->tile_nbbig && !std::getenv("PA_NO_NBM")) {
+                        if (!idx->tile_nbm) {
+                            size_t free_b = 0, total_b = 0;
+                            if (pa::dev_mem_info(&free_b, &total_b) == hipSuccess && nw * 16 + (8ull << 30) < free_b &&
+                                pa::dev_malloc(&idx->tile_nbm, nw * 16 + 64) == hipSuccess)
+                                idx->tile_nbm_mg = -1;
+                            else
+                                idx->tile_nbm = nullptr;
+                            (void)hipGetLastError();
+                        }
+                        if (idx->tile_nbm && idx->tile_nbm_mg != a.prm.mg) {
+                            hipLaunchKernelGGL(k_nb_merge, dim3((unsigned)std::min<uint64_t>((nw + 255) / 256, 1u << 20)),
+                                               dim3(256), 0, st, (const uint64_t *)idx->tile_nb, idx->tile_nbbig, nw,
+                                               idx->tile_nbm);
+                            PA_HIP(hipGetLastError());
+                            idx->tile_nbm_mg = a.prm.mg;
+                        }
+                        a.tile_nbm = idx->tile_nbm;
+                    }
                 }
             }
             // every present neighbour's set size vs mg known from the bits

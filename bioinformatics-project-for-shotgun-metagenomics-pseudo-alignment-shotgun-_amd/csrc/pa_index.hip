@@ -1829,6 +1829,9 @@ void index_release(pa_index *idx) {
     pa::dev_free(idx->tile_nbbig);
     idx->tile_nbbig = nullptr;
     idx->tile_nbbig_mg = -1;
+    pa::dev_free(idx->tile_nbm);
+    idx->tile_nbm = nullptr;
+    idx->tile_nbm_mg = -1;
     pa::dev_free(idx->bloom);
     idx->bloom = nullptr;
     pa::dev_free(idx->tile_rcp);

@@ -108,6 +108,8 @@ struct pa_index {
     uint32_t *tile_rcnb = nullptr;     // [3 tile_n] the same for the neighbours' reverse complements (present), optional
     uint32_t *tile_nbbig = nullptr;    // [3 tile_n] neighbour present with a set > tile_nbbig_mg (pa_align, cached)
     int64_t tile_nbbig_mg = -1;
+    uint4 *tile_nbm = nullptr;         // [3 tile_n] {present, specific, set > tile_nbm_mg, 0}: tile_nb and tile_nbbig
+    int64_t tile_nbm_mg = -1;          //   interleaved, one 16-B load per mismatch (pa_align, cached; when it fits)
     int nb_skip = 0;                   // (index_prepare) make the tiles without the neighbour bits
     int nb_pending = 0;                // 1: tiles made, neighbour bits not yet (too few reads expected)
     uint64_t reads_seen = 0;           // reads aligned so far (the neighbour bits follow at kNbReadsPerBase)

@@ -791,14 +791,18 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
             } else if constexpr (NW == 2) {  // (two-word keys: 64-bit words of present neighbours, k <= 63 windows)
                 v8 = ((const uint64_t *)a.tile_nb)[ni];
                 nv[u] = v8;
+            } else if (MG && a.tile_nbm) {  // (the words and the set-size bits in one 16-B record)
+                const uint4 v = a.tile_nbm[ni];
+                nv[u] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                ng[u] = v.z;
             } else {
                 __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
                 nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
             }
-            if (MG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
+            if (MG && (NW != 1 || !a.tile_nbm)) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
                 const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
                 ng[u] = a.tile_nbbig ? gv : 0u;
-            } else {
+            } else if (!MG) {
                 ng[u] = 0u;
             }
             sf[u] = b0 + u < nnb ? (int32_t)e - k + 1 : 1000;  // bit q of the word <-> window e - k + 1 + q
