@@ -2032,7 +2032,12 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         idx->distinct_estimate = distinct;
         const bool forced = free_b == 0;
         if (forced) PA_HIP(pa::dev_mem_info(&free_b, &total_b));
-        for (double mult : {4.0, 2.0, 1.43}) {
+        double mults[4] = {4.0, 2.0, 1.43, 1.43};
+        if (const char *e = std::getenv("PA_CAP_DISTINCT")) {  // A/B: this many slots per distinct k-mer first
+            const double m = std::atof(e);
+            if (m >= 1.2 && m <= 8.0) mults[0] = m, mults[1] = 2.0;
+        }
+        for (double mult : mults) {
             const uint64_t c = (uint64_t)(mult * (double)distinct) + 64;
             if (forced && mult > 1.5) continue;
             if (fits(c)) {
