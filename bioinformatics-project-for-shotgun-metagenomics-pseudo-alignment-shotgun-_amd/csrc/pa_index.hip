@@ -2032,10 +2032,13 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         idx->distinct_estimate = distinct;
         const bool forced = free_b == 0;
         if (forced) PA_HIP(pa::dev_mem_info(&free_b, &total_b));
-        double mults[4] = {4.0, 2.0, 1.43, 1.43};
+        // (2.5 before 2: C5's kept 2.65 G k-mers at load 0.39 instead of 0.48 run 4-7 % faster,
+        // profiles/r05/ab_c5_table.txt -- and build ~1.5 s slower: the larger table leaves the
+        // neighbour words no free range in the slab pool, whose trim then stalls a hipMalloc)
+        double mults[4] = {4.0, 2.5, 2.0, 1.43};
         if (const char *e = std::getenv("PA_CAP_DISTINCT")) {  // A/B: this many slots per distinct k-mer first
             const double m = std::atof(e);
-            if (m >= 1.2 && m <= 8.0) mults[0] = m, mults[1] = 2.0;
+            if (m >= 1.2 && m <= 8.0) mults[0] = m, mults[1] = 2.0, mults[2] = 1.43;
         }
         for (double mult : mults) {
             const uint64_t c = (uint64_t)(mult * (double)distinct) + 64;
