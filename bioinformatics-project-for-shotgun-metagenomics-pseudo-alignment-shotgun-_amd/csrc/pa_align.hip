@@ -163,56 +163,57 @@ constexpr int kQmDwords = 44;  // 176 bytes
 template <int KQ>
 __device__ __forceinline__ void quality_read(const uint8_t *__restrict__ qual, uint64_t o, uint32_t len, int k,
                                              uint32_t T, int64_t mrq, uint32_t flags, uint4 &mask, uint8_t &drop) {
-    const uint64_t o0 = o & ~15ull;
-    const uint32_t shift = (uint32_t)(o & 15);
-    const uint4 *sp = (const uint4 *)(qual + o0);
-    uint32_t dw[kQmDwords + 8];
+    // 16-B loads from the read's first dword (global loads need 4-B alignment
+    // only), all twelve: the read buffers carry kReadPad bytes past the last read
+    const uint4 *sp = (const uint4 *)(qual + (o & ~3ull));
+    const uint32_t sb = 8 * (uint32_t)(o & 3);
+    uint32_t dw[kQmDwords + 4];
 #pragma unroll
-    for (int c = 0; c < (kQmDwords + 8) / 4; c++) {
-        const uint4 v = 16u * c < shift + len ? sp[c] : make_uint4(0, 0, 0, 0);
+    for (int c = 0; c < (kQmDwords + 4) / 4; c++) {
+        const uint4 v = sp[c];
         dw[4 * c] = v.x, dw[4 * c + 1] = v.y, dw[4 * c + 2] = v.z, dw[4 * c + 3] = v.w;
     }
     // rd[j] = bytes 4j .. 4j + 3 of the read
-    const uint32_t s4 = shift >> 2, sb = 8 * (shift & 3);
     uint32_t rd[kQmDwords];
-    {
-        uint32_t lo = s4 == 0 ? dw[0] : s4 == 1 ? dw[1] : s4 == 2 ? dw[2] : dw[3];
 #pragma unroll
-        for (int j = 0; j < kQmDwords; j++) {
-            const uint32_t hi = s4 == 0 ? dw[j + 1] : s4 == 1 ? dw[j + 2] : s4 == 2 ? dw[j + 3] : dw[j + 4];
-            rd[j] = __builtin_amdgcn_alignbit(hi, lo, sb);
-            lo = hi;
-        }
-    }
-    // total of the read's bytes: the whole dwords below len >> 2, then the rest
+    for (int j = 0; j < kQmDwords; j++) rd[j] = __builtin_amdgcn_alignbit(dw[j + 1], dw[j], sb);
+    // total of the read's bytes: the sum of the whole dwords below len >> 2
+    // (selected, no branch), then the rest
     const uint32_t nfull = len >> 2, pmask = (len & 3) ? (1u << (8 * (len & 3))) - 1 : 0u;
     uint32_t run_tot = 0, total = 0, part = 0;
 #pragma unroll
     for (int j = 0; j < kQmDwords; j++) {
-        if ((uint32_t)j == nfull) total = run_tot, part = rd[j];
+        const bool at = (uint32_t)j == nfull;
+        total = at ? run_tot : total;
+        part = at ? rd[j] : part;
         run_tot = __builtin_amdgcn_sad_u8(rd[j], 0u, run_tot);
     }
-    if (nfull >= (uint32_t)kQmDwords) total = run_tot;
+    total = nfull >= (uint32_t)kQmDwords ? run_tot : total;
     total = __builtin_amdgcn_sad_u8(part & pmask, 0u, total);
     drop = ((flags & 1u) && (int64_t)total < mrq * (int64_t)len) ? 1 : 0;
     mask = make_uint4(0, 0, 0, 0);
     if (!(flags & 2u) || len < (uint32_t)k) return;
     // E bit i: the window ending at byte i fails (its sum < T); bytes i - k
-    // from rk (0 before the read)
+    // from rk (0 before the read).  run carries the window sum minus T, whose
+    // sign is the test (sums and T < 2^31); each sign bit is shifted in at the
+    // bottom of e (v_alignbit: e << 1 | run >> 31), so a word is built
+    // bit-reversed and turned round once.
     const uint32_t kb = 8 * ((uint32_t)k & 3);
     uint32_t E[kQmDwords / 8 + 3] = {};  // (+2 zero words: the shift by up to k - 1 = 94 bits below)
-    uint32_t run = 0;
+    uint32_t run = 0u - T, e = 0;
 #pragma unroll
     for (int j = 0; j < kQmDwords; j++) {
         const uint32_t a1 = j - KQ >= 0 ? rd[j - KQ] : 0u, a0 = j - KQ - 1 >= 0 ? rd[j - KQ - 1] : 0u;
         const uint32_t rk = kb ? __builtin_amdgcn_alignbit(a1, a0, 32 - kb) : a1;
 #pragma unroll
         for (int b = 0; b < 4; b++) {
-            const int i = 4 * j + b;
             run += ((rd[j] >> (8 * b)) & 255u) - ((rk >> (8 * b)) & 255u);
-            E[i >> 5] |= ((run - T) >> 31) << (i & 31);  // (run, T < 2^31)
+            e = __builtin_amdgcn_alignbit(e, run, 31);
         }
+        if (j % 8 == 7) E[j / 8] = __builtin_bitreverse32(e), e = 0;
     }
+    static_assert(kQmDwords % 8 == 4, "the last mask word holds 16 window ends");
+    E[kQmDwords / 8] = __builtin_bitreverse32(e << 16);
     // only windows inside the read (ends k - 1 .. len - 1), bit w = the window starting at w
 #pragma unroll
     for (int d = 0; d <= kQmDwords / 8; d++) {
