@@ -524,7 +524,17 @@ pa_status next_batch(Pgz &g) {
         uint64_t bp = c.start;
         Tables tb;
         const uint64_t lim = stop[i] != ~0ull ? stop[i] : batch_end;
-        const uint64_t cap = std::max<uint64_t>(256ull << 20, 64 * (lim - c.start) / 8 + (1u << 20));
+        // Symbols a chunk may decode before it is given up.  Chunk 0 starts at a
+        // boundary a sequential decode reached: its text is real, and only
+        // input above 64:1 fails it (the caller then inflates with zlib).  The
+        // others start where phase A found a header, possibly a false start:
+        // they are held to 16x their compressed bits (FASTQ deflates ~4:1),
+        // 16-64 M symbols -- one that stops there leaves its range to chunk 0
+        // of the next batch, so the cap bounds the batch's host memory (T x
+        // 2 x 128 MB at most) without failing any input.
+        const uint64_t cbytes = (lim - c.start) / 8;
+        const uint64_t cap = i == 0 ? std::max<uint64_t>(256ull << 20, 64 * cbytes + (1u << 20))
+                                    : std::min<uint64_t>(64ull << 20, std::max<uint64_t>(16ull << 20, 16 * cbytes + (1u << 20)));
         while (bp < lim) {
             bool fin = false;
             if (decode_block(g.in, bp, c.out, fin, tb, cap) != B_OK) {

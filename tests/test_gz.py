@@ -61,6 +61,22 @@ def test_inflate_equals_python_gzip(case, chunk_kb, tmp_path, monkeypatch):
         assert got == want, (name, threads)
 
 
+def test_ratio_above_the_speculative_cap(tmp_path, monkeypatch):
+    """Text at ~1000:1: chunks started by the header search are held to 16-64 M
+    symbols (pa_pgz.cpp phase B, the batch's host-memory bound), stop there and
+    leave their range to the next batch's first chunk -- the text is still
+    exact, on any thread count."""
+    monkeypatch.setenv("PA_PGZ_CHUNK_KB", "64")
+    line = b"@r\n" + b"A" * 4000 + b"\n+\n" + b"I" * 4000 + b"\n"
+    want = line * 12_000  # 96 MB
+    blob = gzip.compress(want, 9)
+    assert len(want) > 500 * len(blob)
+    p = tmp_path / "ratio.gz"
+    p.write_bytes(blob)
+    for threads in (1, 8):
+        assert N.gz_inflate_file(str(p), len(want), threads=threads) == want
+
+
 def test_damaged_and_truncated_data_refused(tmp_path, monkeypatch):
     monkeypatch.setenv("PA_PGZ_CHUNK_KB", "128")
     blob = CASES[1][1]
