@@ -1268,7 +1268,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
     fprintf(stderr, "[pa_stats] lane: cooperative probes %llu re-anchors %llu neighbour words %llu | pending: invalid %llu "
             "2+ mismatches %llu neighbour present %llu\n", d[18], d[19], d[20], d[21], d[22], d[23]);
     fprintf(stderr, "[pa_stats] lane found: shared-neighbour+specific %llu second-walk specific %llu probed-shared+specific %llu"
-            " | unique by bound %llu, by off-walk count %llu | probes past the Bloom filter %llu\n", d[24], d[25], d[26], d[27], d[28],
+            " | unique by bound %llu, by off-walk counts %llu | probes past the Bloom filter %llu\n", d[24], d[25], d[26], d[27], d[28],
             d[29]);
     fprintf(stderr, "[pa_stats] lane seeds: anchor ranked among stretches %llu, second seed round %llu\n", d[30], d[31]);
 #endif

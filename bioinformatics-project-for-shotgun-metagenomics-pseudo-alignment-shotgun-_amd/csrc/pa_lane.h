@@ -97,8 +97,10 @@ template <int NM>
 struct __align__(16) LaneWave {
     uint64_t R[64][LaneShape<NM>::NWD + 1];  // every lane's packed read (+ a zero word), for keys of listed windows
     unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 40) | position
-    uint32_t flags[64];              // bit 0: specific k-mer found off the walk; bits 2..: unspecific ones found
-    uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
+    uint32_t flags[64];              // bits 16..: specific k-mers found off the walk, 2..15: unspecific ones,
+                                     //   bit 1: the specific ones are of two or more genomes
+    uint32_t hr[64];                 // unwalked windows filtered by --max-genomes; without it, 1 + the
+                                     //   genome of the specific k-mers found off the walk
     uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
     uint32_t again_r[128];           // reads to walk again from a specific k-mer found off their walk,
     unsigned long long again_a[128]; //   and that anchor: (window << 40) | position
@@ -1211,7 +1213,9 @@ __device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_
 
 // Phase 3 (whole wave): probe windows Q of the walking lanes; `reset`
 // clears the lanes' outcomes first (LW.flags / hr / cand accumulate otherwise).
-template <int NM, int NW = 1>
+// TWO: also note the genome of the specific k-mers found (LW.hr, flags bit 1),
+// for k_align_lane's two-genome decision
+template <int NM, int NW = 1, bool TWO = false>
 __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM> &LW, const LaneRead<NM> &S,
                                                 const uint64_t (&Qin)[NM], bool reset) {
     const int lane = lane_id();
@@ -1329,7 +1333,11 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
             } else if (cl >= a.G) {
                 atomicAdd(&LW.flags[o], 4u);  // unspecific: counted in bits 2..
             } else {
-                atomicOr(&LW.flags[o], 1u);
+                atomicAdd(&LW.flags[o], 1u << 16);
+                if (TWO) {  // (specific: the class is the genome) one genome, or bit 1
+                    const uint32_t was = atomicCAS(&LW.hr[o], 0u, cl + 1);
+                    if (was != 0u && was != cl + 1) atomicOr(&LW.flags[o], 2u);
+                }
                 atomicMin(&LW.cand[o], ((unsigned long long)w << 40) | first_pos(c4[i], t4[i], a.G, a.class_genomes,
                                                                                a.goff, a.tpos_local));
             }
@@ -1467,10 +1475,31 @@ void k_align_lane(AlignArgs a) {
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
             }
-            lane_probe_wave<NM, NW>(a, LW, S, S.P, true);
+            lane_probe_wave<NM, NW, !MG && !WIN_Q>(a, LW, S, S.P, true);
             if (S.kind == LANE_WALK) {
                 const uint32_t fl = LW.flags[lane];
-                if (fl & 1u) {  // a specific k-mer off the walk: walk again from it (once)
+                const uint32_t nsoff = fl >> 16;  // specific k-mers off the walk (windows)
+                // Specific k-mers of one other genome h off the walk, fewer than
+                // g's walked ones: with ns = nspec (distinct: no local repeat
+                // among the walked windows) and c = nsoff >= h's distinct
+                // specific k-mers, ns >= c + max(m, 1) makes g the strict top
+                // and unique (src/kmer.py:446-456); any genome's total is then
+                // at most (nincl - nspec) + noff + c and g's at least nincl, so
+                // with noff + c - ns <= p the p-check cannot demote
+                // (src/kmer.py:464-480).  (A specific k-mer of g itself off the
+                // walk may repeat a walked one: not decided here.)
+                bool two = false;
+                if (!MG && !WIN_Q && nsoff && !(fl & 2u) && LW.hr[lane] != S.g + 1) {
+                    const int64_t ns = (int64_t)S.nspec, c = (int64_t)nsoff;
+                    const int64_t noff = (int64_t)(((fl >> 2) & 0x3FFFu) + S.uoff);
+                    two = ns >= c + (a.prm.m > 0 ? a.prm.m : 1) && (a.prm.p < 0 || noff + c - ns <= a.prm.p);
+                }
+                if (two) {
+                    S.kind = LANE_UNIQUE;
+#ifdef PA_STATS
+                    atomicAdd(&a.dbg[24], 1ull);  // (with the one-genome case below)
+#endif
+                } else if (nsoff) {  // a specific k-mer off the walk: walk again from it (once)
 #if defined(PA_STATS) || defined(PA_DISSECT)
                     if (a.dbg_mode == 12) S.kind = LANE_AMB;  // timing dissection: no second walk
 #endif
@@ -1486,8 +1515,8 @@ void k_align_lane(AlignArgs a) {
                         LANE_HARD_WHY(17);
                     }
                 } else {
-                    S.hr += LW.hr[lane];
-                    const uint32_t noff = (fl >> 2) + S.uoff;  // unspecific k-mers off the walk
+                    if (MG) S.hr += LW.hr[lane];
+                    const uint32_t noff = ((fl >> 2) & 0x3FFFu) + S.uoff;  // unspecific k-mers off the walk
                     if (noff) {
                         // Only g has specific k-mers (the walked ones; none off the
                         // walk), so the specific map is {g} and the read is UNIQUE g
