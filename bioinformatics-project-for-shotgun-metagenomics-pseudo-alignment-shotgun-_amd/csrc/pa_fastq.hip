@@ -44,6 +44,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <string>
+#include <deque>
 #include <thread>
 #include <vector>
 
@@ -567,7 +568,38 @@ void prefetch_run(pa_fastq_prefetch *pf) {
         });
     pa_status rc = PA_OK;
     std::string msg;
-    for (uint64_t c = 0; c < nchunk; c++) {
+    // Copies stay queued on the stream, up to `inflight` of them: each chunk's
+    // event is waited for only when its slot is needed again or the next
+    // chunk must be announced (a synchronize after every 8 MiB copy left the
+    // DMA engine idle for a host round trip per chunk).  PA_PREFETCH_INFLIGHT=1
+    // is the one-at-a-time loop.
+    int inflight = 4;
+    if (const char *v = std::getenv("PA_PREFETCH_INFLIGHT")) inflight = std::max(1, std::min(nslot - 1, atoi(v)));
+    std::vector<hipEvent_t> ev(nslot, nullptr);
+    for (int s = 0; s < nslot && e == hipSuccess; s++) e = hipEventCreateWithFlags(&ev[s], hipEventDisableTiming);
+    std::deque<uint64_t> q;  // chunks whose copies are queued, in file order
+    auto retire = [&]() -> hipError_t {  // the oldest queued copy done: its slot free, its bytes announced
+        const uint64_t c0 = q.front();
+        const int s0 = (int)(c0 % nslot);
+        const hipError_t r = hipEventSynchronize(ev[s0]);
+        if (r != hipSuccess) return r;
+        q.pop_front();
+        {
+            std::lock_guard<std::mutex> g(rm);
+            slot_chunk[s0] = -1;
+            slot_free_for[s0] = (int64_t)(c0 + nslot);
+            rcv.notify_all();
+        }
+        std::lock_guard<std::mutex> g(pf->mu);
+        pf->ready = std::min(pf->size, (c0 + 1) * kChunk);
+        pf->cv.notify_all();
+        return hipSuccess;
+    };
+    if (e != hipSuccess) {
+        rc = PA_EDEVICE;
+        msg = std::string("HIP error in the FASTQ prefetch: ") + hipGetErrorString(e);
+    }
+    for (uint64_t c = 0; c < nchunk && rc == PA_OK; c++) {
         const int s = (int)(c % nslot);
         {
             std::unique_lock<std::mutex> g(rm);
@@ -587,24 +619,18 @@ void prefetch_run(pa_fastq_prefetch *pf) {
             pf->est_records = m ? (uint64_t)((double)pf->size * (double)(nl / 4 + 1) / (double)m) : 0;
         }
         e = hipMemcpyAsync(pf->text + a, ring + (uint64_t)s * kChunk, n, hipMemcpyHostToDevice, pf->st);
-        if (e == hipSuccess) e = hipStreamSynchronize(pf->st);
+        if (e == hipSuccess) e = hipEventRecord(ev[s], pf->st);
+        if (e == hipSuccess) q.push_back(c);
+        while (e == hipSuccess && !q.empty() && (q.size() >= (size_t)inflight || c + 1 == nchunk)) e = retire();
         if (e != hipSuccess) {
             rc = PA_EDEVICE;
             msg = std::string("HIP error in the FASTQ prefetch copy: ") + hipGetErrorString(e);
             break;
         }
-        {
-            std::lock_guard<std::mutex> g(rm);
-            slot_chunk[s] = -1;
-            slot_free_for[s] = (int64_t)(c + nslot);
-            rcv.notify_all();
-        }
-        {
-            std::lock_guard<std::mutex> g(pf->mu);
-            pf->ready = a + n;
-            pf->cv.notify_all();
-        }
     }
+    if (rc != PA_OK) hipStreamSynchronize(pf->st);  // (no copy may still read the ring)
+    for (hipEvent_t x : ev)
+        if (x) hipEventDestroy(x);
     {
         std::lock_guard<std::mutex> g(rm);
         abort = true;
