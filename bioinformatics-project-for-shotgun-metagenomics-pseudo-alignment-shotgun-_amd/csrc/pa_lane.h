@@ -83,12 +83,12 @@ constexpr int kPassEntries = 64 * PA_LANE_PROBES;
 // Per-workgroup LDS unique counters up to this many genomes (8 B each: the
 // count and the smallest batch-local read index, < 2^32); above it the lane
 // kernel counts in global memory (two device-scope atomics per unique read, on
-// the same G lines from every CU).  1792: a block's counters and its four
-// waves' LaneWave<2> (26 KB) fit 40 KB, four blocks per CU in 160 KB -- the
+// the same G lines from every CU).  1664: a block's counters and its four
+// waves' LaneWave<2> (27 KB) fit 40 KB, four blocks per CU in 160 KB -- the
 // 4 waves per SIMD of the plain variant.  (Round 4 kept 512 at 12 B each: C5's
 // 1200 kept genomes counted in global memory.)
 #ifndef PA_LANE_LDS_GENOMES
-#define PA_LANE_LDS_GENOMES 1792
+#define PA_LANE_LDS_GENOMES 1664
 #endif
 constexpr uint32_t kLaneLdsGenomeCap = PA_LANE_LDS_GENOMES;
 
@@ -99,8 +99,8 @@ struct __align__(16) LaneWave {
     unsigned long long cand[64];     // a found specific unwalked window per lane: (window << 40) | position
     uint32_t flags[64];              // bits 16..: specific k-mers found off the walk, 2..15: unspecific ones,
                                      //   bit 1: the specific ones are of two or more genomes
-    uint32_t hr[64];                 // unwalked windows filtered by --max-genomes; without it, 1 + the
-                                     //   genome of the specific k-mers found off the walk
+    uint32_t hr[64];                 // unwalked windows filtered by --max-genomes
+    uint32_t gsp[64];                // 1 + the genome of the specific k-mers found off the walk (0: none)
     uint16_t list[kPassEntries];     // pass entries: (lane << 8) | window
     uint32_t again_r[128];           // reads to walk again from a specific k-mer found off their walk,
     unsigned long long again_a[128]; //   and that anchor: (window << 40) | position
@@ -1224,6 +1224,7 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
     if (reset) {
         LW.flags[lane] = 0;
         LW.hr[lane] = 0;
+        if (TWO) LW.gsp[lane] = 0;
         LW.cand[lane] = ~0ull;
     }
     uint64_t Q[NM];
@@ -1335,7 +1336,7 @@ __device__ __forceinline__ void lane_probe_wave(const AlignArgs &a, LaneWave<NM>
             } else {
                 atomicAdd(&LW.flags[o], 1u << 16);
                 if (TWO) {  // (specific: the class is the genome) one genome, or bit 1
-                    const uint32_t was = atomicCAS(&LW.hr[o], 0u, cl + 1);
+                    const uint32_t was = atomicCAS(&LW.gsp[o], 0u, cl + 1);
                     if (was != 0u && was != cl + 1) atomicOr(&LW.flags[o], 2u);
                 }
                 atomicMin(&LW.cand[o], ((unsigned long long)w << 40) | first_pos(c4[i], t4[i], a.G, a.class_genomes,
@@ -1475,7 +1476,7 @@ void k_align_lane(AlignArgs a) {
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
             }
-            lane_probe_wave<NM, NW, !MG && !WIN_Q>(a, LW, S, S.P, true);
+            lane_probe_wave<NM, NW, !WIN_Q>(a, LW, S, S.P, true);
             if (S.kind == LANE_WALK) {
                 const uint32_t fl = LW.flags[lane];
                 const uint32_t nsoff = fl >> 16;  // specific k-mers off the walk (windows)
@@ -1489,13 +1490,14 @@ void k_align_lane(AlignArgs a) {
                 // (src/kmer.py:464-480).  (A specific k-mer of g itself off the
                 // walk may repeat a walked one: not decided here.)
                 bool two = false;
-                if (!MG && !WIN_Q && nsoff && !(fl & 2u) && LW.hr[lane] != S.g + 1) {
+                if (!WIN_Q && (!MG || a.mg_nb) && nsoff && !(fl & 2u) && LW.gsp[lane] != S.g + 1) {
                     const int64_t ns = (int64_t)S.nspec, c = (int64_t)nsoff;
                     const int64_t noff = (int64_t)(((fl >> 2) & 0x3FFFu) + S.uoff);
                     two = ns >= c + (a.prm.m > 0 ? a.prm.m : 1) && (a.prm.p < 0 || noff + c - ns <= a.prm.p);
                 }
                 if (two) {
                     S.kind = LANE_UNIQUE;
+                    if (MG) S.hr += LW.hr[lane];
 #ifdef PA_STATS
                     atomicAdd(&a.dbg[24], 1ull);  // (with the one-genome case below)
 #endif
