@@ -87,6 +87,9 @@ constexpr int kPassEntries = 64 * PA_LANE_PROBES;
 // waves' LaneWave<2> (27 KB) fit 40 KB, four blocks per CU in 160 KB -- the
 // 4 waves per SIMD of the plain variant.  (Round 4 kept 512 at 12 B each: C5's
 // 1200 kept genomes counted in global memory.)
+#ifndef PA_TWO_WINQ
+#define PA_TWO_WINQ 1  // the two-genome decision in the --min-kmer-quality variants too
+#endif
 #ifndef PA_LANE_LDS_GENOMES
 #define PA_LANE_LDS_GENOMES 1664
 #endif
@@ -1476,7 +1479,7 @@ void k_align_lane(AlignArgs a) {
                 LANE_HARD_WHY(7);
                 LANE_HARD_WHY(16);
             }
-            lane_probe_wave<NM, NW, !WIN_Q>(a, LW, S, S.P, true);
+            lane_probe_wave<NM, NW, PA_TWO_WINQ || !WIN_Q>(a, LW, S, S.P, true);
             if (S.kind == LANE_WALK) {
                 const uint32_t fl = LW.flags[lane];
                 const uint32_t nsoff = fl >> 16;  // specific k-mers off the walk (windows)
@@ -1490,7 +1493,7 @@ void k_align_lane(AlignArgs a) {
                 // (src/kmer.py:464-480).  (A specific k-mer of g itself off the
                 // walk may repeat a walked one: not decided here.)
                 bool two = false;
-                if (!WIN_Q && (!MG || a.mg_nb) && nsoff && !(fl & 2u) && LW.gsp[lane] != S.g + 1) {
+                if ((PA_TWO_WINQ || !WIN_Q) && (!MG || a.mg_nb) && nsoff && !(fl & 2u) && LW.gsp[lane] != S.g + 1) {
                     const int64_t ns = (int64_t)S.nspec, c = (int64_t)nsoff;
                     const int64_t noff = (int64_t)(((fl >> 2) & 0x3FFFu) + S.uoff);
                     two = ns >= c + (a.prm.m > 0 ? a.prm.m : 1) && (a.prm.p < 0 || noff + c - ns <= a.prm.p);
