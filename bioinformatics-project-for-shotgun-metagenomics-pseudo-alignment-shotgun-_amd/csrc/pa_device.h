@@ -144,7 +144,17 @@ __device__ __forceinline__ uint64_t window_bits(const uint64_t *bm, uint32_t w, 
     uint32_t q = w >> 6, r = w & 63;
     uint64_t v = bm[q] >> r;
     if (r) v |= bm[q + 1] << (64 - r);
-    return v & ((1ull << k) - 1);
+    return k >= 64 ? v : v & ((1ull << k) - 1);
+}
+
+// Any of the k bits from bit w on set (k up to the widest key, 64 at a time).
+// (Round 5: the wave kernel tested min(k, 64) bits -- and for k >= 64 a
+// shifted-out mask -- so a window of k > 63 with a non-ACGT base past its
+// first 64 positions was looked up with the base as a code.)
+__device__ __forceinline__ bool window_any(const uint64_t *bm, uint32_t w, int k) {
+    for (int o = 0; o < k; o += 64)
+        if (window_bits(bm, w + (uint32_t)o, k - o)) return true;
+    return false;
 }
 
 // Where a key starts probing: multiply-high range reduction of its hash over

@@ -488,7 +488,7 @@ __device__ __forceinline__ bool prep_read(const AlignArgs &a, WaveLds<WPL> &L, W
             S.qf++;
             ok = 0;
         }
-        if (ok && any_bad && window_bits(L.poison, w + shift, k) != 0) ok = 0;
+        if (ok && any_bad && window_any(L.poison, w + shift, k)) ok = 0;
         S.key[j] = extract_key<NW>(L.packed, w + shift, k);
         S.pend |= ok << j;
     }

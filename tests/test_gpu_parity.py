@@ -274,6 +274,90 @@ def test_fast_kernel_vs_oracle(cfg):
                                         mkq=full["mkq"], mg=full["mg"]), idents, full["mrq"], full["mkq"], full["mg"])
 
 
+@pytest.mark.parametrize("k", [31, 45, 75])
+def test_chimeric_reads_of_two_genomes(k):
+    """Reads carrying specific k-mers of two genomes of a family in every
+    proportion -- a stretch of genome A with a stretch of its sibling B at the
+    same coordinates spliced in (1..149 bases), some with a second splice or
+    errors, some with an internal repeat -- against the oracle under m / p
+    sets that put the lane kernel's two-genome decision (ns >= c + max(m, 1),
+    noff + c - ns <= p) on both sides of its bounds."""
+    rng = np.random.default_rng(7 + k)
+    gens = synth.family_genomes(8, 30000, seed=k, family_size=4, sub_rate=0.03, conserved_len=300)
+    L, nr = 150, 6000
+    seq = np.empty((nr, L), dtype=np.uint8)
+    for i in range(nr):
+        fam = rng.integers(0, 2) * 4
+        a, b = fam + rng.choice(4, 2, replace=False)
+        st = int(rng.integers(0, 30000 - L))
+        r = np.asarray(gens[a][st:st + L], dtype=np.uint8).copy()
+        cut = int(rng.integers(1, L))
+        if i % 2:
+            r[cut:] = gens[b][st + cut:st + L]
+        else:
+            r[:cut] = gens[b][st:st + cut]
+        if i % 5 == 0:  # a second splice back to A
+            c2 = int(rng.integers(0, L))
+            r[c2:] = gens[a][st + c2:st + L]
+        if i % 3 == 0:  # sequencing errors
+            for e in rng.integers(0, L, 2):
+                if r[e] in b"ACGT":
+                    r[e] = b"ACGT"[(b"ACGT".index(bytes([r[e]])) + 1) % 4]
+        if i % 17 == 0 and k < 60:  # an internal repeat: one k-mer twice
+            r[L - k:] = r[:k]
+        seq[i] = r
+    qual = np.full((nr, L), ord("I"), dtype=np.uint8)
+    off = np.arange(nr + 1, dtype=np.uint64) * L
+    s, q = seq.reshape(-1), qual.reshape(-1)
+    index = N.Index(gens, k)
+    oix = O.OracleIndex(gens, k)
+    reads = N.Reads.upload(s, q, off)
+    for m, p in ((1, 1), (0, 0), (2, 0), (1, 5), (3, -1), (10, 10)):
+        ores = oix.align(s.tobytes(), q.tobytes(), off, m=m, p=p, read_base=0, detail=False)
+        result = N.Result(index)
+        N.align(index, reads, N.Params.make(m, p, None, None, None), 0, result)
+        stats, uq, am, fk = result.fetch()
+        assert stats.tolist() == ores.stats.tolist(), (m, p)
+        assert uq.tolist() == ores.unique.tolist(), (m, p)
+        assert am.tolist() == ores.ambiguous.tolist(), (m, p)
+        ofk = np.where(ores.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, ores.first_key)
+        assert fk.tolist() == ofk.tolist(), (m, p)
+
+
+@pytest.mark.parametrize("k", [63, 64, 75, 100, 127])
+def test_non_acgt_anywhere_in_long_windows(k):
+    """A non-ACGT base at any position of a window of k > 63 rules the window
+    out (src/kmer.py's N k-mers): reads of two sibling genomes with one or a
+    few N (or other) bytes placed at every offset, so that they fall past the
+    first 64 positions of some windows (the wave kernel once tested only
+    min(k, 64) of them)."""
+    rng = np.random.default_rng(k)
+    gens = synth.family_genomes(6, 20000, seed=k, family_size=3, sub_rate=0.01, conserved_len=200)
+    L = 150
+    reads = []
+    for i in range(3000):
+        g = int(rng.integers(0, 6))
+        st = int(rng.integers(0, 20000 - L))
+        r = np.asarray(gens[g][st:st + L], dtype=np.uint8).copy()
+        for _ in range(1 + i % 3):
+            r[(i * 7 + int(rng.integers(0, 5))) % L] = b"NNNRY"[i % 5]
+        reads.append(r)
+    seq = np.stack(reads)
+    qual = np.full(seq.shape, ord("I"), dtype=np.uint8)
+    off = np.arange(len(reads) + 1, dtype=np.uint64) * L
+    s, q = seq.reshape(-1), qual.reshape(-1)
+    index = N.Index(gens, k)
+    oix = O.OracleIndex(gens, k)
+    for m, p in ((1, 1), (0, 0)):
+        ores = oix.align(s.tobytes(), q.tobytes(), off, m=m, p=p, read_base=0, detail=False)
+        result = N.Result(index)
+        N.align(index, N.Reads.upload(s, q, off), N.Params.make(m, p, None, None, None), 0, result)
+        stats, uq, am, fk = result.fetch()
+        assert stats.tolist() == ores.stats.tolist(), (m, p)
+        assert uq.tolist() == ores.unique.tolist(), (m, p)
+        assert am.tolist() == ores.ambiguous.tolist(), (m, p)
+
+
 NO_NB = [c for c in SYNTH if c[4] <= 95 and c[0] in (12, 25, 500, 70, 5)]
 
 
