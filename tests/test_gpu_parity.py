@@ -358,6 +358,63 @@ def test_non_acgt_anywhere_in_long_windows(k):
         assert am.tolist() == ores.ambiguous.tolist(), (m, p)
 
 
+@pytest.mark.parametrize("k", [31, 45, 75])
+def test_repeats_and_genome_boundaries(k):
+    """Genomes with tandem repeats (a 7-bp and a 40-bp unit, 12-20 copies) and
+    a 300-bp segment copied elsewhere in the same genome and into a sibling,
+    and reads from those regions (k-mers repeated inside a read and inside a
+    genome: the local-repeat flags, quirk 3's distinct k-mers) and reads
+    across the end of one genome and the start of the next (windows that lie
+    in no genome, the walk's genome range), against the oracle."""
+    rng = np.random.default_rng(100 + k)
+    gens = [np.asarray(g, dtype=np.uint8).copy() for g in
+            synth.family_genomes(6, 12000, seed=k + 1, family_size=3, sub_rate=0.02, conserved_len=200)]
+    hot = []
+    for gi, g in enumerate(gens):
+        for unit_len, copies in ((7, 20), (40, 12)):
+            unit = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), unit_len)
+            at = int(rng.integers(500, 11000 - unit_len * copies))
+            g[at:at + unit_len * copies] = np.tile(unit, copies)
+            hot.append((gi, at))
+        src = int(rng.integers(0, 11000))
+        dst = int(rng.integers(0, 11000))
+        g[dst:dst + 300] = g[src:src + 300].copy()
+        hot.append((gi, dst))
+        sib = (gi // 3) * 3 + (gi + 1) % 3
+        gens[sib][src:src + 300] = g[src:src + 300]
+    L = 150
+    reads = []
+    for i in range(4000):
+        if i % 4 == 0:  # across a genome boundary
+            g = int(rng.integers(0, 5))
+            tail = int(rng.integers(1, L))
+            r = np.concatenate([gens[g][len(gens[g]) - tail:], gens[g + 1][:L - tail]])
+        else:
+            gi, at = hot[int(rng.integers(0, len(hot)))]
+            st = int(np.clip(at + rng.integers(-120, 300), 0, 12000 - L))
+            r = gens[gi][st:st + L].copy()
+            if i % 3 == 0:
+                r[int(rng.integers(0, L))] = b"ACGT"[int(rng.integers(0, 4))]
+        reads.append(np.asarray(r, dtype=np.uint8))
+    seq = np.stack(reads)
+    qual = np.full(seq.shape, ord("I"), dtype=np.uint8)
+    off = np.arange(len(reads) + 1, dtype=np.uint64) * L
+    s, q = seq.reshape(-1), qual.reshape(-1)
+    index = N.Index(gens, k)
+    oix = O.OracleIndex(gens, k)
+    assert index.n_kmers == oix.n_kmers
+    for m, p in ((1, 1), (0, 0), (2, 5)):
+        ores = oix.align(s.tobytes(), q.tobytes(), off, m=m, p=p, read_base=0, detail=False)
+        result = N.Result(index)
+        N.align(index, N.Reads.upload(s, q, off), N.Params.make(m, p, None, None, None), 0, result)
+        stats, uq, am, fk = result.fetch()
+        assert stats.tolist() == ores.stats.tolist(), (m, p)
+        assert uq.tolist() == ores.unique.tolist(), (m, p)
+        assert am.tolist() == ores.ambiguous.tolist(), (m, p)
+        ofk = np.where(ores.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, ores.first_key)
+        assert fk.tolist() == ofk.tolist(), (m, p)
+
+
 NO_NB = [c for c in SYNTH if c[4] <= 95 and c[0] in (12, 25, 500, 70, 5)]
 
 
