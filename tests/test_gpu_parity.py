@@ -281,7 +281,8 @@ def test_chimeric_reads_of_two_genomes(k):
     same coordinates spliced in (1..149 bases), some with a second splice or
     errors, some with an internal repeat -- against the oracle under m / p
     sets that put the lane kernel's two-genome decision (ns >= c + max(m, 1),
-    noff + c - ns <= p) on both sides of its bounds."""
+    noff + c - ns <= p) on both sides of its bounds, also under --max-genomes,
+    --min-kmer-quality and --min-read-quality (raw-ASCII qualities ~N(60, 8))."""
     rng = np.random.default_rng(7 + k)
     gens = synth.family_genomes(8, 30000, seed=k, family_size=4, sub_rate=0.03, conserved_len=300)
     L, nr = 150, 6000
@@ -306,22 +307,24 @@ def test_chimeric_reads_of_two_genomes(k):
         if i % 17 == 0 and k < 60:  # an internal repeat: one k-mer twice
             r[L - k:] = r[:k]
         seq[i] = r
-    qual = np.full((nr, L), ord("I"), dtype=np.uint8)
+    qual = np.clip(np.rint(rng.normal(60, 8, size=(nr, L))), 35, 74).astype(np.uint8)
     off = np.arange(nr + 1, dtype=np.uint64) * L
     s, q = seq.reshape(-1), qual.reshape(-1)
     index = N.Index(gens, k)
     oix = O.OracleIndex(gens, k)
     reads = N.Reads.upload(s, q, off)
-    for m, p in ((1, 1), (0, 0), (2, 0), (1, 5), (3, -1), (10, 10)):
-        ores = oix.align(s.tobytes(), q.tobytes(), off, m=m, p=p, read_base=0, detail=False)
+    for m, p, mrq, mkq, mg in ((1, 1, None, None, None), (0, 0, None, None, None), (2, 0, None, None, None),
+                               (1, 5, None, None, None), (3, -1, None, None, None), (10, 10, None, None, None),
+                               (1, 1, None, None, 2), (1, 0, None, 58, None), (1, 1, 57, 58, 3)):
+        ores = oix.align(s.tobytes(), q.tobytes(), off, m=m, p=p, mrq=mrq, mkq=mkq, mg=mg, read_base=0, detail=False)
         result = N.Result(index)
-        N.align(index, reads, N.Params.make(m, p, None, None, None), 0, result)
+        N.align(index, reads, N.Params.make(m, p, mrq, mkq, mg), 0, result)
         stats, uq, am, fk = result.fetch()
-        assert stats.tolist() == ores.stats.tolist(), (m, p)
-        assert uq.tolist() == ores.unique.tolist(), (m, p)
-        assert am.tolist() == ores.ambiguous.tolist(), (m, p)
+        assert stats.tolist() == ores.stats.tolist(), (m, p, mrq, mkq, mg)
+        assert uq.tolist() == ores.unique.tolist(), (m, p, mrq, mkq, mg)
+        assert am.tolist() == ores.ambiguous.tolist(), (m, p, mrq, mkq, mg)
         ofk = np.where(ores.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, ores.first_key)
-        assert fk.tolist() == ofk.tolist(), (m, p)
+        assert fk.tolist() == ofk.tolist(), (m, p, mrq, mkq, mg)
 
 
 @pytest.mark.parametrize("k", [63, 64, 75, 100, 127])
@@ -408,11 +411,11 @@ def test_repeats_and_genome_boundaries(k):
         result = N.Result(index)
         N.align(index, N.Reads.upload(s, q, off), N.Params.make(m, p, None, None, None), 0, result)
         stats, uq, am, fk = result.fetch()
-        assert stats.tolist() == ores.stats.tolist(), (m, p)
-        assert uq.tolist() == ores.unique.tolist(), (m, p)
-        assert am.tolist() == ores.ambiguous.tolist(), (m, p)
+        assert stats.tolist() == ores.stats.tolist(), (m, p, mrq, mkq, mg)
+        assert uq.tolist() == ores.unique.tolist(), (m, p, mrq, mkq, mg)
+        assert am.tolist() == ores.ambiguous.tolist(), (m, p, mrq, mkq, mg)
         ofk = np.where(ores.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, ores.first_key)
-        assert fk.tolist() == ofk.tolist(), (m, p)
+        assert fk.tolist() == ofk.tolist(), (m, p, mrq, mkq, mg)
 
 
 NO_NB = [c for c in SYNTH if c[4] <= 95 and c[0] in (12, 25, 500, 70, 5)]
