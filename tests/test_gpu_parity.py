@@ -274,8 +274,8 @@ def test_fast_kernel_vs_oracle(cfg):
                                         mkq=full["mkq"], mg=full["mg"]), idents, full["mrq"], full["mkq"], full["mg"])
 
 
-@pytest.mark.parametrize("k", [31, 45, 75])
-def test_chimeric_reads_of_two_genomes(k):
+@pytest.mark.parametrize("k,L", [(31, 150), (45, 150), (75, 150), (31, 250), (63, 250)])
+def test_chimeric_reads_of_two_genomes(k, L):
     """Reads carrying specific k-mers of two genomes of a family in every
     proportion -- a stretch of genome A with a stretch of its sibling B at the
     same coordinates spliced in (1..149 bases), some with a second splice or
@@ -285,7 +285,7 @@ def test_chimeric_reads_of_two_genomes(k):
     --min-kmer-quality and --min-read-quality (raw-ASCII qualities ~N(60, 8))."""
     rng = np.random.default_rng(7 + k)
     gens = synth.family_genomes(8, 30000, seed=k, family_size=4, sub_rate=0.03, conserved_len=300)
-    L, nr = 150, 6000
+    nr = 6000
     seq = np.empty((nr, L), dtype=np.uint8)
     for i in range(nr):
         fam = rng.integers(0, 2) * 4
