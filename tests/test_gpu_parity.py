@@ -327,6 +327,13 @@ def test_chimeric_reads_of_two_genomes(k, L):
         assert fk.tolist() == ofk.tolist(), (m, p, mrq, mkq, mg)
 
 
+@pytest.mark.parametrize("k,L", [(31, 150), (75, 150), (31, 250)])
+def test_chimeric_reads_without_neighbour_bits(k, L, monkeypatch):
+    """The same without the neighbour bits (every mismatching window probed)."""
+    monkeypatch.setenv("PA_NO_NB", "1")
+    test_chimeric_reads_of_two_genomes(k, L)
+
+
 @pytest.mark.parametrize("k", [63, 64, 75, 100, 127])
 def test_non_acgt_anywhere_in_long_windows(k):
     """A non-ACGT base at any position of a window of k > 63 rules the window
