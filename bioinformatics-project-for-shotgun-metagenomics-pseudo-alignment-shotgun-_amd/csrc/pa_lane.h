@@ -1433,7 +1433,14 @@ void k_align_lane(AlignArgs a) {
         LaneRead<NM> S;
         S.kind = LANE_UNMAPPED + 100;  // (past the end: counted nowhere)
         wave_sync();  // the previous read's rows (and the taken list entries) are done with
-        if (r != ~0u) lane_prep<NM, NEED_Q, WIN_Q, true, NW>(a, r, cd, LW.R[lane], S);
+        // (the lane's row address made again at each use, through an opaque
+        // copy of the lane id: kept live across the phases it was spilled)
+        auto my_row = [&]() -> uint64_t * {
+            uint32_t l = (uint32_t)lane;
+            asm volatile("" : "+v"(l));
+            return LW.R[l];
+        };
+        if (r != ~0u) lane_prep<NM, NEED_Q, WIN_Q, true, NW>(a, r, cd, my_row(), S);
 #if defined(PA_STATS) || defined(PA_DISSECT)
         if (a.dbg_mode == 10 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // timing dissection: stop after the seeds
 #endif
@@ -1441,12 +1448,12 @@ void k_align_lane(AlignArgs a) {
         for (int attempt = again_batch ? 1 : 0; attempt < 2; attempt++) {
             if (S.kind == LANE_WALK) {
                 if constexpr (NM == 2)
-                    lane_walk_150<WIN_Q, MG, NW>(a, LW.R[lane], S);
+                    lane_walk_150<WIN_Q, MG, NW>(a, my_row(), S);
                 else
                     if constexpr (NM == 4 && !WIN_Q && NW == 1 && PA_LANE_HALVES)
-                        lane_walk_halves<MG>(a, LW.R[lane], S);
+                        lane_walk_halves<MG>(a, my_row(), S);
                     else
-                        lane_walk_long<NM, WIN_Q, MG>(a, LW.R[lane], S);
+                        lane_walk_long<NM, WIN_Q, MG>(a, my_row(), S);
             }
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 11 && S.kind == LANE_WALK) S.kind = LANE_AMB;  // stop after the walk
