@@ -11,6 +11,7 @@ prints them to stderr); load it with PA_LIBRARY=<path>.
 
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -42,6 +43,45 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _digest(paths, extra=()) -> str:
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    for e in extra:
+        h.update(str(e).encode() + b"\0")
+    return h.hexdigest()
+
+
+def source_hash(stats: bool = False, defines=()) -> str:
+    """SHA-256 of every csrc source and header, include/pa.h, the target arch
+    and the compile flags: what pa_version() of a library built from this
+    checkout reports after "src=" (the library is rebuilt when it changes)."""
+    flags = FLAGS + (["-DPA_STATS"] if stats else []) + [f"-D{d}" for d in defines]
+    paths = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(INCLUDE, "pa.h")]
+    return _digest(paths, [ARCH] + flags)
+
+
+def library_hash(version: str) -> str:
+    """The source hash a loaded library reports (pa_version() text)."""
+    return version.split("src=", 1)[1].strip() if "src=" in version else ""
+
+
+def _stamp_ok(target: str, digest: str) -> bool:
+    try:
+        with open(target + ".sha") as f:
+            return os.path.exists(target) and f.read().strip() == digest
+    except OSError:
+        return False
+
+
+def _stamp(target: str, digest: str) -> None:
+    with open(target + ".sha", "w") as f:
+        f.write(digest + "\n")
+
+
 def build(force: bool = False, verbose: bool = False, stats: bool = False, variant: str = "",
           defines=()) -> str:
     """Build libpa.so; `stats` or a named `variant` (with extra -D defines) go to
@@ -50,6 +90,7 @@ def build(force: bool = False, verbose: bool = False, stats: bool = False, varia
     build_dir = BUILD + (f"_{name}" if name else "")
     lib = os.path.join(HERE, f"libpa_{name}.so") if name else LIB
     flags = FLAGS + (["-DPA_STATS"] if stats else []) + [f"-D{d}" for d in defines]
+    full = source_hash(stats, defines)
     os.makedirs(build_dir, exist_ok=True)
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "pa.h")]
@@ -59,12 +100,16 @@ def build(force: bool = False, verbose: bool = False, stats: bool = False, varia
         path = os.path.join(CSRC, src)
         obj = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
-        if force or _stale(obj, [path, __file__] + headers):
-            if src.endswith(".hip"):
-                cmd = [hipcc, f"--offload-arch={ARCH}", *flags, "-x", "hip", "-c", path, "-o", obj]
-            else:
-                cmd = [hipcc, *flags, "-c", path, "-o", obj]
-            jobs.append(cmd)
+        # staleness by content: the source, every header and the flags (pa_api
+        # embeds the whole checkout's hash, so it follows every file)
+        extra = [f"-DPA_SOURCE_HASH=\"{full}\""] if src == "pa_api.cpp" else []
+        if src.endswith(".hip"):
+            cmd = [hipcc, f"--offload-arch={ARCH}", *flags, *extra, "-x", "hip", "-c", path, "-o", obj]
+        else:
+            cmd = [hipcc, *flags, *extra, "-c", path, "-o", obj]
+        digest = _digest([path] + headers, cmd[1:])
+        if force or not _stamp_ok(obj, digest):
+            jobs.append((cmd, obj, digest))
 
     def run(cmd):
         if verbose:
@@ -74,10 +119,20 @@ def build(force: bool = False, verbose: bool = False, stats: bool = False, varia
             raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}")
         return r.stdout
 
+    def job(j):
+        cmd, obj, digest = j
+        if os.path.exists(obj + ".sha"):
+            os.remove(obj + ".sha")
+        run(cmd)
+        _stamp(obj, digest)
+
     with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), 4))) as ex:
-        list(ex.map(run, jobs))
-    if force or jobs or _stale(lib, objs):
+        list(ex.map(job, jobs))
+    if force or jobs or not _stamp_ok(lib, full):
+        if os.path.exists(lib + ".sha"):
+            os.remove(lib + ".sha")
         run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-lz", "-lpthread", "-ldl"])
+        _stamp(lib, full)
     return lib
 
 

@@ -165,12 +165,15 @@ __device__ __forceinline__ void quality_read(const uint8_t *__restrict__ qual, u
                                              uint32_t T, int64_t mrq, uint32_t flags, uint4 &mask, uint8_t &drop) {
     // 16-B loads from the read's first dword (global loads need 4-B alignment
     // only), all twelve: the read buffers carry kReadPad bytes past the last read
-    const uint4 *sp = (const uint4 *)(qual + (o & ~3ull));
+    // (a vector type that states its 4-B alignment: the address is a dword's,
+    // not a 16-B one, and the compiler may not assume more)
+    typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4_a4 *sp = (const u32x4_a4 *)(qual + (o & ~3ull));
     const uint32_t sb = 8 * (uint32_t)(o & 3);
     uint32_t dw[kQmDwords + 4];
 #pragma unroll
     for (int c = 0; c < (kQmDwords + 4) / 4; c++) {
-        const uint4 v = sp[c];
+        const u32x4_a4 v = sp[c];
         dw[4 * c] = v.x, dw[4 * c + 1] = v.y, dw[4 * c + 2] = v.z, dw[4 * c + 3] = v.w;
     }
     // rd[j] = bytes 4j .. 4j + 3 of the read
@@ -1156,9 +1159,10 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
                     if (!idx->tile_nbbig) {
                         size_t free_b = 0, total_b = 0;
                         if (pa::dev_mem_info(&free_b, &total_b) == hipSuccess && nw * 4 + (8ull << 30) < free_b &&
-                            pa::dev_malloc(&idx->tile_nbbig, nw * 4 + 64) == hipSuccess)
+                            pa::dev_malloc(&idx->tile_nbbig, nw * 4 + 64) == hipSuccess) {
                             idx->tile_nbbig_mg = -1;
-                        else
+                            idx->device_bytes += nw * 4 + 64;  // (pa_index_get_info reports the real footprint)
+                        } else
                             idx->tile_nbbig = nullptr;
                         (void)hipGetLastError();
                     }
@@ -1176,9 +1180,10 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
                         if (!idx->tile_nbm) {
                             size_t free_b = 0, total_b = 0;
                             if (pa::dev_mem_info(&free_b, &total_b) == hipSuccess && nw * 16 + (8ull << 30) < free_b &&
-                                pa::dev_malloc(&idx->tile_nbm, nw * 16 + 64) == hipSuccess)
+                                pa::dev_malloc(&idx->tile_nbm, nw * 16 + 64) == hipSuccess) {
                                 idx->tile_nbm_mg = -1;
-                            else
+                                idx->device_bytes += nw * 16 + 64;
+                            } else
                                 idx->tile_nbm = nullptr;
                             (void)hipGetLastError();
                         }

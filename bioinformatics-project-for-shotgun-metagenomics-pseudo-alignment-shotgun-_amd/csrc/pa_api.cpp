@@ -62,7 +62,13 @@ extern "C" {
 
 const char *pa_last_error(void) { return pa::g_err.c_str(); }
 
-const char *pa_version(void) { return "libpa 0.1 (gfx950)"; }
+// PA_SOURCE_HASH: SHA-256 of csrc/*, include/pa.h and the compile flags, put on
+// this file's command line by build_native.py, so a test or a bench line can
+// tie the loaded binary to the checkout it came from.
+#ifndef PA_SOURCE_HASH
+#define PA_SOURCE_HASH "unknown"
+#endif
+const char *pa_version(void) { return "libpa 0.2 (gfx950) src=" PA_SOURCE_HASH; }
 
 namespace {
 struct RuntimeStarter {  // joined at exit, before the HIP runtime's own teardown (it was loaded first)
@@ -148,6 +154,7 @@ pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t 
 
 pa_status pa_index_reduce(pa_index *idx, const uint32_t *keep, uint32_t n_keep, uint32_t flags, void *stream) {
     PA_CHECK(idx != nullptr && (n_keep == 0 || keep != nullptr), PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     for (uint32_t i = 0; i < n_keep; i++) {
         PA_CHECK(keep[i] < idx->n_genomes, PA_EINVAL, "genome number out of range");
         PA_CHECK(i == 0 || keep[i] > keep[i - 1], PA_EINVAL, "genome numbers must be ascending");
@@ -159,6 +166,7 @@ pa_status pa_index_reduce(pa_index *idx, const uint32_t *keep, uint32_t n_keep, 
 
 pa_status pa_index_prepare(pa_index *idx, void *stream) {
     PA_CHECK(idx != nullptr, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_HIP(hipSetDevice(idx->device));
     PA_TRY(pa::index_prepare(idx, as_stream(stream)));
     PA_HIP(hipStreamSynchronize(as_stream(stream)));
@@ -192,6 +200,7 @@ pa_status pa_index_get_info(const pa_index *idx, pa_index_info *out) {
 pa_status pa_index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
                           uint32_t *size_out, void *stream) {
     PA_CHECK(idx && cls_out && (n == 0 || kmers), PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_HIP(hipSetDevice(idx->device));
     return pa::index_lookup(idx, kmers, n, kmer_len, cls_out, size_out, as_stream(stream));
 }
@@ -199,6 +208,7 @@ pa_status pa_index_lookup(const pa_index *idx, const char *kmers, uint64_t n, ui
 pa_status pa_index_positions(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, uint32_t flags,
                              pa_kmer_hit *hits, uint64_t cap, uint64_t *n_hits, void *stream) {
     PA_CHECK(idx && n_hits && (n == 0 || kmers), PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_CHECK((flags & ~PA_POS_REVERSE) == 0, PA_EINVAL, "unknown flag bits");
     PA_CHECK(n < PA_POS_RC_BIT, PA_EINVAL, "too many queries");
     PA_HIP(hipSetDevice(idx->device));
@@ -208,6 +218,7 @@ pa_status pa_index_positions(const pa_index *idx, const char *kmers, uint64_t n,
 pa_status pa_index_class_genomes(const pa_index *idx, int64_t cls, uint32_t *genomes, uint32_t cap, uint32_t *n,
                                  void *stream) {
     PA_CHECK(idx && n, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_CHECK(cls >= 0 && (uint64_t)cls < (uint64_t)idx->n_genomes + idx->class_entries, PA_EINVAL,
              "class id out of range");
     if ((uint64_t)cls < idx->n_genomes) {
@@ -235,6 +246,7 @@ pa_status pa_index_class_genomes(const pa_index *idx, int64_t cls, uint32_t *gen
 pa_status pa_index_extsim_stats(const pa_index *idx, const uint32_t *group_of, uint32_t n_groups, uint64_t *total,
                                 uint64_t *uniq, uint64_t *inter, void *stream) {
     PA_CHECK(idx && total && uniq && inter && (idx->n_genomes == 0 || group_of), PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     for (uint32_t g = 0; g < idx->n_genomes; g++)
         PA_CHECK(group_of[g] < n_groups, PA_EINVAL, "group_of entry out of range");
     PA_HIP(hipSetDevice(idx->device));
@@ -298,6 +310,7 @@ pa_status pa_reads_synthesize_mix(const pa_index *idx, uint64_t n_reads, uint32_
                                   uint64_t seed, double sub_rate, double rc_rate, double foreign_rate, void *stream,
                                   pa_reads **out) {
     PA_CHECK(idx && out, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     *out = nullptr;
     PA_CHECK(read_len > 0, PA_EINVAL, "read_len must be positive");
     PA_CHECK(rc_rate >= 0 && foreign_rate >= 0 && rc_rate + foreign_rate <= 1, PA_EINVAL,
@@ -359,6 +372,7 @@ void pa_reads_free(pa_reads *reads) {
 
 pa_status pa_result_create(const pa_index *idx, pa_result **out) {
     PA_CHECK(idx && out, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     *out = nullptr;
     PA_HIP(hipSetDevice(idx->device));
     pa_result *r = new (std::nothrow) pa_result();
@@ -445,6 +459,7 @@ void pa_result_free(pa_result *res) {
 pa_status pa_align(const pa_index *idx, const pa_reads *reads, const pa_params *params, uint64_t read_index_base,
                    pa_result *acc, void *stream) {
     PA_CHECK(idx && reads && acc, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_CHECK(acc->n_genomes == idx->n_genomes, PA_EINVAL, "result was created for a different index");
     PA_CHECK(reads->device == idx->device && acc->device == idx->device, PA_EINVAL,
              "index, reads and result must live on the same device");
@@ -460,6 +475,7 @@ pa_status pa_align_fastq_file(const pa_index *idx, const char *path, const pa_pa
                               uint64_t read_index_base, pa_result *acc, int32_t threads, uint64_t window_bytes,
                               void *stream, uint64_t *n_reads) {
     PA_CHECK(idx && path && acc, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_CHECK(acc->n_genomes == idx->n_genomes, PA_EINVAL, "result was created for a different index");
     PA_CHECK(acc->device == idx->device, PA_EINVAL, "index and result must live on the same device");
     pa::DevParams dp;
@@ -475,6 +491,7 @@ pa_status pa_index_dumpref(const pa_index *idx, const uint8_t *keep, const uint3
                            uint64_t *desc_multi, uint64_t *desc_order, uint32_t *desc_last_genome, uint64_t *n_kmers) {
     PA_CHECK(idx && desc_of && desc_json && desc_unique && desc_multi && desc_order && desc_last_genome, PA_EINVAL,
              "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_CHECK(fd >= 0, PA_EINVAL, "bad file descriptor");
     for (uint32_t d = 0; d < n_desc; d++) PA_CHECK(desc_json[d], PA_EINVAL, "NULL description");
     PA_HIP(hipSetDevice(idx->device));
@@ -498,6 +515,7 @@ void pa_fastq_prefetch_free(pa_fastq_prefetch *pf) { pa::fastq_prefetch_free(pf)
 pa_status pa_align_fastq_prefetched(const pa_index *idx, pa_fastq_prefetch *pf, const pa_params *params,
                                     uint64_t read_index_base, pa_result *acc, void *stream, uint64_t *n_reads) {
     PA_CHECK(idx && pf && acc, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_CHECK(acc->n_genomes == idx->n_genomes, PA_EINVAL, "result was created for a different index");
     PA_CHECK(acc->device == idx->device, PA_EINVAL, "index and result must live on the same device");
     pa::DevParams dp;
@@ -512,6 +530,7 @@ pa_status pa_align_detail(const pa_index *idx, const pa_reads *reads, const pa_p
                           uint32_t *filtered_kmers, uint32_t *redundant_kmers, uint64_t *list_off, uint32_t *lists,
                           uint64_t list_cap, uint64_t *list_total, void *stream) {
     PA_CHECK(idx && reads && read_type && filtered_kmers && redundant_kmers && list_off, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_CHECK(reads->device == idx->device, PA_EINVAL, "index and reads must live on the same device");
     pa::DevParams dp;
     PA_TRY(to_dev_params(params, idx->n_genomes, &dp));
@@ -525,6 +544,7 @@ pa_status pa_align_batch(const pa_index *idx, const uint8_t *seq, const uint8_t 
                          uint64_t n_reads, uint64_t read_index_base, const pa_params *params, pa_stats *stats,
                          uint64_t *unique_reads, uint64_t *ambiguous_reads, uint64_t *first_key, void *stream) {
     PA_CHECK(idx != nullptr, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     pa_reads *r = nullptr;
     pa_result *res = nullptr;
     PA_TRY(pa_reads_upload(idx->device, seq, qual, read_off, n_reads, stream, &r));

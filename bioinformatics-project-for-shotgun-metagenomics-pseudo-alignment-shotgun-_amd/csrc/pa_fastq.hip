@@ -599,16 +599,45 @@ void prefetch_run(pa_fastq_prefetch *pf) {
         rc = PA_EDEVICE;
         msg = std::string("HIP error in the FASTQ prefetch: ") + hipGetErrorString(e);
     }
+    // copies already finished are announced without blocking (hipEventQuery),
+    // also while this loop waits for the readers: a consumer must not stall on
+    // bytes that are in HBM because the next chunk is still being read
+    auto retire_done = [&]() -> hipError_t {
+        while (!q.empty()) {
+            const hipError_t r = hipEventQuery(ev[(int)(q.front() % nslot)]);
+            if (r == hipErrorNotReady) return hipSuccess;
+            if (r != hipSuccess) return r;
+            const hipError_t x = retire();
+            if (x != hipSuccess) return x;
+        }
+        return hipSuccess;
+    };
     for (uint64_t c = 0; c < nchunk && rc == PA_OK; c++) {
         const int s = (int)(c % nslot);
-        {
+        bool failed_read = false;
+        for (;;) {
+            e = retire_done();
+            if (e != hipSuccess) break;
             std::unique_lock<std::mutex> g(rm);
-            rcv.wait(g, [&] { return read_error || slot_chunk[s] == (int64_t)c; });
-            if (read_error) {
-                rc = PA_EIO;
-                msg = "read error in " + pf->path;
+            auto ready = [&] { return read_error || slot_chunk[s] == (int64_t)c; };
+            if (q.empty())
+                rcv.wait(g, ready);
+            else
+                rcv.wait_for(g, std::chrono::microseconds(200), ready);
+            if (ready()) {
+                failed_read = read_error;
                 break;
             }
+        }
+        if (e != hipSuccess) {
+            rc = PA_EDEVICE;
+            msg = std::string("HIP error in the FASTQ prefetch copy: ") + hipGetErrorString(e);
+            break;
+        }
+        if (failed_read) {
+            rc = PA_EIO;
+            msg = "read error in " + pf->path;
+            break;
         }
         const uint64_t a = c * kChunk, n = std::min(kChunk, pf->size - a);
         if (c == 0) {  // records ~ line feeds / 4 of the first chunk, scaled to the file

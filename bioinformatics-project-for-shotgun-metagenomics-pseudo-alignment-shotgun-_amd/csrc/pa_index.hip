@@ -606,6 +606,11 @@ __global__ void k_tile_cls_all(const uint8_t *__restrict__ codes, const uint64_t
 // bits, bit 31 of cls = bit 32 (pad::first_pos).  The lane kernels' anchors
 // then need no class-record and goff loads (C4 laid out genome-locally ran
 // 5 % slower: profiles/r05/ab_tpos_local.txt).  One pass over the slots.
+// The one first occurrence whose low 32 bits are all ones (position 2^32 - 1
+// or 2^33 - 1) reads as NONE afterwards: that k-mer then gives no anchor, so a
+// read seeded only by it takes the seedless path (k_align_lane_na tests every
+// window, a specific k-mer sends the read to the wave kernel) -- slower for
+// that read, never a different result.
 template <int NW>
 __global__ void k_tpos_concat(Slot<NW> *table, uint64_t cap, uint32_t G, const uint32_t *__restrict__ class_genomes,
                               const uint64_t *__restrict__ goff) {
@@ -2109,6 +2114,25 @@ pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream
         if (len) runs.push_back({goff[i], from, len});
         i = j + 1;
     }
+    const int64_t k = idx->k;
+    const int device = idx->device;
+    const bool profile = idx->profile;  // (set through the C ABI: kept across the rebuild)
+    // pa.h: on failure the index holds nothing and may only be freed -- so a
+    // failed copy never leaves half-compacted codes behind a valid-looking index
+    auto empty_index = [&]() {
+        index_release(idx);
+        *idx = pa_index();
+        idx->device = device;
+        idx->profile = profile;
+    };
+    auto fail = [&](hipError_t err, uint8_t *scratch) -> pa_status {
+        (void)hipStreamSynchronize(st);  // (the queued copies may still read or write scratch)
+        pa::dev_free(scratch);
+        empty_index();
+        idx->released = 1;
+        set_error(std::string("index reduce: ") + hipGetErrorString(err) + " (the index was released)");
+        return err == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;
+    };
     uint8_t *codes = nullptr;
     hipError_t e = pa::dev_malloc(&codes, std::max<uint64_t>(goff[n], 1));
     const char *inplace = std::getenv("PA_REDUCE_INPLACE");  // tests: force the in-place path
@@ -2121,43 +2145,54 @@ pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream
         for (size_t r = 0; r < runs.size() && e == hipSuccess; r++)
             e = hipMemcpyAsync(codes + runs[r].to, idx->codes + runs[r].from, runs[r].len, hipMemcpyDeviceToDevice, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) {
-            pa::dev_free(codes);
-            PA_HIP(e);
-        }
+        if (e != hipSuccess) return fail(e, codes);
     } else if (e == hipErrorOutOfMemory) {
         (void)hipGetLastError();
         codes = idx->codes;
         constexpr uint64_t kBounce = 64ull << 20;
+        // the bounce buffer, if any run overlaps its destination, is taken
+        // before the first copy: a failure here changes nothing yet
         uint8_t *bounce = nullptr;
-        for (size_t r = 0; r < runs.size(); r++) {
+        bool overlap = false;
+        for (const Run &u : runs) overlap |= u.to != u.from && u.to + u.len > u.from;
+        // PA_REDUCE_INJECT=bounce|copy (tests): the bounce allocation, or the
+        // copy after the first run, fails
+        const char *inj = std::getenv("PA_REDUCE_INJECT");
+        const bool inj_bounce = inj && std::strcmp(inj, "bounce") == 0, inj_copy = inj && std::strcmp(inj, "copy") == 0;
+        if (overlap && (e = inj_bounce ? hipErrorOutOfMemory : pa::dev_malloc(&bounce, kBounce)) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error(std::string("index reduce: ") + hipGetErrorString(e) + " (the index is unchanged)");
+            return e == hipErrorOutOfMemory ? PA_ENOMEM : PA_EDEVICE;
+        }
+        e = hipSuccess;
+        for (size_t r = 0; r < runs.size() && e == hipSuccess; r++) {
             const Run &u = runs[r];
             if (u.to == u.from) continue;
             if (u.to + u.len <= u.from) {  // no overlap: one copy
-                PA_HIP(hipMemcpyAsync(codes + u.to, codes + u.from, u.len, hipMemcpyDeviceToDevice, st));
+                e = hipMemcpyAsync(codes + u.to, codes + u.from, u.len, hipMemcpyDeviceToDevice, st);
                 continue;
             }
-            if (!bounce) PA_HIP(pa::dev_malloc(&bounce, kBounce));
-            for (uint64_t o = 0; o < u.len; o += kBounce) {  // front to back: a chunk's source is read before it is overwritten
+            for (uint64_t o = 0; o < u.len && e == hipSuccess; o += kBounce) {  // front to back: a chunk's source is read before it is overwritten
                 const uint64_t c = std::min(kBounce, u.len - o);
-                PA_HIP(hipMemcpyAsync(bounce, codes + u.from + o, c, hipMemcpyDeviceToDevice, st));
-                PA_HIP(hipMemcpyAsync(codes + u.to + o, bounce, c, hipMemcpyDeviceToDevice, st));
+                e = hipMemcpyAsync(bounce, codes + u.from + o, c, hipMemcpyDeviceToDevice, st);
+                if (e == hipSuccess) e = hipMemcpyAsync(codes + u.to + o, bounce, c, hipMemcpyDeviceToDevice, st);
             }
+            if (inj_copy && e == hipSuccess) e = hipErrorOutOfMemory;
         }
-        PA_HIP(hipStreamSynchronize(st));
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return fail(e, bounce);  // (codes are the index's own: released with it)
         pa::dev_free(bounce);
         idx->codes = nullptr;  // (kept: the rebuild's codes)
     } else {
         PA_HIP(e);
     }
-    const int64_t k = idx->k;
-    const int device = idx->device;
-    const bool profile = idx->profile;  // (set through the C ABI: kept across the rebuild)
-    index_release(idx);
-    *idx = pa_index();
-    idx->device = device;
-    idx->profile = profile;
-    return index_build(idx, nullptr, goff.data(), n, k, st, defer_tiles, codes);
+    empty_index();
+    const pa_status rc = index_build(idx, nullptr, goff.data(), n, k, st, defer_tiles, codes);
+    if (rc != PA_OK) {  // (the error text stays: releasing sets none)
+        empty_index();
+        idx->released = 1;
+    }
+    return rc;
 }
 
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,

@@ -92,6 +92,7 @@ struct pa_index {
     uint64_t total_windows = 0;
     int tpos_local = 0;                // slot.tpos genome-local (references of >= 2^32 bases), else concatenated
     uint64_t distinct_estimate = 0;    // HyperLogLog estimate (+3 %) when the table was sized on it, else 0
+    int released = 0;                  // a failed pa_index_reduce emptied it: it may only be freed
     int force_large = 0;               // PA_LAYOUT=large: the layout of a reference too large for the default one
     // genome tiling (single-word keys, < 2^32 genome bases): the genomes as one
     // concatenated 2-bit string plus the class of the k-mer starting at every

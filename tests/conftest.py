@@ -22,3 +22,23 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+def _library_line() -> str:
+    """The loaded libpa.so's source hash against this checkout's (build_native.source_hash)."""
+    try:
+        import build_native
+        import pa_native
+        have = build_native.library_hash(pa_native.lib().pa_version().decode())
+        want = build_native.source_hash()
+        return f"libpa.so src={have[:16]} checkout={want[:16]} " + ("(match)" if have == want else "(MISMATCH)")
+    except Exception as e:  # the summary line must not fail the run
+        return f"libpa.so not loaded: {e}"
+
+
+def pytest_report_header(config):
+    return _library_line()
+
+
+def pytest_terminal_summary(terminalreporter):
+    terminalreporter.write_line(_library_line())

@@ -65,3 +65,36 @@ def test_reduce_refuses_bad_lists():
     idx.reduce([1, 2, 3])
     assert idx.n_genomes == 3
     idx.close()
+
+
+@pytest.mark.parametrize("inject", ["bounce", "copy"])
+def test_reduce_in_place_failure_leaves_no_stale_index(inject, monkeypatch):
+    """the in-place path must fail before it changes anything (the
+    bounce buffer is taken first) or release the index (a copy failed
+    mid-compaction) -- never return half-compacted codes behind the old genome
+    offsets.  PA_REDUCE_INJECT makes the bounce allocation / a copy fail."""
+    monkeypatch.setenv("PA_REDUCE_INPLACE", "1")
+    monkeypatch.setenv("PA_REDUCE_INJECT", inject)
+    gens = synth.family_genomes(6, 40_000, seed=4, family_size=3, sub_rate=0.01, conserved_len=500)
+    idx = N.Index(gens, 31)
+    before = idx.info()
+    sel = np.asarray([0, 2, 3, 5], dtype=np.uint32)
+    st = N.lib().pa_index_reduce(idx.handle, sel.ctypes.data_as(N.P), len(sel), 0, None)
+    assert st == N.PA_ENOMEM
+    after = idx.info()
+    if inject == "bounce":  # nothing changed: the old index is whole and still aligns
+        assert (after.n_genomes, after.n_kmers, after.total_windows) == \
+               (before.n_genomes, before.n_kmers, before.total_windows)
+        reads = N.Reads.synthesize(idx, 2000, 150, seed=3)
+        assert _fetch(idx, reads, N.Params.make())[0][2] < 2000  # (most reads map)
+        reads.close()
+    else:  # released: an empty index, nothing left that describes the old genomes
+        assert after.n_genomes == 0 and after.n_kmers == 0 and after.table_slots == 0
+        with pytest.raises(ValueError, match="released"):
+            N.Result(idx)
+    idx.close()
+    monkeypatch.delenv("PA_REDUCE_INJECT")
+    ok = N.Index(gens, 31, defer_tiles=True)
+    ok.reduce(sel)
+    assert ok.n_genomes == 4
+    ok.close()

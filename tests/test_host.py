@@ -56,6 +56,16 @@ def test_version_and_error_string():
     assert isinstance(N.lib().pa_last_error(), bytes)
 
 
+def test_library_built_from_this_checkout():
+    """pa_version() carries the SHA-256 of the sources, header and flags it was
+    built from (build_native.source_hash); it must be this checkout's, so the
+    GPU evidence is tied to HEAD's sources."""
+    import build_native
+    have = build_native.library_hash(N.lib().pa_version().decode())
+    assert len(have) == 64
+    assert have == build_native.source_hash()
+
+
 PARSER = json.load(open(os.path.join(GOLD, "parser_cases.json")))
 
 
