@@ -16,6 +16,10 @@ Files written:
   random quirk-covering scenarios: per-read (type, genomes_mapped_to, windows
   filtered by quality, windows filtered as highly-redundant) and full
   ``PseudoAlignment.get_summary()`` for each parameter set;
+* ``demo_cases.json`` - the reference's demo configurations (src/RUN_LOG:28-84:
+  k = 75 with -m 1 -p 1, k = 150 with --min-read-quality 59 --min-kmer-quality
+  60 --max-genomes 2 / 0; reads of 150 and 151-200 bases) and k = 96 ... 159,
+  in the unit-case format, plus the reference CLI's ``dumpalign -k 150`` stdout;
 * ``config1.fa`` / ``config1.fq`` / ``config1_cli.json`` - BASELINE config 1
   (3 x 5 kb genomes, 1k x 100 bp reads, k=21) with the exact stdout of the
   reference ``dumpalign`` CLI for several flag sets;
@@ -36,7 +40,7 @@ Files written:
   reference's stdout of ``dumpref -r`` / ``dumpalign -r`` / ``dumpalign -a``
   on them.
 
-    python tests/golden/make_golden.py [part ...]   (parts: unit config1 extsim parser dumpref lookup)
+    python tests/golden/make_golden.py [part ...]   (parts: unit demo config1 extsim parser dumpref lookup)
 """
 
 from __future__ import annotations
@@ -220,6 +224,99 @@ def make_unit_cases():
     with open(os.path.join(HERE, "unit_cases.json"), "w") as f:
         json.dump(out, f, separators=(",", ":"))
     print("unit cases:", len(out), "reads x psets:", sum(len(c["reads"]) * len(c["results"]) for c in out))
+
+
+# ----------------------------------------------------------------------------
+# the reference's own demo configurations (src/RUN_LOG:28-84): k = 75 with
+# -m 1 -p 1, and k = 150 with --min-read-quality 59 --min-kmer-quality 60
+# --max-genomes 2 / 0, on reads of 150 and 151-200 bases; plus k = 96 ... 159
+# (keys of four and five 64-bit words) -- the lane kernels stop at k = 95
+# ----------------------------------------------------------------------------
+
+def _demo_reads(gens, n, rng, prefix, lens=(150, 200), err=0.003):
+    """Reads of lens[0]..lens[1] bases from the genomes (N bases replaced by a
+    random base: the FASTQ grammar has no N), with per-read quality levels
+    spread around the RUN_LOG thresholds (59 / 60, raw ASCII: quirk 5)."""
+    out = []
+    for i in range(n):
+        L = int(rng.integers(lens[0], lens[1] + 1))
+        g = gens[int(rng.integers(len(gens)))]
+        if rng.random() < 0.9 and L <= len(g):
+            st = int(rng.integers(0, len(g) - L + 1))
+            s = bytearray(g[st:st + L])
+        else:  # an unindexed stretch
+            s = bytearray(synth.ACGT[rng.integers(0, 4, size=L)])
+        for j in range(L):
+            if s[j] == ord("N") or rng.random() < err:
+                s[j] = int(synth.ACGT[rng.integers(0, 4)])
+        lvl = float(rng.uniform(54, 66))
+        q = np.clip(np.rint(rng.normal(lvl, 6, size=L)), 33, 74).astype(np.uint8).tobytes().decode()
+        out.append((f"{prefix}{i}", s.decode(), q))
+    return out
+
+
+def demo_cases():
+    cases = []
+    rng = np.random.Generator(np.random.PCG64(7150))
+    demo_flags = [P(mrq=59, mkq=60, mg=2), P(mrq=59, mkq=60, mg=0)]  # src/RUN_LOG:64-84
+    more = [P(), P(m=0, p=0), P(m=2, p=2), P(mg=1), P(mg=2), P(mrq=59), P(mkq=60), P(m=1, p=-1)]
+    for name, k, n_gen, glen, fam, sub, cons, n_reads, lens, psets in (
+            # step 5 / 7: align -m 1 -p 1 at k = 75 (small reference)
+            ("demo_k75_small", 75, 8, 4000, 4, 0.01, 300, 300, (150, 150), [P(m=1, p=1)] + demo_flags + more),
+            ("demo_k75_long", 75, 8, 4000, 4, 0.01, 300, 200, (151, 200), [P(m=1, p=1)] + demo_flags + more),
+            # steps 8 / 9: dumpalign -k 150 with the quality flags (mid reference)
+            ("demo_k150_150bp", 150, 10, 6000, 5, 0.002, 700, 400, (150, 150), demo_flags + more),
+            ("demo_k150_long", 150, 10, 6000, 5, 0.002, 700, 300, (151, 200), demo_flags + more)):
+        gens = synth.family_genomes(n_gen, glen, seed=int(rng.integers(1 << 30)), family_size=fam, sub_rate=sub,
+                                    conserved_len=cons, n_rate=2e-4, n_run=5)
+        genomes = [(f"{name}_g{i} mid demo", bytes(g).decode()) for i, g in enumerate(gens)]
+        reads = _demo_reads(gens, n_reads, rng, f"{name}_r", lens)
+        cases.append({"name": name, "genomes": genomes, "k": k, "reads": reads, "psets": psets})
+    # k between the three-word lane keys and the wave kernel's longest (96 ... 159)
+    for k in (96, 101, 113, 127, 128, 129, 140, 159):
+        gens = synth.family_genomes(6, 2500, seed=int(rng.integers(1 << 30)), family_size=3, sub_rate=0.003,
+                                    conserved_len=k + 40, n_rate=2e-4, n_run=4)
+        genomes = [(f"long_k{k}_g{i}", bytes(g).decode()) for i, g in enumerate(gens)]
+        reads = _demo_reads(gens, 120, rng, f"k{k}_r", (max(k - 10, 1), 200))
+        cases.append({"name": f"long_k{k}", "genomes": genomes, "k": k, "reads": reads,
+                      "psets": [P(), P(m=0, p=0), P(mg=1), P(mrq=59, mkq=60, mg=2), P(m=2, p=-1)]})
+    return cases
+
+
+def make_demo_cases():
+    out = []
+    for case in demo_cases():
+        entry = {"name": case["name"], "k": case["k"], "genomes": case["genomes"], "reads": case["reads"],
+                 "results": []}
+        for ps in case["psets"]:
+            res, ref = run_case(case["genomes"], case["k"], case["reads"], ps)
+            entry["results"].append(res)
+        entry["n_kmers"] = len(ref.kmers)
+        gidx = {id(g): i for i, g in enumerate(ref.genomes)}
+        # a sample of the k-mers' genome sets (every n-th in sorted order, about
+        # 400 per case: the long keys make the whole dict megabytes)
+        allk = sorted(ref.kmers)
+        step = max(1, len(allk) // 400)
+        entry["kmer_sets"] = [[km, sorted(gidx[id(g)] for g in ref.kmers[km])] for km in allk[::step]]
+        out.append(entry)
+    # the demo CLI itself: dumpalign -k 150 with RUN_LOG's flags on the mid reference
+    c = next(x for x in out if x["name"] == "demo_k150_150bp")
+    fa = os.path.join(SCRATCH, "demo_mid.fa")
+    fq = os.path.join(SCRATCH, "demo_mid.fq")
+    with open(fa, "w") as f:
+        f.write(fasta_of(c["genomes"]))
+    with open(fq, "w") as f:
+        f.write(fastq_of(c["reads"]))
+    cli = []
+    for fl in (["--min-read-quality", "59", "--min-kmer-quality", "60", "--max-genomes", "2"],
+               ["--min-read-quality", "59", "--min-kmer-quality", "60", "--max-genomes", "0"], []):
+        cmd = [sys.executable, "main.py", "-t", "dumpalign", "-g", fa, "-k", "150", "--reads", fq] + fl
+        r = subprocess.run(cmd, cwd=REFDIR, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        assert r.returncode == 0, r.stderr
+        cli.append({"flags": fl, "stdout": r.stdout})
+    with open(os.path.join(HERE, "demo_cases.json"), "w") as f:
+        json.dump({"cases": out, "cli": {"case": c["name"], "k": 150, "runs": cli}}, f, separators=(",", ":"))
+    print("demo cases:", len(out), "reads x psets:", sum(len(c["reads"]) * len(c["results"]) for c in out))
 
 
 # ----------------------------------------------------------------------------
@@ -457,9 +554,9 @@ def make_lookup_cases():
 
 
 if __name__ == "__main__":
-    parts = sys.argv[1:] or ["unit", "config1", "extsim", "parser", "dumpref", "lookup"]
+    parts = sys.argv[1:] or ["unit", "demo", "config1", "extsim", "parser", "dumpref", "lookup"]
     try:
-        for part, fn in (("unit", make_unit_cases), ("config1", make_config1), ("extsim", make_extsim),
+        for part, fn in (("unit", make_unit_cases), ("demo", make_demo_cases), ("config1", make_config1), ("extsim", make_extsim),
                          ("parser", make_parser_cases), ("dumpref", make_dumpref), ("lookup", make_lookup_cases)):
             if part in parts:
                 fn()

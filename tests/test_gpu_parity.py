@@ -30,6 +30,9 @@ def load(name):
 
 
 UNIT = load("unit_cases.json")
+# the reference's demo configurations (src/RUN_LOG:28-84) and k = 96-159
+DEMO = load("demo_cases.json")
+CASES = UNIT + DEMO["cases"]
 TYPE = {0: "DROPPED", 1: "UNMAPPED", 2: "UNIQUELY_MAPPED", 3: "AMBIGUOUSLY_MAPPED"}
 
 
@@ -66,7 +69,7 @@ def summary_from_counters(idents, stats, uq, am, fk, ps):
                                           for n in sorted(first, key=first.get)}}
 
 
-@pytest.mark.parametrize("case", UNIT, ids=[c["name"] for c in UNIT])
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_golden_unit_cases(case):
     """Per-read results (exact kernel) and summaries (fast + exact kernels) vs the reference."""
     idents = [g[0] for g in case["genomes"]]
@@ -157,6 +160,24 @@ def test_config1_cli_stdout():
         assert r.stdout == case["stdout"], case["flags"]
 
 
+def test_demo_k150_cli_stdout(tmp_path):
+    """The reference's demo runs `dumpalign -k 150 --min-read-quality 59
+    --min-kmer-quality 60 --max-genomes 2` (and `--max-genomes 0`,
+    src/RUN_LOG:64-84) through the drop-in CLI on a mid-sized reference:
+    stdout identical to the reference CLI's."""
+    cli = DEMO["cli"]
+    case = next(c for c in DEMO["cases"] if c["name"] == cli["case"])
+    fa, fq = tmp_path / "mid.fa", tmp_path / "mid.fq"
+    fa.write_text("".join(f">{h}\n{s}\n" for h, s in case["genomes"]))
+    fq.write_text("".join(f"@{i}\n{s}\n+\n{q}\n" for i, s, q in case["reads"]))
+    for run in cli["runs"]:
+        cmd = [sys.executable, os.path.join(PKG, "main.py"), "-t", "dumpalign", "-g", str(fa), "-k", str(cli["k"]),
+               "--reads", str(fq)] + run["flags"]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout == run["stdout"], run["flags"]
+
+
 def test_align_without_reference_file_fails_like_the_reference(tmp_path):
     """`-t align -g -k --reads -a` without -r: the reference saves its k-mer
     reference to None (src/main.py:366-372), gzip.open raises a TypeError the
@@ -217,6 +238,15 @@ SYNTH = [
     (25, 40000, 5, 0.01, 75, 8000, 150, 0.015, [dict(), dict(m=0, p=0), dict(mg=2), dict(m=2, p=0), dict(mg=1),
                                                  dict(mrq=58, mkq=59, mg=2), dict(mkq=60)]),
     (12, 20000, 4, 0.02, 95, 3000, 150, 0.01, [dict(), dict(m=0, p=-1), dict(mg=3), dict(mkq=59)]),
+    # k = 96 ... 159 (four- and five-word keys, the wave kernel): the reference's
+    # demo k = 150 with its flags (src/RUN_LOG:64-84) on 150- and 200-bp reads
+    (6, 8000, 3, 0.004, 101, 1500, 150, 0.003, [dict(), dict(m=0, p=0), dict(mrq=59, mkq=60, mg=2)]),
+    (6, 8000, 3, 0.004, 127, 1500, 180, 0.003, [dict(), dict(mg=1), dict(mrq=59, mkq=60, mg=0)]),
+    (6, 8000, 3, 0.004, 128, 1500, 200, 0.003, [dict(), dict(m=0, p=0), dict(mkq=60)]),
+    (10, 8000, 5, 0.002, 150, 2000, 150, 0.002, [dict(), dict(mrq=59, mkq=60, mg=2), dict(mrq=59, mkq=60, mg=0),
+                                                  dict(m=0, p=0)]),
+    (10, 8000, 5, 0.002, 150, 1500, 200, 0.002, [dict(), dict(mrq=59, mkq=60, mg=2), dict(mrq=59, mkq=60, mg=0)]),
+    (6, 8000, 3, 0.004, 159, 1500, 200, 0.003, [dict(), dict(m=2, p=-1), dict(mrq=59, mkq=60, mg=2)]),
     (3, 4000, 1, 0.0, 17, 1500, 40, 0.02, [dict(), dict(mkq=55)]),
     (70, 3000, 10, 0.01, 15, 3000, 80, 0.01, [dict(), dict(m=0, p=0)]),  # many genomes per class
     # families (1% apart) and 1.5% read errors: off-walk k-mers, sibling walks,
