@@ -148,9 +148,63 @@ def e2e_pass():
 
 
 def bytes_per_read(cfg) -> int:
+    """SURVEY.md 8(d)'s figure: L + q*L + 16 per window (one 8-B key + 8-B value
+    slot read per window).  The lane walk settles most windows without a slot
+    read, so this is not a floor of the design (it can pass the peak): kept as
+    `survey_8d` for reference only."""
     L, k = cfg["read_len"], cfg["k"]
     q = 1 if (cfg["params"].get("mrq") is not None or cfg["params"].get("mkq") is not None) else 0
     return L + q * L + (L - k + 1) * 16
+
+
+def design_bytes_per_read(cfg, quality_applied: bool) -> dict:
+    """The design's algorithmic bytes per read: what the
+    lane kernel must read for a read that is one stretch of one genome, each
+    item priced at its own size (no line granularity) --
+      read:   L ASCII bases (+ L quality bytes when a quality filter is applied
+              after the elision of thresholds no read can fail);
+      walk:   the walk blocks over the read's span, 32 B per 64 genome
+              positions (2-bit bases + flag planes), (L - 1) / 64 + 1 blocks on
+              average over the read's offset in its first block;
+      seeds:  the first and last seed windows' slots (16 B each);
+      mismatches: one 8-B neighbour word per mismatching base (substitution
+              rate x L).
+    A floor of the bytes moved, not a count of lines: the measured traffic (128-B
+    lines) is several times this, the ratio being the random-access overhead."""
+    L = int(cfg["read_len"])
+    parts = {"read": L + (L if quality_applied else 0),
+             "walk": 32.0 * ((L - 1) / 64.0 + 1.0),
+             "seeds": 2 * 16,
+             "mismatches": 8.0 * float(cfg["read_err"]) * L}
+    return {"bytes_per_read": sum(parts.values()), "parts": parts}
+
+
+def measured_bytes_per_read(config: str, kernel: str):
+    """(fabric bytes per read of `kernel` measured by an N = 1 counter pass of
+    `config`, source) from profiles/lines_per_read.json, or (None, reason)."""
+    path = os.path.join(REPO, "profiles", "lines_per_read.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)[config]
+        return float(d["kernels"][kernel]["bytes_per_read"]), f"N = 1 counter pass, {d['source']}"
+    except (OSError, KeyError, ValueError):
+        return None, f"no N = 1 measurement of {config}/{kernel} in profiles/lines_per_read.json"
+
+
+def multi_rank_roofline(config: str, kernel: str, npg: int, slowest_ms: float, design_bpr: float) -> dict:
+    """The roofline of an N > 1 line, where no counter pass runs: each rank's
+    launch of the dominant kernel priced with the fabric bytes per read an
+    N = 1 counter pass of the same config measured (profiles/lines_per_read.json),
+    else with the design's algorithmic bytes per read, over the slowest rank's
+    average launch."""
+    bpr, src = measured_bytes_per_read(config, kernel)
+    if bpr is None:
+        bpr, src = design_bpr, "the design's algorithmic bytes per read (DESIGN.md section 4)"
+    achieved = bpr * npg / (slowest_ms / 1e3) / 1e9
+    return {"traffic": bpr * npg, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
+            "achieved_basis": (f"N > 1 LINES MODEL: {bpr:.1f} fabric bytes per read ({src}) x {npg} reads per rank "
+                               f"and launch / the slowest rank's average {kernel} launch (HIP events on each rank's "
+                               "stream) / 8 TB/s; no counter pass runs at N > 1")}
 
 
 def random_line_roofline():
@@ -541,8 +595,12 @@ def main():
     # index, closed at once (its device memory stays in the library's pool)
     N.Index([np.frombuffer(b"ACGT" * 64, dtype=np.uint8)], cfg["k"], device=local, stream=stream).close()
     torch.cuda.synchronize(dev)
+    first_read, npg = rank_reads(cfg, rank, world)
     t_index0 = t0 = time.perf_counter()
-    index = N.Index(genomes, cfg["k"], device=local, stream=stream, defer_tiles=bool(filtering))
+    # the align-side view is made below by prepare(expected_reads=...), sized
+    # for this rank's job, as the product does (the CLI passes its FASTQ's
+    # record count, PseudoAlignment its batch's)
+    index = N.Index(genomes, cfg["k"], device=local, stream=stream, defer_tiles=True)
     torch.cuda.synchronize(dev)
     build_s = time.perf_counter() - t0
     build_bases = sum(len(g) for g in genomes)
@@ -581,20 +639,37 @@ def main():
                   "max_kept_pair_score_below": cfg["extsim"]}
         log(f"[rank {rank}] EXTSIM: kept {len(keep)} of {len(idents)} in {extsim['total_s']:.1f}s")
     t0 = time.perf_counter()
-    index.prepare(stream)  # the align-side view (a no-op unless deferred)
+    # the job's index: the align-side view this rank's npg reads repay (the
+    # neighbour bits only past PA_NB_READS_PER_BASE reads per genome base:
+    # pa_index_prepare_ex)
+    index.prepare(stream, expected_reads=npg)
     prepare_s = time.perf_counter() - t0
     index_total_s = time.perf_counter() - t_index0
-    info = index.info()
-    first_read, npg = rank_reads(cfg, rank, world)
+    job_index_bytes = int(index.info().device_bytes)
+    t0 = time.perf_counter()
     reads = N.Reads.synthesize(index, npg, cfg["read_len"], first_read=first_read, seed=2, sub_rate=cfg["read_err"],
                                stream=stream, rc_rate=cfg.get("rc_rate", 0.0),
                                foreign_rate=cfg.get("foreign_rate", 0.0))
+    torch.cuda.synchronize(dev)
+    reads_make_s = time.perf_counter() - t0
     result = N.Result(index)
     pk = cfg["params"]
     prm = N.Params.make(pk.get("m", 1), pk.get("p", 1), pk.get("mrq"), pk.get("mkq"), pk.get("mg"))
+    # the filters a pass really applies: thresholds at or below the batch's
+    # smallest quality byte filter nothing (quirk 5) and are dropped
+    eff, q_min = reads.effective(prm, stream)
+    applied = {}
+    if eff.flags & N.HAS_MRQ:
+        applied["mrq"] = pk.get("mrq")
+    if eff.flags & N.HAS_MKQ:
+        applied["mkq"] = pk.get("mkq")
+    if eff.flags & N.HAS_MG:
+        applied["mg"] = pk.get("mg")
+    elided = [n for n, f in (("mrq", N.HAS_MRQ), ("mkq", N.HAS_MKQ)) if (prm.flags & f) and not (eff.flags & f)]
+    quality_applied = bool(eff.flags & (N.HAS_MRQ | N.HAS_MKQ))
     log(f"[rank {rank}] genomes {gen_s:.1f}s, index {index_total_s:.2f}s (first build {build_s:.2f}s, "
-        f"align-side view {prepare_s:.2f}s): {info.n_kmers} k-mers, "
-        f"{info.n_multi_classes} multi-genome sets, table {info.table_bytes / 2**30:.2f} GiB; {npg} reads")
+        f"align-side view {prepare_s:.2f}s): {index.info().n_kmers} k-mers, "
+        f"{index.info().n_multi_classes} multi-genome sets, table {index.info().table_bytes / 2**30:.2f} GiB; {npg} reads")
 
     comm = pa_dist.make_comm(local) if (world > 1 and args.reduce == "capi") else None
     # the ranks an RCCL communicator of this job really spans (ncclCommCount);
@@ -617,6 +692,56 @@ def main():
                 pa_dist.reduce_result_capi(result, comm, stream)
             else:
                 pa_dist.reduce_result(result, dev, stream)
+
+    def timed_passes(n):
+        """n passes between barriers + device syncs; (max-over-ranks seconds,
+        {kernel: (ms, launches)} of HIP events around each launch)."""
+        index.profile_read()  # (drop earlier events)
+        index.profile_enable(True)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        kern = index.profile_read_kernels()
+        index.profile_enable(False)
+        return max_over_ranks(el), kern
+
+    def max_over_ranks(*vals):
+        t = torch.tensor(list(vals), dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        if world > 1:
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        out = [float(x) for x in t.tolist()]
+        return out[0] if len(out) == 1 else out
+
+    # 1) the job as the product runs it: the index built for npg reads, one pass
+    #    of them (timed over a few passes; fewer than would bring the reads
+    #    aligned past the neighbour bits' break-even)
+    product = None
+    if not args.traffic_child:
+        step()  # (warmup)
+        torch.cuda.synchronize(dev)
+        np_ = max(1, min(args.steps, 5))
+        p_el, p_kern = timed_passes(np_)
+        nb_during = int(index.info().device_bytes) != job_index_bytes
+        product = {"passes": np_, "pass_s": p_el / np_, "reads_per_s": world * npg * np_ / p_el,
+                   "kernels_ms": {k: v[0] / v[1] for k, v in p_kern.items() if v[1]},
+                   "valid": not nb_during}
+    # 2) the serving index: the neighbour bits made now (a no-op when the job
+    #    already repaid them) -- the index a long-lived aligner keeps
+    bytes0 = int(index.info().device_bytes)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    index.prepare(stream)
+    torch.cuda.synchronize(dev)
+    nb_s = time.perf_counter() - t0
+    nb_built = int(index.info().device_bytes) > bytes0
+    info = index.info()
 
     if args.traffic_child:  # under rocprofv3: warmup + the measured passes, nothing else
         for _ in range(args.warmup + args.steps):
@@ -642,10 +767,8 @@ def main():
     kern_ms, launches, deferred = index.profile_read()
     kern = index.profile_read_kernels()
     index.profile_enable(False)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed)
+    build_max, nb_max = max_over_ranks(index_total_s, nb_s)
     # every rank's align-kernel times (HIP events on its own stream), for the
     # rank-0 line: at N > 1 no counter pass runs, so the roofline of a scaling
     # run comes from these and the section 8(d) algorithmic bytes
@@ -661,10 +784,34 @@ def main():
     value = total_reads / elapsed
     pass_s = kern_ms / max(launches, 1) / 1e3
     b_read = bytes_per_read(cfg)
-    alg_achieved = b_read * npg / pass_s / 1e9 if pass_s > 0 else 0.0
+    design = design_bytes_per_read(cfg, quality_applied)
     # the dominant kernel: the largest share of the timed align passes
     dominant = max((k for k in kern if kern[k][1] > 0), key=lambda k: kern[k][0], default="k_align_lane")
     dom_s = kern[dominant][0] / max(kern[dominant][1], 1) / 1e3
+    alg_achieved = design["bytes_per_read"] * npg / dom_s / 1e9 if dom_s > 0 else 0.0
+    # the job as the product runs it (section 1 above): build + one pass, per GPU
+    job = None
+    if product is not None:
+        job_s = build_max + product["pass_s"]
+        job = {"reads_per_gpu": npg, "index_build_s": build_max, "align_pass_s": product["pass_s"],
+               "job_s": job_s, "job_reads_per_s_per_gpu": npg / job_s, "job_reads_per_s": world * npg / job_s,
+               "plan_8_gpus": {"reads": 8 * npg, "job_reads_per_s": 8 * npg / job_s,
+                               "basis": "8 ranks each building the same replica and aligning its npg reads in the "
+                                        "same time as this rank (weak scaling, one latency-bound all-reduce)"},
+               "basis": ("the index built for this rank's reads (pa_index_prepare_ex with expected_reads = npg: "
+                         "neighbour bits only past their break-even) from genomes in host memory, plus one align "
+                         "pass of the npg device-resident reads on it; max over ranks")}
+    serving_pass_s = elapsed / args.steps
+    breakeven = None
+    if product is not None and product["valid"] and nb_built:
+        saved = (product["pass_s"] - serving_pass_s) / npg
+        per_base = nb_max / max(int(info.total_windows), 1)
+        breakeven = {"neighbour_bits_s": nb_max, "saved_ns_per_read": saved * 1e9,
+                     "cost_ns_per_base": per_base * 1e9,
+                     "reads_per_base": per_base / saved if saved > 0 else None,
+                     "policy_reads_per_base": N.PA_NB_READS_PER_BASE,
+                     "basis": "neighbour bits' build time per genome window / align time they save per read "
+                              "(job-index pass - serving-index pass, per read)"}
     out = {
         "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -673,7 +820,14 @@ def main():
         "config": {"workload": cfg["name"], "genomes": cfg["n_genomes"], "genome_len": cfg["genome_len"],
                    "k": cfg["k"], "reads_per_gpu": npg, "job_reads_per_step": world * npg,
                    "read_len": cfg["read_len"],
-                   "filters": cfg["params"] or None, "parallelism": f"read-sharded x{world}, index replicated",
+                   "filters": cfg["params"] or None,
+                   "filters_applied": applied or None,
+                   "filters_note": (f"{'/'.join(elided)} elided (q_min = {q_min}: a threshold at or below the batch's "
+                                    "smallest quality byte filters nothing, strict <, quirk 5; measured when the reads "
+                                    "are made, outside the timed step)") if elided else None,
+                   "index": ("serving: neighbour bits built (pa_index_prepare after the job-index passes)"
+                             if nb_built or not product else "job index (neighbour bits already repaid)"),
+                   "parallelism": f"read-sharded x{world}, index replicated",
                    "reduce": args.reduce if world > 1 else None, "backend": backend, "rccl_ranks": rccl_ranks,
                    "read_mix": {"reverse_complement": cfg.get("rc_rate", 0.0), "foreign": cfg.get("foreign_rate", 0.0),
                                 "substitution_rate": cfg["read_err"]}},
@@ -682,20 +836,34 @@ def main():
                      "achieved_basis": ("MEASURED fabric read bytes of the dominant kernel per launch (traffic, "
                                         "counter pass) / its average duration (HIP events around each launch on "
                                         "its stream over the timed steps) / 8 TB/s"),
-                     "algorithmic": {"bytes_per_read": b_read, "bytes_per_pass": b_read * npg,
-                                     "pass_ms": pass_s * 1e3, "achieved": alg_achieved,
+                     "algorithmic": {"model": "design bytes per read (DESIGN.md section 4)",
+                                     "bytes_per_read": design["bytes_per_read"], "parts": design["parts"],
+                                     "bytes_per_launch": design["bytes_per_read"] * npg,
+                                     "kernel_ms": dom_s * 1e3, "achieved": alg_achieved,
                                      "frac": alg_achieved / HBM_PEAK_GBS,
-                                     "basis": ("SURVEY.md 8d: L + q*L + 16*(L-k+1) per read over the whole align "
-                                               "pass (all align kernels); it prices one 16-B slot read per window, "
-                                               "which the lane walk mostly skips, so it can pass 1.0 and no longer "
-                                               "measures the kernel")},
+                                     "basis": ("the lane design's bytes per read, each item at its own size: the read "
+                                               "(+ qualities when a quality filter is applied), the walk blocks over "
+                                               "its span (32 B per 64 positions), two seed slots (16 B), one 8-B "
+                                               "neighbour word per mismatching base -- x reads per launch / the "
+                                               "dominant kernel's average launch: a floor of the bytes moved"),
+                                     "survey_8d": {"bytes_per_read": b_read, "pass_ms": pass_s * 1e3,
+                                                   "achieved": b_read * npg / pass_s / 1e9 if pass_s > 0 else None,
+                                                   "note": ("SURVEY.md 8d prices one 16-B slot read per window, "
+                                                            "which the walk skips: not a bound of this design "
+                                                            "(it can pass the peak); reference only")}},
                      "kernels": {k: {"ms_avg": v[0] / v[1], "launches": v[1]} for k, v in kern.items() if v[1]}},
+        "job": job,
+        "job_index": (dict(product, neighbour_bits=not nb_built) if product is not None else None),
+        "neighbour_bits_breakeven": breakeven,
         "deferred_read_fraction": deferred / max(npg * args.steps, 1),
         "job_counters": job_counters,
         "index": {"build_s": index_total_s, "first_build_s": build_s, "prepare_s": prepare_s,
-                  "build_basis": ("FASTA genomes in host memory -> align-ready index: table + genome sets"
+                  "neighbour_bits_s": nb_s, "serving_build_s": index_total_s + nb_s,
+                  "reads_make_s": reads_make_s,
+                  "build_basis": ("FASTA genomes in host memory -> the job's align-ready index: table + genome sets"
                                   + (", EXTSIM statistics and greedy pass, rebuild of the kept genomes" if extsim else "")
-                                  + ", tiles / neighbour bits / Bloom filter"),
+                                  + ", tiles / Bloom filter (neighbour bits when the job repays them); "
+                                    "neighbour_bits_s: making them afterwards for the serving index"),
                   "n_kmers": int(info.n_kmers), "multi_genome_sets": int(info.n_multi_classes),
                   "table_bytes": int(info.table_bytes), "table_slots": int(info.table_slots)},
         "extsim": extsim,
@@ -739,14 +907,11 @@ def main():
     rl["per_rank"] = [{"rank": r["rank"], "dominant_kernel_ms": r["kernels_ms"].get(dominant),
                        "kernels_ms": r["kernels_ms"]} for r in ranks_kern]
     if world > 1 and all(dom_rank_ms):
-        # no counter pass at N > 1: the dominant kernel's section 8(d)
-        # algorithmic bytes per launch over its slowest rank's launch time
-        slow = max(dom_rank_ms)
-        rl["achieved"] = b_read * npg / (slow / 1e3) / 1e9
-        rl["frac"] = rl["achieved"] / HBM_PEAK_GBS
-        rl["achieved_basis"] = (f"ALGORITHMIC bytes (SURVEY.md 8d: {b_read} B per read x {npg} reads per rank and "
-                                f"launch) / the slowest rank's average {dominant} launch (HIP events on each rank's "
-                                "stream) / 8 TB/s; traffic is not measured at N > 1")
+        # no counter pass at N > 1: each rank's dominant-kernel launch priced
+        # with the fabric bytes per read a counter pass of the same config
+        # measured at N = 1 (profiles/lines_per_read.json), else with the
+        # design's algorithmic bytes
+        rl.update(multi_rank_roofline(args.config, dominant, npg, max(dom_rank_ms), design["bytes_per_read"]))
     rl["random_line_peak"], rl["random_line_peak_source"] = line_peak, line_src
     if per is not None:
         for k, d in per.items():
@@ -769,6 +934,7 @@ def main():
                 f"= {rl['achieved']:.0f} GB/s ({rl['frac']:.3f} of HBM peak)")
     # (at N > 1 frac is the algorithmic one, which prices skipped slot reads: no bound from it)
     rl["bound"] = bound_of(rl["frac"] if world == 1 else None, rl.get("sq"))
+    out["libpa"] = N.lib().pa_version().decode()
     if kept_path:
         os.unlink(kept_path)
     if rank == 0 and world == 1 and not args.no_e2e and not args.traffic_child:

@@ -60,6 +60,7 @@ def source_hash(stats: bool = False, defines=()) -> str:
     and the compile flags: what pa_version() of a library built from this
     checkout reports after "src=" (the library is rebuilt when it changes)."""
     flags = FLAGS + (["-DPA_STATS"] if stats else []) + [f"-D{d}" for d in defines]
+    flags = [f.replace(INCLUDE, "<repo>/include") for f in flags]  # (the checkout's path is not part of it)
     paths = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(INCLUDE, "pa.h")]
     return _digest(paths, [ARCH] + flags)
 

@@ -1043,12 +1043,42 @@ pa_status reserve_queues(pa_index *idx, uint64_t n) {
 }
 
 // Smallest quality byte of all reads and smallest read length (grid-stride).
-__global__ void k_reads_qstats(const uint8_t *__restrict__ qual, const uint64_t *__restrict__ off, uint64_t n,
-                               uint32_t *out) {
+// The quality bytes are read as 16-B vectors (the unaligned head and tail of
+// the range byte by byte), the byte minimum kept as packed 16-bit minima of
+// the even and odd bytes (v_pk_min_u16: one op per two bytes); four vectors in
+// flight per thread.  (Round 5: byte loads, 1.15 TB/s.)
+__global__ __launch_bounds__(256) void k_reads_qstats(const uint8_t *__restrict__ qual,
+                                                      const uint64_t *__restrict__ off, uint64_t n, uint32_t *out) {
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t b0 = off[0], b1 = off[n];
+    // [a0, a1): the part of [b0, b1) whose addresses are whole 16-B vectors
+    const uint64_t mis = (uint64_t)(uintptr_t)qual & 15;
+    const uint64_t a0 = min(b1, ((b0 + mis + 15) & ~15ull) - mis), a1 = max(a0, ((b1 + mis) & ~15ull) - mis);
     uint32_t qm = 255, lm = 0xFFFFFFFFu;
-    for (uint64_t i = b0 + tid; i < b1; i += stride) qm = min(qm, (uint32_t)qual[i]);
+    if (tid < 16) {  // the head and tail bytes outside the whole vectors
+        if (b0 + tid < a0) qm = min(qm, (uint32_t)qual[b0 + tid]);
+        if (a1 + tid < b1) qm = min(qm, (uint32_t)qual[a1 + tid]);
+    }
+    us2 mlo = {255, 255}, mhi = {255, 255};
+    const uint4 *vp = (const uint4 *)(qual + a0);  // (16-B aligned)
+    const uint64_t nv = (a1 - a0) >> 4;
+    auto fold = [&](const uint4 x) {
+        const uint32_t d[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t lo = d[j] & 0x00FF00FFu, hi = (d[j] >> 8) & 0x00FF00FFu;
+            mlo = __builtin_elementwise_min(mlo, __builtin_bit_cast(us2, lo));
+            mhi = __builtin_elementwise_min(mhi, __builtin_bit_cast(us2, hi));
+        }
+    };
+    uint64_t v = tid;
+    for (; v + 3 * stride < nv; v += 4 * stride) {
+        const uint4 x0 = vp[v], x1 = vp[v + stride], x2 = vp[v + 2 * stride], x3 = vp[v + 3 * stride];
+        fold(x0), fold(x1), fold(x2), fold(x3);
+    }
+    for (; v < nv; v += stride) fold(vp[v]);
+    qm = min(qm, (uint32_t)min(min(mlo.x, mlo.y), min(mhi.x, mhi.y)));
     for (uint64_t r = tid; r < n; r += stride) lm = min(lm, (uint32_t)min<uint64_t>(off[r + 1] - off[r], 0xFFFFFFFFull));
     for (int o = 32; o > 0; o >>= 1) {
         qm = min(qm, (uint32_t)__shfl_down(qm, o));
@@ -1071,7 +1101,7 @@ pa_status reads_measure(pa_reads *r, hipStream_t st) {
     PA_HIP(pa::dev_malloc(&d, 8));
     hipError_t e = hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_reads_qstats, dim3(2048), dim3(256), 0, st, r->qual, r->off, r->n, d);
+        hipLaunchKernelGGL(k_reads_qstats, dim3(4096), dim3(256), 0, st, r->qual, r->off, r->n, d);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);

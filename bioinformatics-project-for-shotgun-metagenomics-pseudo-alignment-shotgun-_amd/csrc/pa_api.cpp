@@ -168,7 +168,16 @@ pa_status pa_index_prepare(pa_index *idx, void *stream) {
     PA_CHECK(idx != nullptr, PA_EINVAL, "NULL argument");
     PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
     PA_HIP(hipSetDevice(idx->device));
-    PA_TRY(pa::index_prepare(idx, as_stream(stream)));
+    PA_TRY(pa::index_prepare(idx, as_stream(stream), ~0ull, true));
+    PA_HIP(hipStreamSynchronize(as_stream(stream)));
+    return PA_OK;
+}
+
+pa_status pa_index_prepare_ex(pa_index *idx, uint64_t expected_reads, void *stream) {
+    PA_CHECK(idx != nullptr, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
+    PA_HIP(hipSetDevice(idx->device));
+    PA_TRY(pa::index_prepare(idx, as_stream(stream), expected_reads, true));
     PA_HIP(hipStreamSynchronize(as_stream(stream)));
     return PA_OK;
 }
@@ -340,6 +349,20 @@ pa_status pa_reads_info(const pa_reads *reads, uint64_t *n_reads, uint64_t *n_ba
     if (n_reads) *n_reads = reads->n;
     if (n_bases) *n_bases = reads->n_bases;
     if (max_len) *max_len = reads->max_len;
+    return PA_OK;
+}
+
+pa_status pa_params_effective(const pa_reads *reads, const pa_params *in, pa_params *out, int32_t *q_min,
+                              void *stream) {
+    PA_CHECK(reads && in && out, PA_EINVAL, "NULL argument");
+    pa::DevParams dp, eff;
+    PA_TRY(to_dev_params(in, 1u << 20, &dp));
+    PA_HIP(hipSetDevice(reads->device));
+    PA_TRY(pa::effective_params(reads, dp, eff, as_stream(stream)));
+    const pa_params copy = *in;
+    *out = copy;
+    out->flags = eff.flags;
+    if (q_min) *q_min = reads->q_min < 0 ? 255 : reads->q_min;
     return PA_OK;
 }
 

@@ -1885,8 +1885,17 @@ pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st) {
     return build_nb(idx, st);
 }
 
-pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint) {
-    if (!idx->tiles_pending) return PA_OK;
+pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint, bool complete) {
+    if (!idx->tiles_pending) {  // (tiles made: the pending neighbour bits, if the reads still to come repay them)
+        if (complete && idx->nb_pending &&
+            (reads_hint == ~0ull || idx->reads_seen + reads_hint >= kNbReadsPerBase * idx->tile_n)) {
+            std::unique_ptr<PhaseTimer> own;
+            if (!t_phase) own.reset(new PhaseTimer(st));
+            PhaseScope ps(t_phase ? t_phase : own.get());
+            return build_nb(idx, st);
+        }
+        return PA_OK;
+    }
     idx->tiles_pending = 0;
     std::unique_ptr<PhaseTimer> own;  // (timed on its own unless a timed build called it)
     if (!t_phase) own.reset(new PhaseTimer(st));

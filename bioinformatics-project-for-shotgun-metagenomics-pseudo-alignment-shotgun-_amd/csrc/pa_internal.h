@@ -180,8 +180,10 @@ pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream
 // base the neighbour bits are left for later (index_note_reads makes them once
 // the reads aligned pass that point): they cost ~0.5 ns per base and save
 // ~0.25 ns per read on C2 (3.43 vs 1.87 G reads/s; build 0.36 vs 0.24 s).
-constexpr uint64_t kNbReadsPerBase = 4;
-pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint = ~0ull);
+constexpr uint64_t kNbReadsPerBase = PA_NB_READS_PER_BASE;
+// complete: also make neighbour bits left pending, when reads_hint (the reads
+// still to come; ~0: unknown) passes the break-even (pa_index_prepare[_ex]).
+pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint = ~0ull, bool complete = false);
 pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st);
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
                        uint32_t *size_out, hipStream_t st);
@@ -197,6 +199,8 @@ pa_status align_detail(pa_index *idx, const pa_reads *r, const DevParams &p, uin
                        uint32_t *hr, uint64_t *list_off, uint32_t *lists, uint64_t list_cap, uint64_t *list_total,
                        hipStream_t st);
 pa_status reads_measure(pa_reads *r, hipStream_t st);  // q_min / len_min of a batch (at its creation)
+// the filters an align of batch r applies: quality thresholds no read can fail dropped
+pa_status effective_params(const pa_reads *r, const DevParams &p, DevParams &out, hipStream_t st);
 pa_status ensure_workspace(pa_index *idx, size_t bytes);
 pa_status reserve_queues(pa_index *idx, uint64_t n);  // align queues for batches of up to n reads
 pa_status ensure_qmask(pa_index *idx, uint64_t n);    // quality-filter masks for batches of up to n reads

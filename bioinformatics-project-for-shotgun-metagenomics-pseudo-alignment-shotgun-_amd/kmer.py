@@ -729,6 +729,9 @@ class PseudoAlignment:
             if self._result is None:
                 self._result = N.Result(ref.index)
             prm = N.Params.make(m, p, mrq, mkq, mg)
+            # the align-side view this batch repays (the neighbour bits only
+            # past their break-even in reads per genome base; pa_index_prepare_ex)
+            ref.index.prepare(expected_reads=n)
             reads = N.Reads.upload(seq, qual, off, device=ref.index.device)
             N.align(ref.index, reads, prm, self._next_index, self._result)
             stats, _, _, _ = self._result.fetch()

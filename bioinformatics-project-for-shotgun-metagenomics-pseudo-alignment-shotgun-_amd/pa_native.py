@@ -28,14 +28,17 @@ HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4
 NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
 PA_BUILD_DEFER_TILES = 1
 PA_POS_REVERSE, PA_POS_RC_BIT = 1, 0x80000000
+PA_READS_UNKNOWN = 2 ** 64 - 1
+PA_NB_READS_PER_BASE = 4  # (include/pa.h: the neighbour bits' break-even, reads per genome base)
 
 # every symbol declared in include/pa.h
 EXPORTS = (
     "pa_last_error", "pa_version", "pa_device_count", "pa_runtime_start",
-    "pa_index_build", "pa_index_build_ex", "pa_index_reduce", "pa_index_prepare", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
+    "pa_index_build", "pa_index_build_ex", "pa_index_reduce", "pa_index_prepare", "pa_index_prepare_ex", "pa_index_free", "pa_index_get_info", "pa_index_lookup", "pa_index_class_genomes",
     "pa_index_positions",
     "pa_index_extsim_stats", "pa_index_dumpref",
-    "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_reads_download", "pa_reads_free",
+    "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_params_effective",
+    "pa_reads_download", "pa_reads_free",
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
     "pa_result_copy_in", "pa_result_free",
     "pa_align", "pa_align_detail", "pa_align_batch", "pa_align_fastq_file",
@@ -113,6 +116,7 @@ def lib():
         "pa_index_build_ex": (I32, [I32, ctypes.c_char_p, P, U32, I64, U32, P, PP]),
         "pa_index_reduce": (I32, [P, P, U32, U32, P]),
         "pa_index_prepare": (I32, [P, P]),
+        "pa_index_prepare_ex": (I32, [P, U64, P]),
         "pa_index_free": (None, [P]),
         "pa_index_get_info": (I32, [P, ctypes.POINTER(IndexInfo)]),
         "pa_index_lookup": (I32, [P, ctypes.c_char_p, U64, U32, P, P, P]),
@@ -126,6 +130,7 @@ def lib():
         "pa_reads_synthesize_mix": (I32, [P, U64, U32, U64, U64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                           P, PP]),
         "pa_reads_info": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U32)]),
+        "pa_params_effective": (I32, [P, ctypes.POINTER(Params), ctypes.POINTER(Params), ctypes.POINTER(I32), P]),
         "pa_reads_download": (I32, [P, U64, U64, P, P, P, P]),
         "pa_reads_free": (None, [P]),
         "pa_result_create": (I32, [P, PP]),
@@ -411,9 +416,15 @@ class Index:
         _check(st)
         self.n_genomes = len(sel)
 
-    def prepare(self, stream=None) -> None:
-        """Make a deferred build's align-side view now (pa_index_prepare)."""
-        _check(lib().pa_index_prepare(self._h, _stream(stream)))
+    def prepare(self, stream=None, expected_reads: Optional[int] = None) -> None:
+        """Make a deferred build's align-side view now (pa_index_prepare), or,
+        with expected_reads, the view a job of that many reads repays
+        (pa_index_prepare_ex: the neighbour bits only above the break-even;
+        a later call with more reads to come, or None, makes them)."""
+        if expected_reads is None:
+            _check(lib().pa_index_prepare(self._h, _stream(stream)))
+        else:
+            _check(lib().pa_index_prepare_ex(self._h, max(0, min(int(expected_reads), 2 ** 64 - 1)), _stream(stream)))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -555,6 +566,15 @@ class Reads:
             _check(lib().pa_reads_synthesize(index.handle, n_reads, read_len, first_read, seed, sub_rate,
                                              _stream(stream), ctypes.byref(h)))
         return cls(h, index.device)
+
+    def effective(self, params: "Params", stream=None) -> Tuple["Params", int]:
+        """(the filters an align of this batch applies, the batch's smallest
+        quality byte): pa_params_effective."""
+        out = Params()
+        q = I32(0)
+        _check(lib().pa_params_effective(self._h, ctypes.byref(params), ctypes.byref(out), ctypes.byref(q),
+                                         _stream(stream)))
+        return out, int(q.value)
 
     def download(self, first: int = 0, count: Optional[int] = None):
         count = self.n - first if count is None else count

@@ -10,6 +10,9 @@
  *   pa_index_build_ex        the same, the align-side view deferred        src/kmer.py:113-133
  *   pa_index_reduce          KmerReference._filter_similar_genomes (pruning)  src/kmer.py:232-263
  *   pa_index_prepare         (the deferred view, before the first align)
+ *   pa_index_prepare_ex      the same, sized for the reads the caller expects
+ *   pa_params_effective      the filters a batch's align applies (Read.mean_quality /
+ *                            kmer_quality thresholds no read can fail) src/kmer.py:394-408
  *   pa_index_lookup          KmerReference.get_kmer_references / __getitem__ src/kmer.py:284-298
  *   pa_index_class_genomes   (genome set of a k-mer, i.e. the keys of kmers[kmer]) src/kmer.py:130
  *   pa_index_positions       KmerReference.get_kmer_references (positions) and
@@ -163,9 +166,20 @@ pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t 
  * numbers (< n_genomes); flags as pa_index_build_ex.  On failure the index
  * holds nothing and may only be freed. */
 pa_status pa_index_reduce(pa_index *idx, const uint32_t *keep, uint32_t n_keep, uint32_t flags, void *stream);
-/* Make a deferred build's align-side view now (no-op otherwise); returns when
- * it is done. */
+/* Make a deferred build's align-side view now, with the neighbour bits a
+ * pa_index_prepare_ex or a FASTQ prefetch left pending (no-op otherwise);
+ * returns when it is done. */
 pa_status pa_index_prepare(pa_index *idx, void *stream);
+/* The same for a job of about expected_reads reads (PA_READS_UNKNOWN: as
+ * pa_index_prepare).  The one-substitution neighbour bits (DESIGN.md section
+ * 3) cost time per genome base and save time per read: below the break-even
+ * (PA_NB_READS_PER_BASE reads per genome base) they are left out, and made by
+ * the align that brings the reads aligned with this index past that point --
+ * or by a later call of this function whose expected_reads (the reads still to
+ * come) passes it.  Results never depend on them.  Returns when done. */
+#define PA_READS_UNKNOWN UINT64_MAX
+#define PA_NB_READS_PER_BASE 4
+pa_status pa_index_prepare_ex(pa_index *idx, uint64_t expected_reads, void *stream);
 void pa_index_free(pa_index *idx);
 pa_status pa_index_get_info(const pa_index *idx, pa_index_info *out);
 /* n k-mers of length kmer_len packed back to back; cls_out[i] = class id or -1
@@ -217,6 +231,13 @@ pa_status pa_reads_synthesize_mix(const pa_index *idx, uint64_t n_reads, uint32_
                                   uint64_t seed, double sub_rate, double rc_rate, double foreign_rate, void *stream,
                                   pa_reads **out);
 pa_status pa_reads_info(const pa_reads *reads, uint64_t *n_reads, uint64_t *n_bases, uint32_t *max_len);
+/* The filter arguments a pa_align of this batch applies (out, may alias in):
+ * a --min-read-quality / --min-kmer-quality at or below the batch's smallest
+ * quality byte can filter nothing (strict <, src/kmer.py:420, 587; quirk 5)
+ * and is dropped from the pass -- its flag cleared, the counters unchanged.
+ * q_min (nullable): that byte (255: no quality bytes). */
+pa_status pa_params_effective(const pa_reads *reads, const pa_params *in, pa_params *out, int32_t *q_min,
+                              void *stream);
 /* copy reads [first, first+count) back to the host (seq/qual: n_bases of that range) */
 pa_status pa_reads_download(const pa_reads *reads, uint64_t first, uint64_t count, uint8_t *seq, uint8_t *qual,
                             uint64_t *read_off, void *stream);

@@ -159,3 +159,24 @@ def test_kernel_short_names():
     }
     for mangled, want in names.items():
         assert bench.kernel_short_name(mangled) == want, mangled
+
+
+def test_roofline_models_are_bounds():
+    """SURVEY.md 8(d)'s bytes (one slot per window) passed the peak
+    over the measured pass, so the lines carry (a) the design's algorithmic
+    bytes per read (a floor of the bytes moved) and (b) at N > 1 the fabric
+    bytes per read an N = 1 counter pass measured (profiles/lines_per_read.json)
+    -- both below the peak at round 5's measured C4 launch (14.733 ms)."""
+    sys.path.insert(0, REPO)
+    import bench
+    cfg = bench.CONFIGS["c4"]
+    d = bench.design_bytes_per_read(cfg, quality_applied=False)
+    assert abs(d["bytes_per_read"] - (150 + 32 * (149 / 64 + 1) + 32 + 8 * 0.005 * 150)) < 1e-9
+    assert bench.design_bytes_per_read(cfg, True)["parts"]["read"] == 300
+    npg = cfg["reads_per_gpu"]
+    assert d["bytes_per_read"] * npg / 14.733e-3 / 1e9 / bench.HBM_PEAK_GBS < 1.0
+    rl = bench.multi_rank_roofline("c4", "k_align_lane", npg, 14.733, d["bytes_per_read"])
+    assert rl["achieved_basis"].startswith("N > 1 LINES MODEL") and "profiles/" in rl["achieved_basis"]
+    assert 0.3 < rl["frac"] <= 1.0
+    rl2 = bench.multi_rank_roofline("no_such_config", "k_align_lane", npg, 14.733, d["bytes_per_read"])
+    assert "design's algorithmic bytes" in rl2["achieved_basis"] and rl2["frac"] < 1.0

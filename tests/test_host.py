@@ -56,6 +56,13 @@ def test_version_and_error_string():
     assert isinstance(N.lib().pa_last_error(), bytes)
 
 
+def test_header_constants_match_binding():
+    text = open(os.path.join(REPO, "include", "pa.h")).read()
+    for name in ("PA_NB_READS_PER_BASE", "PA_MAX_K"):
+        m = re.search(rf"#define {name} (\d+)", text)
+        assert m and int(m.group(1)) == getattr(N, name), name
+
+
 def test_library_built_from_this_checkout():
     """pa_version() carries the SHA-256 of the sources, header and flags it was
     built from (build_native.source_hash); it must be this checkout's, so the
