@@ -54,6 +54,12 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kRun = 16;  // windows per thread in the genome scans
+// PA_BATCHED_INSERT=0 (compile time): the round-5 one-window-at-a-time insert
+// and fill passes for single-word keys (A/B)
+#ifndef PA_BATCHED_INSERT
+#define PA_BATCHED_INSERT 1
+#endif
+constexpr bool kBatchedInsert = PA_BATCHED_INSERT != 0;
 
 // Windows per thread of the per-genome build scans (insert, fill, tile
 // classes): PA_BUILD_RUN overrides (A/B).  Fewer per thread = more threads in
@@ -247,6 +253,147 @@ __global__ void k_build_insert(const uint8_t *__restrict__ codes, uint64_t gstar
     if (lane_id() == 0 && fresh) atomicAdd(n_kmers, (unsigned long long)fresh);
 }
 
+// Single-word keys (k <= 31), batched: a thread makes the keys of kInsBatch
+// windows first and loads their home slots (key + bookkeeping word, 16 B)
+// together -- kInsBatch random lines in flight instead of one chain of
+// dependent ones (a genome launch fills only ~2 waves per SIMD) -- then
+// settles each window: found, claimed (CAS EMPTY -> key) or probed on; and
+// counts g for the slot with ONE 64-bit CAS of the bookkeeping word
+// {cls = ~(last genome + 1), tpos = ~genomes} (round 5: atomicMin + atomicSub).
+// A stale plain load can only show EMPTY or an older (larger) cls: the CASes
+// correct both.  Exact for the same reason as k_build_insert: every thread of a
+// launch carries the same g.
+constexpr int kInsBatch = 8;
+__device__ __forceinline__ uint64_t *meta_of(Slot<1> *t, uint64_t pos) { return (uint64_t *)&t[pos].cls; }
+
+// Count genome `mark` for the slot at pos once: (cls, tpos) -> (mark, tpos - 1)
+// unless cls is already <= mark.  Returns the genomes listed before g (~old
+// tpos), or ~0u when g was counted already.
+__device__ __forceinline__ uint32_t count_genome(Slot<1> *t, uint64_t pos, uint64_t m, uint32_t mark) {
+    while ((uint32_t)m > mark) {
+        const uint64_t nv = ((uint64_t)((uint32_t)(m >> 32) - 1u) << 32) | mark;
+        const uint64_t old = atomicCAS((unsigned long long *)meta_of(t, pos), (unsigned long long)m,
+                                       (unsigned long long)nv);
+        if (old == m) return ~(uint32_t)(m >> 32);
+        m = old;
+    }
+    return ~0u;
+}
+
+__global__ __launch_bounds__(256) void k_build_insert1(const uint8_t *__restrict__ codes, uint64_t gstart,
+                                                       uint64_t nwin, int k, uint64_t mask0, uint32_t g,
+                                                       Slot<1> *table, HomeCfg hc, unsigned long long *n_kmers,
+                                                       uint32_t *err, int wpt) {
+    const uint64_t cap = hc.cap;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
+    uint32_t fresh = 0;
+    if (w0 < nwin) {
+        const uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
+        const uint8_t *s = codes + gstart + w0;
+        Key<1> key;
+        key.w[0] = 0;
+        int run = 0;
+        for (int i = 0; i < k - 1; i++) {
+            const uint32_t c = s[i];
+            run = c > 3 ? 0 : run + 1;
+            key_push(key, c & 3, mask0);
+        }
+        const uint32_t mark = ~(g + 1);
+        for (uint64_t wb = w0; wb < w1; wb += kInsBatch) {
+            uint64_t kk[kInsBatch], hp[kInsBatch];
+            uint32_t ok = 0;
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++) {
+                kk[i] = 0, hp[i] = 0;
+                if (wb + i < w1) {
+                    const uint32_t c = s[wb + i - w0 + k - 1];
+                    run = c > 3 ? 0 : run + 1;
+                    key_push(key, c & 3, mask0);
+                    if (run >= k) {  // (a window with a non-ACGT base is skipped, src/kmer.py:145)
+                        kk[i] = key.w[0];
+                        hp[i] = home_of(key, key_hash(key), hc);
+                        ok |= 1u << i;
+                    }
+                }
+            }
+            ulonglong2 sv[kInsBatch];
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++)
+                if (ok >> i & 1) sv[i] = *(const ulonglong2 *)&table[hp[i]];
+            // the claims of the windows whose home slot is EMPTY, issued together
+            uint64_t got[kInsBatch];
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++)
+                got[i] = (ok >> i & 1) && sv[i].x == EMPTY
+                             ? atomicCAS((unsigned long long *)&table[hp[i]].key[0], EMPTY, kk[i])
+                             : sv[i].x;
+            // settle every window's slot (probing on past other keys: rare at the build's load)
+            uint64_t pos[kInsBatch], m[kInsBatch];
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++) {
+                pos[i] = hp[i], m[i] = sv[i].y;
+                if (!(ok >> i & 1)) continue;
+                if (sv[i].x == EMPTY && got[i] == EMPTY) {  // claimed: a fresh key
+                    fresh++;
+                    m[i] = ~0ull;
+                    continue;
+                }
+                if (got[i] == kk[i]) {
+                    if (sv[i].x == EMPTY) m[i] = ld_agent(meta_of(table, pos[i]));  // (claimed by a sibling window)
+                    continue;
+                }
+                bool found = false;
+                uint64_t p = pos[i];
+                for (uint64_t it = 0; it < cap; it++) {
+                    p = (p + 1 == cap) ? 0 : p + 1;
+                    const ulonglong2 v = *(const ulonglong2 *)&table[p];
+                    uint64_t mm = v.y;
+                    if (v.x == EMPTY) {
+                        const uint64_t o = atomicCAS((unsigned long long *)&table[p].key[0], EMPTY, kk[i]);
+                        if (o == EMPTY) {
+                            fresh++;
+                            mm = ~0ull;
+                            found = true;
+                        } else if (o == kk[i]) {
+                            mm = ld_agent(meta_of(table, p));
+                            found = true;
+                        }
+                    } else if (v.x == kk[i]) {
+                        found = true;
+                    }
+                    if (found) {
+                        pos[i] = p, m[i] = mm;
+                        break;
+                    }
+                }
+                if (!found) {
+                    atomicOr(err, 1u);
+                    ok &= ~(1u << i);
+                }
+            }
+            // count g for every slot: the batch's CASes issued together, then
+            // the (rare) failed ones again one by one
+            uint64_t old[kInsBatch];
+            uint32_t want = 0;
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++) {
+                old[i] = m[i];
+                if ((ok >> i & 1) && (uint32_t)m[i] > mark) {
+                    want |= 1u << i;
+                    const uint64_t nv = ((uint64_t)((uint32_t)(m[i] >> 32) - 1u) << 32) | mark;
+                    old[i] = atomicCAS((unsigned long long *)meta_of(table, pos[i]), (unsigned long long)m[i],
+                                       (unsigned long long)nv);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++)
+                if ((want >> i & 1) && old[i] != m[i]) count_genome(table, pos[i], old[i], mark);
+        }
+    }
+    fresh = wave_sum_u32(fresh);
+    if (lane_id() == 0 && fresh) atomicAdd(n_kmers, (unsigned long long)fresh);
+}
+
 // Distinct k-mer estimate (HyperLogLog, 2^16 registers, ~0.4 % error) of one
 // genome's windows, to size the table of references whose windows would not
 // fit at the default load (e.g. 2000 x 4 Mbp: 8 G windows, ~3.8 G distinct).
@@ -386,6 +533,84 @@ __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart,
     }
 }
 
+// Pass 2 for single-word keys, batched like k_build_insert1: the windows'
+// slots loaded together, then each multi slot's genome list appended with one
+// CAS of its bookkeeping word (cls = ~(last genome + 1), tpos = ~listed).
+__global__ __launch_bounds__(256) void k_build_fill1(const uint8_t *__restrict__ codes, uint64_t gstart,
+                                                     uint64_t nwin, int k, uint64_t mask0, uint32_t g,
+                                                     Slot<1> *table, HomeCfg hc, uint32_t G,
+                                                     const uint64_t *__restrict__ off, uint32_t *lists, int wpt) {
+    const uint64_t cap = hc.cap;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
+    if (w0 >= nwin) return;
+    const uint64_t w1 = min(w0 + (uint64_t)wpt, nwin);
+    const uint8_t *s = codes + gstart + w0;
+    Key<1> key;
+    key.w[0] = 0;
+    int run = 0;
+    for (int i = 0; i < k - 1; i++) {
+        const uint32_t c = s[i];
+        run = c > 3 ? 0 : run + 1;
+        key_push(key, c & 3, mask0);
+    }
+    const uint32_t mark = ~(g + 1);
+    for (uint64_t wb = w0; wb < w1; wb += kInsBatch) {
+        uint64_t kk[kInsBatch], hp[kInsBatch];
+        uint32_t ok = 0;
+#pragma unroll
+        for (int i = 0; i < kInsBatch; i++) {
+            kk[i] = 0, hp[i] = 0;
+            if (wb + i < w1) {
+                const uint32_t c = s[wb + i - w0 + k - 1];
+                run = c > 3 ? 0 : run + 1;
+                key_push(key, c & 3, mask0);
+                if (run >= k) {
+                    kk[i] = key.w[0];
+                    hp[i] = home_of(key, key_hash(key), hc);
+                    ok |= 1u << i;
+                }
+            }
+        }
+        ulonglong2 sv[kInsBatch];
+#pragma unroll
+        for (int i = 0; i < kInsBatch; i++)
+            if (ok >> i & 1) sv[i] = *(const ulonglong2 *)&table[hp[i]];
+        uint64_t pos[kInsBatch], m[kInsBatch];
+        uint32_t want = 0;
+#pragma unroll
+        for (int i = 0; i < kInsBatch; i++) {
+            pos[i] = hp[i], m[i] = sv[i].y;
+            if (!(ok >> i & 1)) continue;
+            uint64_t cur = sv[i].x;
+            while (cur != kk[i] && cur != EMPTY) {  // (every window's key is in the table after pass 1)
+                pos[i] = (pos[i] + 1 == cap) ? 0 : pos[i] + 1;
+                const ulonglong2 v = *(const ulonglong2 *)&table[pos[i]];
+                cur = v.x, m[i] = v.y;
+            }
+            // multi slots not yet holding g (a singleton's genome is in cls already)
+            if (cur == kk[i] && (uint32_t)m[i] >= G && (uint32_t)m[i] > mark) want |= 1u << i;
+        }
+        // the batch's list appends: their CASes issued together, the (rare)
+        // failed ones again one by one
+        uint64_t old[kInsBatch];
+#pragma unroll
+        for (int i = 0; i < kInsBatch; i++) {
+            old[i] = m[i];
+            if (want >> i & 1) {
+                const uint64_t nv = ((uint64_t)((uint32_t)(m[i] >> 32) - 1u) << 32) | mark;
+                old[i] = atomicCAS((unsigned long long *)meta_of(table, pos[i]), (unsigned long long)m[i],
+                                   (unsigned long long)nv);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kInsBatch; i++) {
+            if (!(want >> i & 1)) continue;
+            const uint32_t p = old[i] == m[i] ? ~(uint32_t)(m[i] >> 32) : count_genome(table, pos[i], old[i], mark);
+            if (p != ~0u) lists[off[pos[i]] + p] = g;
+        }
+    }
+}
+
 __device__ __forceinline__ uint64_t list_hash(const uint32_t *l, uint32_t n) {
     uint64_t h = fmix64(0x51ED27C3A9F0B1D5ull ^ n);
     for (uint32_t i = 0; i < n; i++) h = fmix64(h ^ ((uint64_t)l[i] * 0x9E3779B97F4A7C15ull + i));
@@ -393,10 +618,16 @@ __device__ __forceinline__ uint64_t list_hash(const uint32_t *l, uint32_t n) {
 }
 
 // (after pass 2: a multi slot has cls >= G and tpos = ~deg)
+// A reference has few distinct genome sets and many multi slots (C4: ~10^4 sets,
+// ~4 x 10^8 slots), so almost every slot finds its set's entry already there:
+// a plain load first, the CAS only on an EMPTY entry (round 5 CASed every
+// slot onto a handful of hot words).  cache_pos: the set's entry is left in
+// the slot's cls as G + its position (cls is free after pass 2), so that
+// k_class_assign needs neither the hash nor the probe again.
 template <int NW>
-__global__ void k_class_insert(const Slot<NW> *table, uint64_t cap, uint32_t G, const uint64_t *off,
+__global__ void k_class_insert(Slot<NW> *table, uint64_t cap, uint32_t G, const uint64_t *off,
                                const uint32_t *lists, uint64_t *cs_key, uint64_t *cs_rep, uint64_t cs_cap,
-                               uint32_t *err) {
+                               uint32_t *err, int cache_pos) {
     uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; s < cap; s += stride) {
@@ -405,15 +636,21 @@ __global__ void k_class_insert(const Slot<NW> *table, uint64_t cap, uint32_t G, 
         uint64_t pos = home_slot(fmix64(h), cs_cap);
         uint64_t it = 0;
         for (; it < cs_cap; it++) {
-            uint64_t old = atomicCAS((unsigned long long *)&cs_key[pos], EMPTY, h);
-            if (old == EMPTY) {
-                cs_rep[pos] = s;
-                break;
+            uint64_t cur = ld_agent(&cs_key[pos]);
+            if (cur == EMPTY) {
+                cur = atomicCAS((unsigned long long *)&cs_key[pos], EMPTY, h);
+                if (cur == EMPTY) {
+                    cs_rep[pos] = s;
+                    break;
+                }
             }
-            if (old == h) break;
+            if (cur == h) break;
             pos = (pos + 1 == cs_cap) ? 0 : pos + 1;
         }
-        if (it == cs_cap) atomicOr(err, 4u);
+        if (it == cs_cap)
+            atomicOr(err, 4u);
+        else if (cache_pos)
+            table[s].cls = G + (uint32_t)pos;
     }
 }
 
@@ -465,16 +702,22 @@ template <int NW>
 __global__ void k_class_assign(Slot<NW> *table, uint64_t cap, const uint64_t *off, const uint32_t *lists,
                                const uint64_t *cs_key, const uint64_t *cs_rep, const uint32_t *cs_id, uint64_t cs_cap,
                                const uint32_t *class_size, const uint64_t *class_off, uint32_t n_genomes,
-                               uint32_t *err) {
+                               uint32_t *err, int cache_pos) {
     uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (; s < cap; s += stride) {
-        if (table[s].key[0] == EMPTY || table[s].cls < n_genomes) continue;
-        const uint32_t d = ~table[s].tpos;
+        const Slot<NW> me = table[s];
+        if (me.key[0] == EMPTY || me.cls < n_genomes) continue;
+        const uint32_t d = ~me.tpos;
         const uint32_t *l = lists + off[s];
-        uint64_t h = list_hash(l, d);
-        uint64_t pos = home_slot(fmix64(h), cs_cap);
-        while (cs_key[pos] != h) pos = (pos + 1 == cs_cap) ? 0 : pos + 1;
+        uint64_t pos;
+        if (cache_pos) {
+            pos = me.cls - n_genomes;  // (k_class_insert left the set's entry there)
+        } else {
+            const uint64_t h = list_hash(l, d);
+            pos = home_slot(fmix64(h), cs_cap);
+            while (cs_key[pos] != h) pos = (pos + 1 == cs_cap) ? 0 : pos + 1;
+        }
         uint64_t rep = cs_rep[pos];
         const uint32_t id = cs_id[pos];
         bool same = class_size[id] == d;
@@ -1299,8 +1542,13 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
         if (k <= 0 || (uint64_t)k > len) continue;
         uint64_t nwin = len - k + 1;
-        hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
-                           idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, cnt + 0, err, wpt);
+        if (NW == 1 && kBatchedInsert)
+            hipLaunchKernelGGL(k_build_insert1, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
+                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, (Slot<1> *)table, idx->home, cnt + 0,
+                               err, wpt);
+        else
+            hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
+                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, cnt + 0, err, wpt);
     }
     B_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_build_prep<NW>, dim3(grid_for(cap, kBlock) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0,
@@ -1325,9 +1573,14 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             uint64_t len = idx->h_goff[g + 1] - idx->h_goff[g];
             if ((uint64_t)k > len) continue;
             uint64_t nwin = len - k + 1;
-            hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
-                               idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, G, off, lists,
-                               wpt);
+            if (NW == 1 && kBatchedInsert)
+                hipLaunchKernelGGL(k_build_fill1, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
+                                   idx->codes, idx->h_goff[g], nwin, k, mask0, g, (Slot<1> *)table, idx->home, G, off,
+                                   lists, wpt);
+            else
+                hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
+                                   idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, G, off, lists,
+                                   wpt);
         }
         B_HIP(hipGetLastError());
         // distinct genome sets: a hash over the multi slots' genome lists.  A
@@ -1337,13 +1590,15 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         const uint64_t cs_max = 2 * n_multi + 64;
         uint64_t cs_cap = std::min<uint64_t>(cs_max, (1ull << 24) + 64);
         unsigned sgrid = grid_for(cap) > 65536 ? 65536 : grid_for(cap);
+        int cache_pos = 0;
         for (;;) {
             B_HIP(pa::dev_malloc(&cs_key, cs_cap * 8));
             B_HIP(pa::dev_malloc(&cs_rep, cs_cap * 8));
             hipLaunchKernelGGL(k_fill_u64, dim3(grid_for(cs_cap) > 65536 ? 65536 : grid_for(cs_cap)), dim3(kBlock), 0,
                                st, cs_key, cs_cap, EMPTY);
+            cache_pos = (uint64_t)G + cs_cap < 0xFFF00000ull ? 1 : 0;  // (G + position below pass 2's marks)
             hipLaunchKernelGGL(k_class_insert<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, G, off, lists,
-                               cs_key, cs_rep, cs_cap, err);
+                               cs_key, cs_rep, cs_cap, err, cache_pos);
             B_HIP(hipGetLastError());
             B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
             B_HIP(hipStreamSynchronize(st));
@@ -1386,7 +1641,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
                                dim3(kBlock), 0, st, n_cls, idx->class_off, idx->class_genomes, idx->class_mask);
         }
         hipLaunchKernelGGL(k_class_assign<NW>, dim3(sgrid), dim3(kBlock), 0, st, table, cap, off, lists, cs_key,
-                           cs_rep, cs_id, cs_cap, idx->class_size, idx->class_off, G, err);
+                           cs_rep, cs_id, cs_cap, idx->class_size, idx->class_off, G, err, cache_pos);
         B_HIP(hipGetLastError());
         B_HIP(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, st));
         B_HIP(hipStreamSynchronize(st));
