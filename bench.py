@@ -140,7 +140,7 @@ def e2e_pass():
         return {"error": f"{type(e).__name__}: {e}"}
     keep = ("workload", "cli_wall_s", "cli_wall_runs_s", "cli_reads_per_s", "cli_stdout_equals_api",
             "device_parse_path_taken", "host_path_summary_equal", "phases", "dumpref_c2_to_devnull", "fq_gz",
-            "fq_plain_gz", "cli_stages")
+            "fq_plain_gz", "cli_stages", "sharded")
     out = {k: d.get(k) for k in keep}
     out["basis"] = ("median wall time of 3 runs of the whole `main.py -t dumpalign -g c2.fa -k 31 --reads c2.fq` "
                     "command (an idle device between runs), files in the page cache; reads/s = 10 M / that")
@@ -640,7 +640,7 @@ def main():
         log(f"[rank {rank}] EXTSIM: kept {len(keep)} of {len(idents)} in {extsim['total_s']:.1f}s")
     t0 = time.perf_counter()
     # the job's index: the align-side view this rank's npg reads repay (the
-    # neighbour bits only past PA_NB_READS_PER_BASE reads per genome base:
+    # neighbour bits only past PA_NB_READS_PER_KBASE / 1000 reads per genome base:
     # pa_index_prepare_ex)
     index.prepare(stream, expected_reads=npg)
     prepare_s = time.perf_counter() - t0
@@ -809,7 +809,7 @@ def main():
         breakeven = {"neighbour_bits_s": nb_max, "saved_ns_per_read": saved * 1e9,
                      "cost_ns_per_base": per_base * 1e9,
                      "reads_per_base": per_base / saved if saved > 0 else None,
-                     "policy_reads_per_base": N.PA_NB_READS_PER_BASE,
+                     "policy_reads_per_base": N.PA_NB_READS_PER_KBASE / 1000,
                      "basis": "neighbour bits' build time per genome window / align time they save per read "
                               "(job-index pass - serving-index pass, per read)"}
     out = {

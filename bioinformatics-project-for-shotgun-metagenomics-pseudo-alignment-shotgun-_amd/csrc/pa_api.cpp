@@ -446,6 +446,15 @@ pa_status pa_result_copy_in(pa_result *res, const void *sum_src, const void *min
     return PA_OK;
 }
 
+pa_status pa_result_load(pa_result *res, const uint64_t *sum_block, const uint64_t *min_block) {
+    PA_CHECK(res && sum_block && (res->n_genomes == 0 || min_block), PA_EINVAL, "NULL argument");
+    PA_HIP(hipSetDevice(res->device));
+    const uint64_t G = res->n_genomes;
+    PA_HIP(hipMemcpy(res->sum_block, sum_block, (6 + 2 * G) * 8, hipMemcpyHostToDevice));
+    if (G) PA_HIP(hipMemcpy(res->min_block, min_block, G * 8, hipMemcpyHostToDevice));
+    return PA_OK;
+}
+
 pa_status pa_result_fetch(const pa_result *res, pa_stats *stats, uint64_t *unique_reads, uint64_t *ambiguous_reads,
                           uint64_t *first_key, void *stream) {
     PA_CHECK(res != nullptr, PA_EINVAL, "NULL argument");
@@ -508,6 +517,50 @@ pa_status pa_align_fastq_file(const pa_index *idx, const char *path, const pa_pa
     return pa::align_fastq_file(const_cast<pa_index *>(idx), path, dp, read_index_base, acc, threads > 0 ? threads : 8,
                                 window_bytes ? window_bytes : (128ull << 20), as_stream(stream), n_reads);
 }
+
+pa_status pa_align_fastq_range(const pa_index *idx, const char *path, uint64_t offset, uint64_t length,
+                               const pa_params *params, uint64_t read_index_base, pa_result *acc, int32_t threads,
+                               uint64_t window_bytes, void *stream, uint64_t *n_reads, pa_idset **ids) {
+    PA_CHECK(idx && path && acc, PA_EINVAL, "NULL argument");
+    PA_CHECK(!idx->released, PA_EINVAL, "the index was released by a failed pa_index_reduce: it may only be freed");
+    PA_CHECK(acc->n_genomes == idx->n_genomes, PA_EINVAL, "result was created for a different index");
+    PA_CHECK(acc->device == idx->device, PA_EINVAL, "index and result must live on the same device");
+    PA_CHECK(length > 0, PA_EINVAL, "empty byte range");
+    if (ids) *ids = nullptr;
+    pa::DevParams dp;
+    PA_TRY(to_dev_params(params, idx->n_genomes, &dp));
+    PA_HIP(hipSetDevice(idx->device));
+    if (n_reads) *n_reads = 0;
+    pa_idset *set = nullptr;
+    if (ids) {
+        set = new (std::nothrow) pa_idset();
+        PA_CHECK(set != nullptr, PA_ENOMEM, "out of host memory");
+    }
+    const pa_status rc = pa::align_fastq_file(const_cast<pa_index *>(idx), path, dp, read_index_base, acc,
+                                              threads > 0 ? threads : 8, window_bytes ? window_bytes : (128ull << 20),
+                                              as_stream(stream), n_reads, offset, length, set ? &set->h : nullptr);
+    if (rc != PA_OK) {
+        delete set;
+        return rc;
+    }
+    if (ids) *ids = set;
+    return PA_OK;
+}
+
+pa_status pa_idsets_disjoint(const pa_idset *const *sets, uint32_t n_sets, int32_t device, int32_t *disjoint) {
+    PA_CHECK(disjoint && (n_sets == 0 || sets), PA_EINVAL, "NULL argument");
+    std::vector<const std::vector<uint64_t> *> v;
+    for (uint32_t i = 0; i < n_sets; i++) {
+        PA_CHECK(sets[i] != nullptr, PA_EINVAL, "NULL id set");
+        v.push_back(&sets[i]->h);
+    }
+    bool d = true;
+    PA_TRY(pa::idsets_disjoint(v, device, &d));
+    *disjoint = d ? 1 : 0;
+    return PA_OK;
+}
+
+void pa_idset_free(pa_idset *ids) { delete ids; }
 
 pa_status pa_index_dumpref(const pa_index *idx, const uint8_t *keep, const uint32_t *desc_of, uint32_t n_desc,
                            const char *const *desc_json, int32_t fd, int32_t threads, uint64_t *desc_unique,

@@ -342,6 +342,38 @@ struct Source {  // plain file (positional reads on host threads) or gzip (pa_gz
 
 namespace pa {
 
+// The occupied entries of an id set, compacted (order unspecified).
+__global__ void k_ids_compact(const unsigned long long *ids, uint64_t cap, unsigned long long *out, uint64_t out_cap,
+                              unsigned long long *n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long h = ids[i];
+        if (!h) continue;
+        const unsigned long long at = atomicAdd(n, 1ull);
+        if (at < out_cap) out[at] = h;
+    }
+}
+
+// Insert the id hashes of several ranges into one set; *dup = 1 when a hash
+// arrives twice (within a range the parse already refused duplicates, so a
+// repeat is a duplicate id across ranges -- or a 2^-64 collision: the exact
+// parser decides).
+__global__ void k_ids_union(const unsigned long long *h_in, uint64_t n, unsigned long long *set, uint64_t cap,
+                            unsigned int *dup) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long h = h_in[i];
+        uint64_t pos = h & (cap - 1);
+        for (uint64_t it = 0; it < cap; it++) {
+            const unsigned long long old = atomicCAS(&set[pos], 0ull, h);
+            if (old == 0ull) break;
+            if (old == h) {
+                atomicOr(dup, 1u);
+                break;
+            }
+            pos = (pos + 1) & (cap - 1);
+        }
+    }
+}
+
 // Device buffers of the per-window parse (sized for windows of up to `span`
 // bytes of text) and the id set of the whole file.
 struct ParseBufs {
@@ -791,7 +823,8 @@ pa_status align_fastq_prefetched(pa_index *idx, pa_fastq_prefetch *pf, const Dev
     return PA_OK;
 }
 pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,
-                           int threads, uint64_t window, hipStream_t st, uint64_t *n_reads) {
+                           int threads, uint64_t window, hipStream_t st, uint64_t *n_reads, uint64_t offset,
+                           uint64_t length, std::vector<uint64_t> *ids_out) {
     // PA_STREAM_TIMING=1: where the time goes (stderr)
     const bool timing = env_on("PA_STREAM_TIMING");
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -806,6 +839,10 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         const size_t pl = strlen(path);
         const bool gz = pl >= 3 && strcmp(path + pl - 3, ".gz") == 0;
         if (gz) {
+            if (offset != 0 || length != ~0ull) {
+                set_error("pa_align_fastq_range: byte ranges of plain files only");
+                return PA_EUNSUPPORTED;
+            }
             PA_TRY(pa::gz_open(path, src.threads, &src.gz));  // (not gzip data: PA_ENOTCANON, the exact path)
         } else {
             src.fd = open(path, O_RDONLY);
@@ -815,13 +852,16 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
                 set_error(std::string("cannot open ") + path);
                 return PA_EIO;
             }
-            src.size = (uint64_t)sb.st_size;
+            // a byte range [offset, offset + length) read as if it were the file
+            // (pa_align_fastq_range: the caller cuts on record boundaries)
+            src.size = std::min<uint64_t>((uint64_t)sb.st_size, offset + std::min<uint64_t>(length, ~0ull - offset));
+            src.pos = std::min<uint64_t>(offset, src.size);
         }
     }
     const uint64_t W = std::min<uint64_t>(std::max<uint64_t>(window, 1 << 16), 1ull << 31) & ~(uint64_t)(kTile - 1);
     const uint64_t dbytes = kCarryMax + W + 2 * kTile;       // one device text buffer
     const uint64_t est_rec = src.gz ? std::max<uint64_t>(1ull << 24, pa::gz_text_size(src.gz) / 16 + 1024)
-                                    : src.size / 16 + 1024;
+                                    : (src.size - src.pos) / 16 + 1024;
 
     uint8_t *H[2] = {nullptr, nullptr}, *D[2] = {nullptr, nullptr};
     ParseBufs B;
@@ -944,6 +984,32 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
         rc = PA_ENOTCANON;
     }
     if (rc == PA_OK && n_reads) *n_reads = records;
+    if (rc == PA_OK && ids_out) {  // the range's id hashes (pa_idsets_disjoint: duplicates across ranges)
+        unsigned long long *d_out = nullptr, *d_n = nullptr;
+        unsigned long long h_n = 0;
+        hipError_t e = pa::dev_malloc(&d_out, std::max<uint64_t>(records, 1) * 8);
+        if (e == hipSuccess) e = pa::dev_malloc(&d_n, 8);
+        if (e == hipSuccess) e = hipMemsetAsync(d_n, 0, 8, st);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_ids_compact, dim3((unsigned)std::min<uint64_t>((B.ids_cap + 255) / 256, 65536)),
+                               dim3(256), 0, st, B.ids, B.ids_cap, d_out, std::max<uint64_t>(records, 1), d_n);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&h_n, d_n, 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess && h_n != records) e = hipErrorUnknown;  // (one hash per record: the set holds them all)
+        if (e == hipSuccess) {
+            ids_out->resize(h_n);
+            e = hipMemcpyAsync(ids_out->data(), d_out, h_n * 8, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+        }
+        pa::dev_free(d_out);
+        pa::dev_free(d_n);
+        if (e != hipSuccess) {
+            set_error(std::string("pa_align_fastq_range: id set export: ") + hipGetErrorString(e));
+            rc = PA_EDEVICE;
+        }
+    }
     const auto t_c = now();
     cleanup();
     if (timing)
@@ -952,6 +1018,52 @@ pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm
                 (unsigned long long)records, t_alloc, t_prepare, t_wait_read, t_wait_meta, t_wait_rec, ms(t_c, now()),
                 ms(t_start, now()));
     return rc;
+}
+
+}  // namespace pa
+
+namespace pa {
+
+// Whether id hash sets (one per byte range of a file) are pairwise disjoint:
+// all inserted into one device set on `device`.
+pa_status idsets_disjoint(const std::vector<const std::vector<uint64_t> *> &sets, int device, bool *disjoint) {
+    *disjoint = true;
+    uint64_t total = 0;
+    for (auto *v : sets) total += v->size();
+    if (total == 0) return PA_OK;
+    PA_HIP(hipSetDevice(device));
+    uint64_t cap = 1024;
+    while (cap < 2 * total) cap <<= 1;
+    unsigned long long *set = nullptr, *in = nullptr;
+    unsigned int *dup = nullptr, h_dup = 0;
+    hipStream_t st = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = pa::dev_malloc(&set, cap * 8);
+    if (e == hipSuccess) e = pa::dev_malloc(&in, total * 8);
+    if (e == hipSuccess) e = pa::dev_malloc(&dup, 4);
+    if (e == hipSuccess) e = hipMemsetAsync(set, 0, cap * 8, st);
+    if (e == hipSuccess) e = hipMemsetAsync(dup, 0, 4, st);
+    uint64_t at = 0;
+    for (auto *v : sets) {
+        if (e == hipSuccess && !v->empty())
+            e = hipMemcpyAsync(in + at, v->data(), v->size() * 8, hipMemcpyHostToDevice, st);
+        at += v->size();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_ids_union, dim3((unsigned)std::min<uint64_t>((total + 255) / 256, 65536)), dim3(256), 0, st,
+                           in, total, set, cap, dup);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&h_dup, dup, 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (st) hipStreamSynchronize(st);
+    pa::dev_free(set);
+    pa::dev_free(in);
+    pa::dev_free(dup);
+    if (st) hipStreamDestroy(st);
+    PA_HIP(e);
+    *disjoint = h_dup == 0;
+    return PA_OK;
 }
 
 }  // namespace pa

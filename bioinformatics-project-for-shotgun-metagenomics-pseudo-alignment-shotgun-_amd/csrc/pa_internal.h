@@ -113,7 +113,7 @@ struct pa_index {
     int64_t tile_nbm_mg = -1;          //   interleaved, one 16-B load per mismatch (pa_align, cached; when it fits)
     int nb_skip = 0;                   // (index_prepare) make the tiles without the neighbour bits
     int nb_pending = 0;                // 1: tiles made, neighbour bits not yet (too few reads expected)
-    uint64_t reads_seen = 0;           // reads aligned so far (the neighbour bits follow at kNbReadsPerBase)
+    uint64_t reads_seen = 0;           // reads aligned so far (the neighbour bits follow at kNbReadsPerKBase / 1000 per base)
     uint32_t *tile_gblk = nullptr;     // [(tile_n >> 16) + 2] the genome holding position j << 16
     uint64_t *bloom = nullptr;         // [2^bloom_lg] Bloom filter of the table's keys (k_bloom_build), optional
     uint32_t *mm_bits = nullptr;       // [2^mm_lg / 32] minimizer presence bitmap (k_mm_build), optional
@@ -164,6 +164,10 @@ struct pa_reads {
     int64_t len_min = -1;
 };
 
+struct pa_idset {  // id hashes of a FASTQ byte range (pa_align_fastq_range)
+    std::vector<uint64_t> h;
+};
+
 struct pa_result {
     int device = 0;
     uint32_t n_genomes = 0;
@@ -176,11 +180,13 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
                       hipStream_t st, bool defer_tiles, uint8_t *dev_codes = nullptr);
 pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream_t st, bool defer_tiles);
 // The tiles of a deferred build (no-op otherwise).  reads_hint: the reads the
-// caller expects to align with this index; below kNbReadsPerBase per genome
+// caller expects to align with this index; below kNbReadsPerKBase / 1000 per genome
 // base the neighbour bits are left for later (index_note_reads makes them once
 // the reads aligned pass that point): they cost ~0.5 ns per base and save
 // ~0.25 ns per read on C2 (3.43 vs 1.87 G reads/s; build 0.36 vs 0.24 s).
-constexpr uint64_t kNbReadsPerBase = PA_NB_READS_PER_BASE;
+constexpr uint64_t kNbReadsPerKBase = PA_NB_READS_PER_KBASE;
+// reads past the neighbour bits' break-even for an index of `bases` genome bases
+inline bool nb_repaid(uint64_t reads, uint64_t bases) { return reads >= (bases * kNbReadsPerKBase + 999) / 1000; }
 // complete: also make neighbour bits left pending, when reads_hint (the reads
 // still to come; ~0: unknown) passes the break-even (pa_index_prepare[_ex]).
 pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint = ~0ull, bool complete = false);
@@ -204,8 +210,12 @@ pa_status effective_params(const pa_reads *r, const DevParams &p, DevParams &out
 pa_status ensure_workspace(pa_index *idx, size_t bytes);
 pa_status reserve_queues(pa_index *idx, uint64_t n);  // align queues for batches of up to n reads
 pa_status ensure_qmask(pa_index *idx, uint64_t n);    // quality-filter masks for batches of up to n reads
+// offset / length: a byte range of a plain file, cut on record boundaries
+// (pa_align_fastq_range); ids_out: the range's id hashes
 pa_status align_fastq_file(pa_index *idx, const char *path, const DevParams &prm, uint64_t base, pa_result *acc,
-                           int threads, uint64_t window, hipStream_t st, uint64_t *n_reads);
+                           int threads, uint64_t window, hipStream_t st, uint64_t *n_reads, uint64_t offset = 0,
+                           uint64_t length = ~0ull, std::vector<uint64_t> *ids_out = nullptr);
+pa_status idsets_disjoint(const std::vector<const std::vector<uint64_t> *> &sets, int device, bool *disjoint);
 pa_status fastq_prefetch_start(const char *path, int device, int threads, uint64_t window, pa_fastq_prefetch **out);
 void fastq_prefetch_free(pa_fastq_prefetch *pf);
 pa_status align_fastq_prefetched(pa_index *idx, pa_fastq_prefetch *pf, const DevParams &prm, uint64_t base,

@@ -66,6 +66,8 @@ def _early_reads_path(argv: List[str]) -> Optional[str]:
         i += 1
     if task != "dumpalign" or not reads or not reads.endswith(_FQ_PLAIN_EXT):
         return None
+    if os.environ.get("PA_GPUS", "1") not in ("", "0", "1"):  # (read-sharded over GPUs: no whole-file prefetch)
+        return None
     if os.environ.get("PA_STREAM", "1") == "0" or os.environ.get("PA_PREFETCH", "1") == "0":
         return None
     return reads
@@ -255,6 +257,34 @@ def _check_task(args: argparse.Namespace) -> None:
         sys.exit("Error: Unsupported task.")
 
 
+def _dumpalign_sharded(args: argparse.Namespace, filt) -> Optional[PseudoAlignment]:
+    """PA_GPUS=N > 1: the dumpalign job read-sharded over N devices (pa_shard:
+    one index replica per device, one byte range of the FASTQ file each, the
+    counters reduced on the host); None where it does not apply -- one GPU,
+    a .gz or non-canonical file, a duplicate id across ranges -- and the
+    one-GPU path runs (and raises the reference's errors)."""
+    import pa_shard
+    n, share = pa_shard.gpus_from_env()
+    if n < 2 or args.reads.endswith(".gz"):
+        return None
+    FASTAQFile.check_extension(args.reads)
+    devices = pa_shard.devices_for(n, share)
+    if len(devices) < 2:
+        return None
+    container = FASTAFile(args.genomefile).container
+    _stage("fasta parsed")
+    refs = pa_shard.build_replicas(args.kmer_size, container, devices, args.filter_similar,
+                                   args.similarity_threshold)
+    _stage(f"{len(refs)} references built")
+    pa = pa_shard.align_sharded(refs, args.reads, *filt)
+    _stage("reads aligned (sharded)" if pa is not None else "sharded path not taken")
+    if pa is None:
+        return None
+    if _TIMING:
+        print(f"[pa_cli] shards (offset, bytes, records): {pa._shards}", file=sys.stderr, flush=True)
+    return pa
+
+
 def _run(args: argparse.Namespace) -> None:
     filt = (args.unique_threshold, args.ambiguous_threhold, args.min_read_quality, args.min_kmer_quality,
             args.max_genomes)
@@ -295,6 +325,10 @@ def _run(args: argparse.Namespace) -> None:
         elif args.genomefile and args.kmer_size and args.reads:
             validate_file_readable(args.reads, "FASTQ reads")
             validate_file_readable(args.genomefile, "Genome FASTA")
+            sharded = _dumpalign_sharded(args, filt)
+            if sharded is not None:
+                _print_json(sharded.get_summary())
+                return
             pf = _prefetch_reads(args.reads)
             ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
             _print_json(create_alignment_from_reference(ref, args.reads, *filt, prefetch=pf).get_summary())

@@ -29,7 +29,7 @@ NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
 PA_BUILD_DEFER_TILES = 1
 PA_POS_REVERSE, PA_POS_RC_BIT = 1, 0x80000000
 PA_READS_UNKNOWN = 2 ** 64 - 1
-PA_NB_READS_PER_BASE = 4  # (include/pa.h: the neighbour bits' break-even, reads per genome base)
+PA_NB_READS_PER_KBASE = 3500  # (include/pa.h: the neighbour bits' break-even, reads per 1000 genome bases)
 
 # every symbol declared in include/pa.h
 EXPORTS = (
@@ -40,8 +40,9 @@ EXPORTS = (
     "pa_reads_upload", "pa_reads_synthesize", "pa_reads_synthesize_mix", "pa_reads_info", "pa_params_effective",
     "pa_reads_download", "pa_reads_free",
     "pa_result_create", "pa_result_reset", "pa_result_fetch", "pa_result_device_view", "pa_result_copy_out",
-    "pa_result_copy_in", "pa_result_free",
-    "pa_align", "pa_align_detail", "pa_align_batch", "pa_align_fastq_file",
+    "pa_result_copy_in", "pa_result_load", "pa_result_free",
+    "pa_align", "pa_align_detail", "pa_align_batch", "pa_align_fastq_file", "pa_align_fastq_range",
+    "pa_idsets_disjoint", "pa_idset_free",
     "pa_fastq_prefetch_start", "pa_align_fastq_prefetched", "pa_fastq_prefetch_free",
     "pa_comm_unique_id", "pa_comm_init", "pa_comm_free", "pa_comm_count", "pa_counters_reduce",
     "pa_profile_enable", "pa_profile_read", "pa_profile_read_kernels", "pa_mem_trim",
@@ -139,12 +140,17 @@ def lib():
         "pa_result_device_view": (I32, [P, PP, ctypes.POINTER(U64), PP, ctypes.POINTER(U64)]),
         "pa_result_copy_out": (I32, [P, P, P, P]),
         "pa_result_copy_in": (I32, [P, P, P, P]),
+        "pa_result_load": (I32, [P, P, P]),
         "pa_result_free": (None, [P]),
         "pa_align": (I32, [P, P, ctypes.POINTER(Params), U64, P, P]),
         "pa_align_detail": (I32, [P, P, ctypes.POINTER(Params), P, P, P, P, P, U64, ctypes.POINTER(U64), P]),
         "pa_align_batch": (I32, [P, P, P, P, U64, U64, ctypes.POINTER(Params), ctypes.POINTER(Stats), P, P, P, P]),
         "pa_align_fastq_file": (I32, [P, ctypes.c_char_p, ctypes.POINTER(Params), U64, P, I32, U64, P,
                                       ctypes.POINTER(U64)]),
+        "pa_align_fastq_range": (I32, [P, ctypes.c_char_p, U64, U64, ctypes.POINTER(Params), U64, P, I32, U64, P,
+                                       ctypes.POINTER(U64), PP]),
+        "pa_idsets_disjoint": (I32, [ctypes.POINTER(P), U32, I32, ctypes.POINTER(I32)]),
+        "pa_idset_free": (None, [P]),
         "pa_fastq_prefetch_start": (I32, [ctypes.c_char_p, I32, I32, U64, PP]),
         "pa_align_fastq_prefetched": (I32, [P, P, ctypes.POINTER(Params), U64, P, P, ctypes.POINTER(U64)]),
         "pa_fastq_prefetch_free": (None, [P]),
@@ -643,6 +649,14 @@ class Result:
         """D2D copy of [stats|unique|ambiguous] and [first_key] into caller device buffers."""
         _check(lib().pa_result_copy_out(self._h, sum_dst_ptr or None, min_dst_ptr or None, _stream(stream)))
 
+    def load(self, stats: np.ndarray, unique: np.ndarray, ambiguous: np.ndarray, first_key: np.ndarray) -> None:
+        """Overwrite the counters from host arrays (pa_result_load): the
+        host SUM / MIN of read shards."""
+        sb = np.ascontiguousarray(np.concatenate([stats, unique, ambiguous]).astype(np.uint64))
+        mb = np.ascontiguousarray(np.asarray(first_key, dtype=np.uint64))
+        assert sb.size == self.n_sum and mb.size == self.n_genomes
+        _check(lib().pa_result_load(self._h, _ptr(sb), _ptr(mb) if mb.size else None))
+
     def copy_in(self, sum_src_ptr: int, min_src_ptr: int, stream=None) -> None:
         _check(lib().pa_result_copy_in(self._h, sum_src_ptr or None, min_src_ptr or None, _stream(stream)))
 
@@ -721,6 +735,56 @@ def align_fastq_file(index: Index, path: str, params: Params, read_index_base: i
         return None
     _check(st)
     return int(n.value)
+
+
+class IdSet:
+    """Read-id hashes of a FASTQ byte range (pa_align_fastq_range), for
+    idsets_disjoint; freed by close()."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pa_idset_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+
+def align_fastq_range(index: Index, path: str, offset: int, length: int, params: Params, read_index_base: int,
+                      result: Result, threads: Optional[int] = None, window_bytes: int = 0, stream=None,
+                      want_ids: bool = True):
+    """pa_align_fastq_range: the records of bytes [offset, offset + length) of a
+    plain FASTQ file (cut on record boundaries) parsed and aligned on the
+    index's device; returns (records, IdSet or None), or None when the range
+    is outside the device-parsed subset of the grammar (the caller then takes
+    the exact path for the whole file)."""
+    n = U64(0)
+    h = P()
+    if window_bytes <= 0:
+        env = os.environ.get("PA_STREAM_WINDOW")
+        window_bytes = int(env) if env and env.isdigit() else 0
+    st = lib().pa_align_fastq_range(index.handle, os.fsencode(path), int(offset), int(length), ctypes.byref(params),
+                                    int(read_index_base), result.handle, int(threads or ingest_threads()),
+                                    int(window_bytes), _stream(stream), ctypes.byref(n),
+                                    ctypes.byref(h) if want_ids else None)
+    if st == PA_ENOTCANON:
+        return None
+    _check(st)
+    return int(n.value), (IdSet(h) if want_ids else None)
+
+
+def idsets_disjoint(sets: Sequence[IdSet], device: int = 0) -> bool:
+    """pa_idsets_disjoint: no read-id hash in two of the sets."""
+    arr = (P * max(len(sets), 1))(*[s.handle for s in sets])
+    d = I32(0)
+    _check(lib().pa_idsets_disjoint(arr, len(sets), int(device), ctypes.byref(d)))
+    return bool(d.value)
 
 
 NO_ORDER = 0xFFFFFFFFFFFFFFFF  # pa_index_dumpref: a description no k-mer holds

@@ -30,6 +30,8 @@
  *   pa_align_fastq_file      FASTAQFile + align_reads_from_container as one
  *                            device-parsed stream                          src/data_file.py:134-158,
  *                                                                          src/kmer.py:600-620
+ *   pa_align_fastq_range     the same over a byte range of the file, one per device:
+ *   pa_idsets_disjoint       the dumpalign job read-sharded over N GPUs     src/main.py:289-310
  *   pa_fastq_prefetch_start  the same with the file moved to the device in the
  *   pa_align_fastq_prefetched  background (overlaps the index build)       src/main.py:286-310
  *   pa_counters_reduce       the multi-GPU sum/min of PseudoAlignment counters
@@ -173,12 +175,14 @@ pa_status pa_index_prepare(pa_index *idx, void *stream);
 /* The same for a job of about expected_reads reads (PA_READS_UNKNOWN: as
  * pa_index_prepare).  The one-substitution neighbour bits (DESIGN.md section
  * 3) cost time per genome base and save time per read: below the break-even
- * (PA_NB_READS_PER_BASE reads per genome base) they are left out, and made by
+ * (PA_NB_READS_PER_KBASE reads per 1000 genome bases) they are left out, and made by
  * the align that brings the reads aligned with this index past that point --
  * or by a later call of this function whose expected_reads (the reads still to
  * come) passes it.  Results never depend on them.  Returns when done. */
 #define PA_READS_UNKNOWN UINT64_MAX
-#define PA_NB_READS_PER_BASE 4
+/* the measured break-even (bench.py neighbour_bits_breakeven: C2 3.26, C4 3.53
+ * reads per genome base on MI355X, round 6) */
+#define PA_NB_READS_PER_KBASE 3500
 pa_status pa_index_prepare_ex(pa_index *idx, uint64_t expected_reads, void *stream);
 void pa_index_free(pa_index *idx);
 pa_status pa_index_get_info(const pa_index *idx, pa_index_info *out);
@@ -259,6 +263,10 @@ pa_status pa_result_device_view(pa_result *res, uint64_t **sum_block, uint64_t *
  * NULL.  Values fit int64: counts < 2^63, first keys < 2^63 (PA_NO_FIRST_KEY). */
 pa_status pa_result_copy_out(const pa_result *res, void *sum_dst, void *min_dst, void *stream);
 pa_status pa_result_copy_in(pa_result *res, const void *sum_src, const void *min_src, void *stream);
+/* Overwrite the two blocks from HOST arrays ([6 + 2G] sums, [G] first keys, as
+ * pa_result_fetch's order: stats, unique, ambiguous); returns when copied.
+ * The host-side reduction of read shards (dumpalign over N GPUs). */
+pa_status pa_result_load(pa_result *res, const uint64_t *sum_block, const uint64_t *min_block);
 void pa_result_free(pa_result *res);
 
 /* ---- alignment ---------------------------------------------------------------- */
@@ -292,6 +300,27 @@ pa_status pa_align_batch(const pa_index *idx, const uint8_t *seq, const uint8_t 
 pa_status pa_align_fastq_file(const pa_index *idx, const char *path, const pa_params *params,
                               uint64_t read_index_base, pa_result *acc, int32_t threads, uint64_t window_bytes,
                               void *stream, uint64_t *n_reads);
+
+/* pa_align_fastq_file over the byte range [offset, offset + length) of a plain
+ * (not gzip) FASTQ file, read as if it were the whole file: the shard of one
+ * device in a read-sharded job (the dumpalign CLI with PA_GPUS = N).  The
+ * range must start at a record's '@' and end after a record's last line feed
+ * (or at the end of the file).  read_index_base orders the shards' records:
+ * any base at least as large as the previous shard's base + its record count
+ * keeps the Summary key order of one pass over the file (e.g. the range's
+ * byte offset: every record takes more than one byte).  ids (nullable): the
+ * range's read-id hashes, for pa_idsets_disjoint -- the duplicate-id check
+ * (DuplicateRecordError, src/records.py:290-302) across ranges; a duplicate
+ * within the range is PA_ENOTCANON as in pa_align_fastq_file. */
+typedef struct pa_idset pa_idset;
+pa_status pa_align_fastq_range(const pa_index *idx, const char *path, uint64_t offset, uint64_t length,
+                               const pa_params *params, uint64_t read_index_base, pa_result *acc, int32_t threads,
+                               uint64_t window_bytes, void *stream, uint64_t *n_reads, pa_idset **ids);
+/* *disjoint = 1 when no read-id hash is in two of the sets (else 0: a duplicate
+ * id across shards, or a 2^-64 hash collision -- parse the file the exact way,
+ * which decides and raises the reference's error).  Checked on `device`. */
+pa_status pa_idsets_disjoint(const pa_idset *const *sets, uint32_t n_sets, int32_t device, int32_t *disjoint);
+void pa_idset_free(pa_idset *ids);
 
 /* The same as one device-resident step: pa_fastq_prefetch_start begins moving
  * the (plain, not gzip) FASTQ file into device memory on a background thread

@@ -125,6 +125,19 @@ def main():
     rs = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
                         env=dict(os.environ, PA_CLI_TIMING="1", PA_FAST_EXIT="0"))
     stages["normal_exit"] = {"wall_s": time.perf_counter() - t, "stderr": rs.stderr.strip().splitlines()[-3:]}
+    # the same command read-sharded over two devices (PA_GPUS=2, pa_shard.py;
+    # on a one-GPU box both replicas on device 0: PA_GPUS_SHARE=1)
+    shard_env = dict(os.environ, PA_GPUS="2", PA_CLI_TIMING="1")
+    if N.device_count() < 2:
+        shard_env["PA_GPUS_SHARE"] = "1"
+    time.sleep(3)
+    t = time.perf_counter()
+    rsh = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=shard_env)
+    sharded = {"gpus": 2, "shared_device": shard_env.get("PA_GPUS_SHARE") == "1",
+               "wall_s": time.perf_counter() - t, "rc": rsh.returncode,
+               "stdout_equals_api": rsh.stdout == summary + "\n",
+               "sharded_path_taken": "reads aligned (sharded)" in rsh.stderr,
+               "stages": [x for x in rsh.stderr.strip().splitlines() if x.startswith("[pa_cli]")][-8:]}
     t = time.perf_counter()
     subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); import main" % PKG])
     stages["python_and_imports_s"] = time.perf_counter() - t
@@ -183,7 +196,7 @@ def main():
         if not args.keep:
             os.remove(fqz)
     out = {"workload": f"dumpalign C2: 50 x 2 Mbp FASTA, {args.reads} x 150 bp FASTQ, k=31",
-           "fq_gz": gz, "fq_plain_gz": pgz,
+           "fq_gz": gz, "fq_plain_gz": pgz, "sharded": sharded,
            "fastq_bytes": os.path.getsize(fq), "cli_wall_s": cli_s, "cli_wall_runs_s": walls, "cli_reads_per_s": args.reads / cli_s,
            "cli_rc": r.returncode, "cli_stdout_equals_api": r.stdout == summary + "\n",
            "device_parse_path_taken": streamed, "host_path_summary_equal": host_equal,
