@@ -805,6 +805,7 @@ struct KernelTimer {
 // reads then go to the wave kernel).
 // nw: key words (2: 31 < k <= 63, 3: 63 < k <= 95 -- the 150-bp shape, no
 // reverse-strand path: reads without a seed go to the wave kernel).
+constexpr uint64_t kRcnbMinReads = 32768;  // seedless reads in a pass that make the reverse-complement bits worth it
 pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr, bool long_reads = false,
                       int nw = 1) {
     const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
@@ -840,12 +841,28 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
     }
     if (a.queue_na) {  // the reads without a seed in the index (count on the device)
         AlignArgs b = a;
+        // the reverse-complement neighbour bits, left out by the build
+        // (build_nb), are made by the first pass that queues enough seedless
+        // reads; passes that queue too few look twice, then stop looking (the
+        // reverse-strand walk runs without them, exactly, only slower)
+        if (prof && prof->rcnb_pending && a.queue_na_keys) {
+            unsigned long long c = 0;
+            PA_HIP(hipMemcpyAsync(&c, a.queue_na_count, 8, hipMemcpyDeviceToHost, st));
+            PA_HIP(hipStreamSynchronize(st));
+            if (c >= std::max<uint64_t>(kRcnbMinReads, a.n / 64)) {
+                PA_TRY(pa::index_build_rcnb(prof, st));
+                const char *e = std::getenv("PA_NA_RCNB");
+                if (!(e && e[0] == '0')) b.tile_rcnb = prof->tile_rcnb;
+            } else if (++prof->rcnb_checks >= 2) {
+                prof->rcnb_pending = 0;
+            }
+        }
         if (a.queue_na_keys) {  // reverse-complement seeds, the reverse-strand walk; the rest on to k_align_lane_na
             {
                 KernelTimer kt(prof, st, PA_PROF_RC_SEEDS);
                 hipLaunchKernelGGL(k_rc_seeds, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(
                                                         (a.n + kBlock * 4 - 1) / (kBlock * 4), 8192))),
-                                   dim3(kBlock), 0, st, a);
+                                   dim3(kBlock), 0, st, b);
                 PA_HIP(hipGetLastError());
             }
             auto rc = win_q ? (mg ? k_align_lane_rc<true, true, true> : k_align_lane_rc<true, true, false>)
@@ -856,7 +873,7 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
             const unsigned rgrid = (unsigned)std::max<uint64_t>(
                 1, std::min<uint64_t>(want, (uint64_t)std::max(1, rc_cu) * (uint64_t)cus));
             KernelTimer kt(prof, st, PA_PROF_LANE_RC);
-            hipLaunchKernelGGL(rc, dim3(rgrid), dim3(kBlock), 0, st, a);
+            hipLaunchKernelGGL(rc, dim3(rgrid), dim3(kBlock), 0, st, b);
             PA_HIP(hipGetLastError());
             b.queue_na = a.queue_na2;
             b.queue_na_count = a.queue_na2_count;

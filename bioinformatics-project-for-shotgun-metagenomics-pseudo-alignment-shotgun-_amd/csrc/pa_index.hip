@@ -874,15 +874,37 @@ __global__ void k_tpos_concat(Slot<NW> *table, uint64_t cap, uint32_t G, const u
 // < kTileRepDist apart), which the lane kernel (pa_lane.h) tests instead of
 // deduplicating.  One block per 256 positions, keys staged in LDS.
 constexpr int kTileRepDist = 255;  // (>= the lane kernels' longest span of windows: 256 windows, pa_lane.h)
+// One block per 256 windows and the 255 after them, staged in LDS; round 6:
+// instead of comparing every window with each of the next 255 (~500 LDS reads
+// per window, VALU-bound: 47 ms for C4's 1 Gbp), the span's keys go into an
+// LDS hash of their distinct values, each holding the chain of the positions
+// where it occurs; a window then walks only its own key's chain -- one entry
+// unless the k-mer repeats.
 template <int NW>  // (1: k <= 31, 2: k <= 63, 3: k <= 95 -- the key words compared)
 __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ pk, uint32_t *tile_cls, uint64_t n,
                                                   int k) {
-    __shared__ uint64_t keys[NW][256 + kTileRepDist];
-    __shared__ uint32_t valid[256 + kTileRepDist];
-    const int sh = 64 - 2 * k, hb = 2 * k - 64;
+    constexpr int SPAN = 256 + kTileRepDist, HS = 1024;  // (the hash at most half full)
+    constexpr uint32_t NIL = 0xFFFFFFFFu;
+    __shared__ uint64_t keys[NW][SPAN];
+    __shared__ uint32_t valid[SPAN], nxt[SPAN];
+    __shared__ uint32_t rep_of[HS], chain[HS];  // a slot's representative position / its latest position
+    const int sh = 64 - 2 * k;
+    auto same = [&](int a, int b) {
+        bool eq = true;
+#pragma unroll
+        for (int j = 0; j < NW; j++) eq = eq && keys[j][a] == keys[j][b];
+        return eq;
+    };
+    auto slot_of = [&](int i) {
+        uint64_t h = keys[0][i];
+#pragma unroll
+        for (int j = 1; j < NW; j++) h = h * 0x9E3779B97F4A7C15ull ^ keys[j][i];
+        return (uint32_t)(fmix64(h) >> 54);  // HS = 2^10
+    };
     for (uint64_t b = (uint64_t)blockIdx.x * 256; b < n; b += (uint64_t)gridDim.x * 256) {
         __syncthreads();
-        for (int i = threadIdx.x; i < 256 + kTileRepDist; i += 256) {
+        for (int i = threadIdx.x; i < HS; i += 256) rep_of[i] = NIL, chain[i] = NIL;
+        for (int i = threadIdx.x; i < SPAN; i += 256) {
             const uint64_t t = b + i;
             const bool ok = t < n && tile_cls[t] != NONE;
             valid[i] = ok;
@@ -895,18 +917,31 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
             }
         }
         __syncthreads();
+        // every indexed window of the span into the hash: its key's slot (a
+        // slot's representative is the first position to claim it), then
+        // pushed on the slot's chain
+        for (int i = threadIdx.x; i < SPAN; i += 256) {
+            if (!valid[i]) continue;
+            uint32_t s = slot_of(i);
+            for (;;) {
+                uint32_t r = rep_of[s];
+                if (r == NIL) {
+                    r = atomicCAS(&rep_of[s], NIL, (uint32_t)i);
+                    if (r == NIL) break;
+                }
+                if (same((int)r, i)) break;
+                s = (s + 1) & (HS - 1);
+            }
+            nxt[i] = atomicExch(&chain[s], (uint32_t)i);
+        }
+        __syncthreads();
         const uint64_t t = b + threadIdx.x;
         if (t < n && valid[threadIdx.x]) {
-            uint64_t me[NW];
-#pragma unroll
-            for (int j = 0; j < NW; j++) me[j] = keys[j][threadIdx.x];
+            const int me = threadIdx.x;
+            uint32_t s = slot_of(me);
+            while (!same((int)rep_of[s], me)) s = (s + 1) & (HS - 1);
             bool rep = false;
-            for (int d = 1; d <= kTileRepDist; d++) {
-                bool eq = valid[threadIdx.x + d] != 0;
-#pragma unroll
-                for (int j = 0; j < NW; j++) eq = eq && keys[j][threadIdx.x + d] == me[j];
-                rep |= eq;
-            }
+            for (uint32_t q = chain[s]; q != NIL && !rep; q = nxt[q]) rep = (int)q > me && (int)q <= me + kTileRepDist;
             if (rep) tile_cls[t] |= PA_TILE_REP;
         }
     }
@@ -1685,6 +1720,71 @@ pa_status build_nb2(pa_index *idx, hipStream_t st);
 
 pa_status build_nb3(pa_index *idx, hipStream_t st);
 
+// The reverse-complement neighbour bits (tile_rcnb, 12 B per base) when they
+// leave a quarter of the free memory; bb: the build-time Bloom filter of the
+// keys (nullable: every neighbour probed).
+pa_status build_rcnb(pa_index *idx, hipStream_t st, const uint64_t *bb, uint32_t bb_lg) {
+    const uint64_t n = idx->tile_n;
+    const int k = (int)idx->k;
+    const uint32_t G = idx->n_genomes;
+    const Slot<1> *table = (const Slot<1> *)idx->table;
+    idx->rcnb_pending = 0;
+    size_t fr_b = 0, tr_b = 0;
+    if (!(pa::dev_mem_info(&fr_b, &tr_b) == hipSuccess && n * 12 <= fr_b / 4 * 3 &&
+          pa::dev_malloc(&idx->tile_rcnb, n * 12 + 64) == hipSuccess)) {
+        (void)hipGetLastError();
+        idx->tile_rcnb = nullptr;
+        return PA_OK;  // (no room: the seedless reads are walked without them)
+    }
+    PA_HIP(hipMemsetAsync(idx->tile_rcnb, 0, n * 12 + 64, st));
+    for (int pass = 0; pass < 2; pass++)
+        if (pass == 0 && kNbFirstOrder)
+            hipLaunchKernelGGL(k_nb_first, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
+                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, (void *)idx->tile_rcnb, 0,
+                               idx->class_genomes, idx->goff, idx->tpos_local, bb, bb_lg, 1);
+        else if (pass == 1)
+            hipLaunchKernelGGL(k_nb_copy, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
+                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, (void *)idx->tile_rcnb, 0,
+                               idx->class_genomes, idx->goff, idx->tpos_local);
+        else
+            hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
+                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, (void *)idx->tile_rcnb, 0,
+                               idx->class_genomes, idx->goff, idx->tpos_local, pass, bb, bb_lg, 1);
+    PA_HIP(hipGetLastError());
+    idx->device_bytes += n * 12;
+    phase_mark("nb: reverse complements");
+    return PA_OK;
+}
+
+// The neighbour-bit build's Bloom filter of the keys (~16 bits per key in HBM,
+// the caller frees it): most of a window's 3k neighbours are absent and share
+// its Bloom line (minimizer-chosen), so a probe costs an L2 hit instead of a
+// table line.  nullptr when it does not fit (or PA_NB_BLOOM=0).
+pa_status make_nb_bloom(pa_index *idx, hipStream_t st, uint64_t **out, uint32_t *out_lg) {
+    *out = nullptr;
+    *out_lg = 6;
+    uint64_t *bb = nullptr;
+    uint32_t bb_lg = 6;
+    const char *nbb = std::getenv("PA_NB_BLOOM");
+    if ((nbb && nbb[0] == '0') || idx->n_kmers == 0) return PA_OK;
+    while (bb_lg < 33 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;  // (bloom_block: lg <= 33)
+    size_t fb = 0, tb = 0;
+    if (pa::dev_mem_info(&fb, &tb) != hipSuccess) fb = 0;
+    while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
+    if ((1ull << bb_lg) * 64 < idx->n_kmers * 8 || pa::dev_malloc(&bb, (1ull << bb_lg) * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        return PA_OK;
+    }
+    PA_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
+    phase_mark(bb_lg >= 30 ? "nb: Bloom alloc (lg >= 30)" : "nb: Bloom alloc (lg < 30)");
+    hipLaunchKernelGGL(k_bloom_build<true>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
+                       dim3(kBlock), 0, st, (const Slot<1> *)idx->table, idx->cap, bb, bb_lg, (int)idx->k);
+    PA_HIP(hipGetLastError());
+    *out = bb;
+    *out_lg = bb_lg;
+    return PA_OK;
+}
+
 pa_status build_nb(pa_index *idx, hipStream_t st) {
     if (idx->nw == 2) return build_nb2(idx, st);
     if (idx->nw == 3) return build_nb3(idx, st);
@@ -1714,21 +1814,7 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
             // PA_NB_BLOOM=0 turns it off (A/B)
             uint64_t *bb = nullptr;
             uint32_t bb_lg = 6;
-            const char *nbb = std::getenv("PA_NB_BLOOM");
-            if (!(nbb && nbb[0] == '0') && idx->n_kmers > 0) {
-                while (bb_lg < 33 && (1ull << bb_lg) * 4 < idx->n_kmers) bb_lg++;  // (bloom_block: lg <= 33)
-                size_t fb = 0, tb = 0;
-                if (pa::dev_mem_info(&fb, &tb) != hipSuccess) fb = 0;
-                while (bb_lg > 6 && (1ull << bb_lg) * 8 > fb / 4) bb_lg--;
-                if ((1ull << bb_lg) * 64 >= idx->n_kmers * 8 && pa::dev_malloc(&bb, (1ull << bb_lg) * 8) == hipSuccess) {
-                    B_HIP(hipMemsetAsync(bb, 0, (1ull << bb_lg) * 8, st));
-                    phase_mark(bb_lg >= 30 ? "nb: Bloom alloc (lg >= 30)" : "nb: Bloom alloc (lg < 30)");
-                    hipLaunchKernelGGL(k_bloom_build<true>, dim3(grid_for(idx->cap) > 65536 ? 65536 : grid_for(idx->cap)),
-                                       dim3(kBlock), 0, st, (const Slot<1> *)table, idx->cap, bb, bb_lg, k);
-                } else {
-                    bb = nullptr;
-                }
-            }
+            PA_TRY(make_nb_bloom(idx, st, &bb, &bb_lg));
             phase_mark("nb: build Bloom");
             for (int pass = 0; pass < 2; pass++) {
                 if (pass == 0 && kNbFirstOrder)
@@ -1747,31 +1833,18 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                                        pass, bb, bb_lg, 0);
                 phase_mark(pass == 0 ? "nb: first occurrences" : "nb: copies");
             }
-            // the reverse-complement neighbour bits (tile_rcnb, 12 B per base)
-            // when they leave a quarter of the free memory; PA_NO_RCNB=1: none
-            const char *no_rcnb = std::getenv("PA_NO_RCNB");
-            size_t fr_b = 0, tr_b = 0;
-            if (k <= 31 && !(no_rcnb && no_rcnb[0] == '1') && pa::dev_mem_info(&fr_b, &tr_b) == hipSuccess &&
-                n * 12 <= fr_b / 4 * 3 && pa::dev_malloc(&idx->tile_rcnb, n * 12 + 64) == hipSuccess) {
-                B_HIP(hipMemsetAsync(idx->tile_rcnb, 0, n * 12 + 64, st));
-                for (int pass = 0; pass < 2; pass++)
-                    if (pass == 0 && kNbFirstOrder)
-                        hipLaunchKernelGGL(k_nb_first, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock),
-                                           0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,
-                                           G, (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff,
-                                           idx->tpos_local, bb, bb_lg, 1);
-                    else if (pass == 1)
-                        hipLaunchKernelGGL(k_nb_copy, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock),
-                                           0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,
-                                           G, (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff,
-                                           idx->tpos_local);
-                    else
-                        hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock),
-                                           0, st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home,
-                                           G, (void *)idx->tile_rcnb, 0, idx->class_genomes, idx->goff,
-                                           idx->tpos_local, pass, bb, bb_lg, 1);
-                idx->device_bytes += n * 12;
-                phase_mark("nb: reverse complements");
+            // the reverse-complement neighbour bits (tile_rcnb, 12 B per base):
+            // only reads with no forward seed use them (k_align_lane_rc), so by
+            // default they are left for the first align pass that queues enough
+            // such reads (index_rcnb_wanted: C4's forward reads never do, and
+            // its serving index skips their 0.35 s); PA_RCNB_EAGER=1 makes them
+            // now, PA_NO_RCNB=1 never
+            const char *no_rcnb = std::getenv("PA_NO_RCNB"), *eager = std::getenv("PA_RCNB_EAGER");
+            if (k <= 31 && !(no_rcnb && no_rcnb[0] == '1')) {
+                if (eager && eager[0] == '1')
+                    PA_TRY(build_rcnb(idx, st, bb, bb_lg));
+                else
+                    idx->rcnb_pending = 1;
             }
             if (bb) {
                 B_HIP(hipStreamSynchronize(st));
@@ -2132,6 +2205,22 @@ void index_release(pa_index *idx) {
     }
     idx->kev.clear();
     idx->table = nullptr;
+}
+
+pa_status index_build_rcnb(pa_index *idx, hipStream_t st) {
+    if (!idx->rcnb_pending) return PA_OK;
+    std::unique_ptr<PhaseTimer> own;
+    if (!t_phase) own.reset(new PhaseTimer(st));
+    PhaseScope ps(t_phase ? t_phase : own.get());
+    uint64_t *bb = nullptr;
+    uint32_t bb_lg = 6;
+    PA_TRY(make_nb_bloom(idx, st, &bb, &bb_lg));
+    const pa_status rc = build_rcnb(idx, st, bb, bb_lg);
+    if (bb) {
+        PA_HIP(hipStreamSynchronize(st));
+        pa::dev_free(bb);
+    }
+    return rc;
 }
 
 pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st) {

@@ -107,6 +107,8 @@ struct pa_index {
     void *tile_nb = nullptr;           // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional:
     int nb_spec = 0;                   //   1: 64-bit words, present | specific << 32; 0: 32-bit words, present
     uint32_t *tile_rcnb = nullptr;     // [3 tile_n] the same for the neighbours' reverse complements (present), optional
+    int rcnb_pending = 0;              //   1: left for the first pass that queues enough seedless reads (pa_align.hip)
+    int rcnb_checks = 0;               //   passes that looked and found too few
     uint32_t *tile_nbbig = nullptr;    // [3 tile_n] neighbour present with a set > tile_nbbig_mg (pa_align, cached)
     int64_t tile_nbbig_mg = -1;
     uint4 *tile_nbm = nullptr;         // [3 tile_n] {present, specific, set > tile_nbm_mg, 0}: tile_nb and tile_nbbig
@@ -191,6 +193,7 @@ inline bool nb_repaid(uint64_t reads, uint64_t bases) { return reads >= (bases *
 // still to come; ~0: unknown) passes the break-even (pa_index_prepare[_ex]).
 pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint = ~0ull, bool complete = false);
 pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st);
+pa_status index_build_rcnb(pa_index *idx, hipStream_t st);  // the pending reverse-complement neighbour bits, now
 pa_status index_lookup(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, int64_t *cls_out,
                        uint32_t *size_out, hipStream_t st);
 pa_status index_positions(const pa_index *idx, const char *kmers, uint64_t n, uint32_t kmer_len, uint32_t flags,

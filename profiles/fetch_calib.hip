@@ -29,6 +29,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
+#include <algorithm>
 
 #define CK(x)                                                                                   \
     do {                                                                                        \
@@ -146,7 +148,44 @@ static void timed(const char *name, uint64_t lines, uint64_t bytes, F launch) {
     first_row = false;
 }
 
-int main() {
+// --footprint: random 16-B loads over buffers of 16 GiB up to ~250 GB (the
+// C4 / C5 indexes' footprints: ~100 / ~250 GB touched by the lane kernel), to
+// see whether the random-line ceiling falls as a buffer outgrows the TLB reach.
+static int footprint_sweep() {
+    size_t fr = 0, tot = 0;
+    CK(hipMemGetInfo(&fr, &tot));
+    uint64_t bytes = std::min<uint64_t>(250ull * 1000 * 1000 * 1000, (uint64_t)fr - (12ull << 30));
+    bytes &= ~((1ull << 30) - 1);
+    uint4 *buf = nullptr;
+    uint32_t *out = nullptr;
+    CK(hipMalloc(&buf, bytes));
+    CK(hipMalloc(&out, 4u << 20));
+    CK(hipMemset(buf, 0x5A, bytes));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipDeviceSynchronize());
+    const unsigned blocks = 16384;
+    const uint64_t lanes = (uint64_t)blocks * 256;
+    constexpr int R = 8;
+    const uint64_t L = lanes * R;
+    std::printf("{\"buffer_bytes\": %llu, \"footprint_sweep\": [\n", (unsigned long long)bytes);
+    for (uint64_t gb : {16ull, 32ull, 64ull, 100ull, 128ull, 192ull, 250ull}) {
+        const uint64_t nb = std::min<uint64_t>(gb * 1000 * 1000 * 1000, bytes);
+        if (gb > 16 && nb < gb * 1000 * 1000 * 1000) break;
+        char name[64];
+        std::snprintf(name, sizeof name, "k_rand<16>@%lluGB", (unsigned long long)gb);
+        timed(name, L, L * 64, [&] { hipLaunchKernelGGL((k_rand<16, false, R>), dim3(blocks), dim3(256), 0, 0, buf, nb / 64, 11ull + gb, out); });
+        std::snprintf(name, sizeof name, "k_rand<16,nt>@%lluGB", (unsigned long long)gb);
+        timed(name, L, L * 64, [&] { hipLaunchKernelGGL((k_rand<16, true, R>), dim3(blocks), dim3(256), 0, 0, buf, nb / 64, 12ull + gb, out); });
+    }
+    std::printf("]}\n");
+    CK(hipFree(buf));
+    CK(hipFree(out));
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc > 1 && std::string(argv[1]) == "--footprint") return footprint_sweep();
     const uint64_t bytes = 16ull << 30, n_lines = bytes / 64;
     uint4 *buf = nullptr;
     uint32_t *out = nullptr;
