@@ -1101,9 +1101,14 @@ __global__ __launch_bounds__(256) void k_reads_qstats(const uint8_t *__restrict_
         qm = min(qm, (uint32_t)__shfl_down(qm, o));
         lm = min(lm, (uint32_t)__shfl_down(lm, o));
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin(&out[0], qm);
-        atomicMin(&out[1], lm);
+    // one atomic pair per block (same-address atomics serialise: a pair per
+    // wave of 4096 blocks cost more than the loads)
+    __shared__ uint32_t red[2][4];
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = qm, red[1][threadIdx.x >> 6] = lm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicMin(&out[0], min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3])));
+        atomicMin(&out[1], min(min(red[1][0], red[1][1]), min(red[1][2], red[1][3])));
     }
 }
 
@@ -1118,7 +1123,8 @@ pa_status reads_measure(pa_reads *r, hipStream_t st) {
     PA_HIP(pa::dev_malloc(&d, 8));
     hipError_t e = hipMemcpyAsync(d, h, 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_reads_qstats, dim3(4096), dim3(256), 0, st, r->qual, r->off, r->n, d);
+        const unsigned qgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(2048, (r->n_bases >> 14) + 1));
+        hipLaunchKernelGGL(k_reads_qstats, dim3(qgrid), dim3(256), 0, st, r->qual, r->off, r->n, d);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
