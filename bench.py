@@ -596,81 +596,75 @@ def main():
     N.Index([np.frombuffer(b"ACGT" * 64, dtype=np.uint8)], cfg["k"], device=local, stream=stream).close()
     torch.cuda.synchronize(dev)
     first_read, npg = rank_reads(cfg, rank, world)
-    t_index0 = t0 = time.perf_counter()
-    # the align-side view is made below by prepare(expected_reads=...), sized
-    # for this rank's job, as the product does (the CLI passes its FASTQ's
-    # record count, PseudoAlignment its batch's)
-    index = N.Index(genomes, cfg["k"], device=local, stream=stream, defer_tiles=True)
-    torch.cuda.synchronize(dev)
-    build_s = time.perf_counter() - t0
-    build_bases = sum(len(g) for g in genomes)
-    extsim = None
+    all_genomes = genomes
     kept_path = None
+    kept_from_file = None
     if args.kept_file:  # traffic child: the parent's EXTSIM outcome
         with open(args.kept_file) as f:
-            kept_idx = json.load(f)
-        genomes = [genomes[i] for i in kept_idx]
-        index.reduce(kept_idx, stream)
+            kept_from_file = json.load(f)
+
+    def build_index(expected_reads):
+        """genomes in host memory -> an align-ready index: build (the view
+        deferred), EXTSIM + the rebuild of the kept genomes (C5), then the
+        align-side view -- for a job of `expected_reads` reads
+        (pa_index_prepare_ex: the neighbour bits only past their break-even),
+        or, with None, the full view (the serving index, pa_index_prepare).
+        Returns (index, kept genomes, timings)."""
+        nonlocal kept_path
+        t_all = t0 = time.perf_counter()
+        ix = N.Index(all_genomes, cfg["k"], device=local, stream=stream, defer_tiles=True)
         torch.cuda.synchronize(dev)
-    elif cfg.get("extsim") is not None:
-        # EXTSIM (src/kmer.py:152-263): GPU statistics + the greedy pass; a
-        # genome dropped -> the index of the kept genomes
-        import kmer
-        t0 = time.perf_counter()
-        idents = [f"genome_{i}" for i in range(len(genomes))]
-        keep, sim_info = kmer.extsim_filter(index, idents, [len(g) for g in genomes], cfg["extsim"])
-        stats_s = time.perf_counter() - t0
-        kept_idx = [j for j, i in enumerate(idents) if i in keep]
-        t1 = time.perf_counter()
-        if len(keep) != len(idents):  # the kept genomes' index, from their codes on the device
-            genomes = [genomes[j] for j in kept_idx]
-            index.reduce(kept_idx, stream)
+        tm = {"first_build_s": time.perf_counter() - t0, "bases_built": sum(len(g) for g in all_genomes),
+              "extsim": None}
+        kept = all_genomes
+        if kept_from_file is not None:
+            kept = [all_genomes[i] for i in kept_from_file]
+            ix.reduce(kept_from_file, stream)
             torch.cuda.synchronize(dev)
-            build_bases += sum(len(g) for g in genomes)
-        rebuild_s = time.perf_counter() - t1
-        import tempfile
-        fd, kept_path = tempfile.mkstemp(prefix="pa_kept_", suffix=".json", dir="/tmp")
-        with os.fdopen(fd, "w") as f:
-            json.dump(kept_idx, f)
-        scores = [v["similarity_score"] for v in sim_info.values() if v["kept"] == "no"]
-        extsim = {"threshold": cfg["extsim"], "genomes_in": len(idents), "genomes_kept": len(keep),
-                  "stats_and_greedy_s": stats_s, "rebuild_kept_s": rebuild_s, "total_s": time.perf_counter() - t0,
-                  "min_dropped_score": min(scores) if scores else None,
-                  "max_kept_pair_score_below": cfg["extsim"]}
-        log(f"[rank {rank}] EXTSIM: kept {len(keep)} of {len(idents)} in {extsim['total_s']:.1f}s")
-    t0 = time.perf_counter()
-    # the job's index: the align-side view this rank's npg reads repay (the
-    # neighbour bits only past PA_NB_READS_PER_KBASE / 1000 reads per genome base:
-    # pa_index_prepare_ex)
-    index.prepare(stream, expected_reads=npg)
-    prepare_s = time.perf_counter() - t0
-    index_total_s = time.perf_counter() - t_index0
-    job_index_bytes = int(index.info().device_bytes)
-    t0 = time.perf_counter()
-    reads = N.Reads.synthesize(index, npg, cfg["read_len"], first_read=first_read, seed=2, sub_rate=cfg["read_err"],
+        elif cfg.get("extsim") is not None:
+            # EXTSIM (src/kmer.py:152-263): GPU statistics + the greedy pass; a
+            # genome dropped -> the index of the kept genomes
+            import kmer
+            t0 = time.perf_counter()
+            idents = [f"genome_{i}" for i in range(len(all_genomes))]
+            keep, sim_info = kmer.extsim_filter(ix, idents, [len(g) for g in all_genomes], cfg["extsim"])
+            stats_s = time.perf_counter() - t0
+            kept_idx = [j for j, i in enumerate(idents) if i in keep]
+            t1 = time.perf_counter()
+            if len(keep) != len(idents):  # the kept genomes' index, from their codes on the device
+                kept = [all_genomes[j] for j in kept_idx]
+                ix.reduce(kept_idx, stream)
+                torch.cuda.synchronize(dev)
+                tm["bases_built"] += sum(len(g) for g in kept)
+            rebuild_s = time.perf_counter() - t1
+            if kept_path is None:
+                import tempfile
+                fd, kept_path = tempfile.mkstemp(prefix="pa_kept_", suffix=".json", dir="/tmp")
+                with os.fdopen(fd, "w") as f:
+                    json.dump(kept_idx, f)
+            scores = [v["similarity_score"] for v in sim_info.values() if v["kept"] == "no"]
+            tm["extsim"] = {"threshold": cfg["extsim"], "genomes_in": len(idents), "genomes_kept": len(keep),
+                            "stats_and_greedy_s": stats_s, "rebuild_kept_s": rebuild_s,
+                            "total_s": time.perf_counter() - t0, "min_dropped_score": min(scores) if scores else None,
+                            "max_kept_pair_score_below": cfg["extsim"]}
+            log(f"[rank {rank}] EXTSIM: kept {len(keep)} of {len(idents)} in {tm['extsim']['total_s']:.1f}s")
+        t0 = time.perf_counter()
+        ix.prepare(stream, expected_reads=expected_reads)
+        torch.cuda.synchronize(dev)
+        tm["prepare_s"] = time.perf_counter() - t0
+        tm["build_s"] = time.perf_counter() - t_all
+        return ix, kept, tm
+
+    def make_reads(ix):
+        t0 = time.perf_counter()
+        r = N.Reads.synthesize(ix, npg, cfg["read_len"], first_read=first_read, seed=2, sub_rate=cfg["read_err"],
                                stream=stream, rc_rate=cfg.get("rc_rate", 0.0),
                                foreign_rate=cfg.get("foreign_rate", 0.0))
-    torch.cuda.synchronize(dev)
-    reads_make_s = time.perf_counter() - t0
-    result = N.Result(index)
+        torch.cuda.synchronize(dev)
+        return r, time.perf_counter() - t0
+
     pk = cfg["params"]
     prm = N.Params.make(pk.get("m", 1), pk.get("p", 1), pk.get("mrq"), pk.get("mkq"), pk.get("mg"))
-    # the filters a pass really applies: thresholds at or below the batch's
-    # smallest quality byte filter nothing (quirk 5) and are dropped
-    eff, q_min = reads.effective(prm, stream)
-    applied = {}
-    if eff.flags & N.HAS_MRQ:
-        applied["mrq"] = pk.get("mrq")
-    if eff.flags & N.HAS_MKQ:
-        applied["mkq"] = pk.get("mkq")
-    if eff.flags & N.HAS_MG:
-        applied["mg"] = pk.get("mg")
-    elided = [n for n, f in (("mrq", N.HAS_MRQ), ("mkq", N.HAS_MKQ)) if (prm.flags & f) and not (eff.flags & f)]
-    quality_applied = bool(eff.flags & (N.HAS_MRQ | N.HAS_MKQ))
-    log(f"[rank {rank}] genomes {gen_s:.1f}s, index {index_total_s:.2f}s (first build {build_s:.2f}s, "
-        f"align-side view {prepare_s:.2f}s): {index.info().n_kmers} k-mers, "
-        f"{index.info().n_multi_classes} multi-genome sets, table {index.info().table_bytes / 2**30:.2f} GiB; {npg} reads")
-
     comm = pa_dist.make_comm(local) if (world > 1 and args.reduce == "capi") else None
     # the ranks an RCCL communicator of this job really spans (ncclCommCount);
     # the torch path's communicator is torch's own, so one is made to ask
@@ -683,8 +677,10 @@ def main():
         if rccl_ranks != world:
             log(f"[rank {rank}] error: the RCCL communicator spans {rccl_ranks} ranks, WORLD_SIZE is {world}")
             sys.exit(4)
+    cur = {}
 
     def step():
+        index, reads, result = cur["index"], cur["reads"], cur["result"]
         result.reset(stream)
         N.align(index, reads, prm, first_read, result, stream)
         if world > 1:
@@ -696,6 +692,7 @@ def main():
     def timed_passes(n):
         """n passes between barriers + device syncs; (max-over-ranks seconds,
         {kernel: (ms, launches)} of HIP events around each launch)."""
+        index = cur["index"]
         index.profile_read()  # (drop earlier events)
         index.profile_enable(True)
         if world > 1:
@@ -719,29 +716,56 @@ def main():
         out = [float(x) for x in t.tolist()]
         return out[0] if len(out) == 1 else out
 
-    # 1) the job as the product runs it: the index built for npg reads, one pass
-    #    of them (timed over a few passes; fewer than would bring the reads
-    #    aligned past the neighbour bits' break-even)
+    # 1) the job as the product runs it: the index built for this rank's npg
+    #    reads (the neighbour bits only past their break-even), then one pass of
+    #    them (timed over a few passes: fewer than would bring the reads aligned
+    #    past the break-even, where the align would make the bits itself)
     product = None
+    job_tm = None
     if not args.traffic_child:
+        jix, _, job_tm = build_index(npg)
+        job_bytes = int(jix.info().device_bytes)
+        jreads, _ = make_reads(jix)
+        cur.update(index=jix, reads=jreads, result=N.Result(jix))
         step()  # (warmup)
         torch.cuda.synchronize(dev)
         np_ = max(1, min(args.steps, 5))
         p_el, p_kern = timed_passes(np_)
-        nb_during = int(index.info().device_bytes) != job_index_bytes
         product = {"passes": np_, "pass_s": p_el / np_, "reads_per_s": world * npg * np_ / p_el,
                    "kernels_ms": {k: v[0] / v[1] for k, v in p_kern.items() if v[1]},
-                   "valid": not nb_during}
-    # 2) the serving index: the neighbour bits made now (a no-op when the job
-    #    already repaid them) -- the index a long-lived aligner keeps
-    bytes0 = int(index.info().device_bytes)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    index.prepare(stream)
-    torch.cuda.synchronize(dev)
-    nb_s = time.perf_counter() - t0
-    nb_built = int(index.info().device_bytes) > bytes0
+                   "device_bytes": job_bytes, "valid": int(jix.info().device_bytes) == job_bytes}
+        for h in ("result", "reads", "index"):
+            cur.pop(h).close()
+        torch.cuda.synchronize(dev)
+    # 2) the serving index -- the full align-side view (neighbour bits), what a
+    #    long-lived aligner keeps and what pa_index_build makes -- built anew
+    #    from the same genomes: the measured passes below run on it
+    index, genomes, srv_tm = build_index(None)
+    build_s, prepare_s, index_total_s = srv_tm["first_build_s"], srv_tm["prepare_s"], srv_tm["build_s"]
+    build_bases = srv_tm["bases_built"]
+    extsim = srv_tm["extsim"] or (job_tm or {}).get("extsim")
+    reads, reads_make_s = make_reads(index)
+    result = N.Result(index)
+    cur.update(index=index, reads=reads, result=result)
     info = index.info()
+    nb_built = product is not None and int(info.device_bytes) > product["device_bytes"]
+    nb_s = index_total_s - job_tm["build_s"] if job_tm else 0.0
+    # the filters a pass really applies: thresholds at or below the batch's
+    # smallest quality byte filter nothing (quirk 5) and are dropped
+    eff, q_min = reads.effective(prm, stream)
+    applied = {}
+    if eff.flags & N.HAS_MRQ:
+        applied["mrq"] = pk.get("mrq")
+    if eff.flags & N.HAS_MKQ:
+        applied["mkq"] = pk.get("mkq")
+    if eff.flags & N.HAS_MG:
+        applied["mg"] = pk.get("mg")
+    elided = [n for n, f in (("mrq", N.HAS_MRQ), ("mkq", N.HAS_MKQ)) if (prm.flags & f) and not (eff.flags & f)]
+    quality_applied = bool(eff.flags & (N.HAS_MRQ | N.HAS_MKQ))
+    log(f"[rank {rank}] genomes {gen_s:.1f}s, serving index {index_total_s:.2f}s (first build {build_s:.2f}s, "
+        f"align-side view {prepare_s:.2f}s), job index {job_tm['build_s'] if job_tm else float('nan'):.2f}s: "
+        f"{info.n_kmers} k-mers, {info.n_multi_classes} multi-genome sets, table {info.table_bytes / 2**30:.2f} GiB; "
+        f"{npg} reads")
 
     if args.traffic_child:  # under rocprofv3: warmup + the measured passes, nothing else
         for _ in range(args.warmup + args.steps):
@@ -768,7 +792,8 @@ def main():
     kern = index.profile_read_kernels()
     index.profile_enable(False)
     elapsed = max_over_ranks(elapsed)
-    build_max, nb_max = max_over_ranks(index_total_s, nb_s)
+    job_build_s = job_tm["build_s"] if job_tm else index_total_s
+    build_max, srv_build_max, nb_max = max_over_ranks(job_build_s, index_total_s, nb_s)
     # every rank's align-kernel times (HIP events on its own stream), for the
     # rank-0 line: at N > 1 no counter pass runs, so the roofline of a scaling
     # run comes from these and the section 8(d) algorithmic bytes
@@ -825,8 +850,8 @@ def main():
                    "filters_note": (f"{'/'.join(elided)} elided (q_min = {q_min}: a threshold at or below the batch's "
                                     "smallest quality byte filters nothing, strict <, quirk 5; measured when the reads "
                                     "are made, outside the timed step)") if elided else None,
-                   "index": ("serving: neighbour bits built (pa_index_prepare after the job-index passes)"
-                             if nb_built or not product else "job index (neighbour bits already repaid)"),
+                   "index": ("serving: the full align-side view, neighbour bits included (built anew after the "
+                             "job-index passes, pa_index_prepare)"),
                    "parallelism": f"read-sharded x{world}, index replicated",
                    "reduce": args.reduce if world > 1 else None, "backend": backend, "rccl_ranks": rccl_ranks,
                    "read_mix": {"reverse_complement": cfg.get("rc_rate", 0.0), "foreign": cfg.get("foreign_rate", 0.0),
@@ -857,13 +882,16 @@ def main():
         "neighbour_bits_breakeven": breakeven,
         "deferred_read_fraction": deferred / max(npg * args.steps, 1),
         "job_counters": job_counters,
-        "index": {"build_s": index_total_s, "first_build_s": build_s, "prepare_s": prepare_s,
-                  "neighbour_bits_s": nb_s, "serving_build_s": index_total_s + nb_s,
-                  "reads_make_s": reads_make_s,
-                  "build_basis": ("FASTA genomes in host memory -> the job's align-ready index: table + genome sets"
+        "index": {"build_s": job_build_s, "serving_build_s": index_total_s,
+                  "serving_first_build_s": build_s, "serving_prepare_s": prepare_s,
+                  "job_first_build_s": job_tm["first_build_s"] if job_tm else None,
+                  "job_prepare_s": job_tm["prepare_s"] if job_tm else None,
+                  "neighbour_bits_s": nb_s, "reads_make_s": reads_make_s,
+                  "build_basis": ("FASTA genomes in host memory -> an align-ready index: table + genome sets"
                                   + (", EXTSIM statistics and greedy pass, rebuild of the kept genomes" if extsim else "")
-                                  + ", tiles / Bloom filter (neighbour bits when the job repays them); "
-                                    "neighbour_bits_s: making them afterwards for the serving index"),
+                                  + ", tiles / Bloom filter; build_s: the job's index (neighbour bits only when the "
+                                    "job repays them), serving_build_s: the serving index the timed passes run on "
+                                    "(every bit; built anew), neighbour_bits_s: their difference"),
                   "n_kmers": int(info.n_kmers), "multi_genome_sets": int(info.n_multi_classes),
                   "table_bytes": int(info.table_bytes), "table_slots": int(info.table_slots)},
         "extsim": extsim,
@@ -874,10 +902,11 @@ def main():
     bases_built = int(build_bases)
     ib = out["index"]
     ib["bases_built"] = bases_built
-    ib["Mbp_per_s"] = bases_built / index_total_s / 1e6 if index_total_s > 0 else None
-    ib["roofline"] = {"bytes_per_base": 17, "achieved": 17 * bases_built / index_total_s / 1e9,
-                      "frac": 17 * bases_built / index_total_s / 1e9 / HBM_PEAK_GBS, "unit": "GB/s",
-                      "basis": "17 B per genome base of every build (first build + EXTSIM rebuild) / build_s"}
+    ib["Mbp_per_s"] = bases_built / job_build_s / 1e6 if job_build_s > 0 else None
+    ib["roofline"] = {"bytes_per_base": 17, "achieved": 17 * bases_built / job_build_s / 1e9,
+                      "frac": 17 * bases_built / job_build_s / 1e9 / HBM_PEAK_GBS, "unit": "GB/s",
+                      "basis": "17 B per genome base of every build (first build + EXTSIM rebuild) / build_s "
+                               "(the job's index)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize(dev)
         # C5: the oracle's full index of the kept ~5 Gbp would need ~0.7 TB of host memory
