@@ -17,5 +17,5 @@ import json, re
 d=json.load(open('$OUT/$i.json')); r=d['roofline']; ix=d['index']
 err=open('$OUT/$i.err').read()
 st=re.findall(r'(insert \+ sets|nb: first occurrences|nb: copies|tile classes|repeats \+ walk blocks) ([0-9.]+)', err)
-print('$CFG $v', round(d['value']/1e6,1), 'Mreads/s, pass', round(r['algorithmic']['pass_ms'],3), 'ms, index', round(ix['build_s'],2), 's', st)"
+print('$CFG $v', round(d['value']/1e6,1), 'Mreads/s, pass', round(r['algorithmic']['survey_8d']['pass_ms'],3), 'ms, index', round(ix['build_s'],2), 's', st)"
 done
