@@ -29,7 +29,7 @@ NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
 PA_BUILD_DEFER_TILES = 1
 PA_POS_REVERSE, PA_POS_RC_BIT = 1, 0x80000000
 PA_READS_UNKNOWN = 2 ** 64 - 1
-PA_NB_READS_PER_KBASE = 3500  # (include/pa.h: the neighbour bits' break-even, reads per 1000 genome bases)
+PA_NB_READS_PER_KBASE = 2500  # (include/pa.h: the neighbour bits' break-even, reads per 1000 genome bases)
 
 # every symbol declared in include/pa.h
 EXPORTS = (

@@ -180,9 +180,10 @@ pa_status pa_index_prepare(pa_index *idx, void *stream);
  * or by a later call of this function whose expected_reads (the reads still to
  * come) passes it.  Results never depend on them.  Returns when done. */
 #define PA_READS_UNKNOWN UINT64_MAX
-/* the measured break-even (bench.py neighbour_bits_breakeven: C2 3.26, C4 3.53
- * reads per genome base on MI355X, round 6) */
-#define PA_NB_READS_PER_KBASE 3500
+/* the measured break-even (bench.py neighbour_bits_breakeven, MI355X, round 6,
+ * reverse-complement bits made lazily: C2 1.71, C4 2.03, C5 4.28 reads per
+ * genome base) */
+#define PA_NB_READS_PER_KBASE 2500
 pa_status pa_index_prepare_ex(pa_index *idx, uint64_t expected_reads, void *stream);
 void pa_index_free(pa_index *idx);
 pa_status pa_index_get_info(const pa_index *idx, pa_index_info *out);

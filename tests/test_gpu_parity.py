@@ -487,7 +487,7 @@ def test_neighbour_bits_deferred_then_built(tmp_path):
     o = oix.align(s.tobytes(), q.tobytes(), off, read_base=0, detail=False)
     stats, *_ = pa._result.fetch()
     assert stats.tolist() == o.stats.tolist()
-    # 300 k reads > 3.5 x 60 kb: this align builds the neighbour bits first
+    # 300 k reads > 2.5 x 60 kb: this align builds the neighbour bits first
     seq2, qual2, _ = synth.sample_reads(gens, 300000, 150, seed=43, err_rate=0.01)
     s2, q2 = seq2.reshape(-1), qual2.reshape(-1)
     off2 = np.arange(0, 300001 * 150, 150, dtype=np.uint64)
