@@ -68,6 +68,9 @@ struct AlignArgs {
     const uint64_t *tile_lw;        // lane kernel walk blocks (2-bit words + flag planes per 64 positions)
     const uint64_t *tile_big;       // lane kernel, --max-genomes >= 2: plane "set size > mg" (else null)
     const void *tile_nb;            // one-substitution neighbour bits (null: none)
+    uint64_t nb_base1, nb_split;    //   words nb_split.. at nb_base1 + i * word bytes (pa_device.h NbW; ~0: one piece)
+    const uint32_t *nbbig_ld;       //   the --max-genomes >= 2 half's loads: tile_nbbig, or a dummy word 0
+    uint64_t nbbig_mask;            //   ~0 with tile_nbbig, 0 without (the loads read word 0 of a valid buffer)
     int nb_spec;                    //   1: 64-bit present | specific << 32, 0: 32-bit present
     const uint32_t *tile_nbbig;     // --max-genomes >= 2: neighbour present with a set > mg (k_nb_big; null: none)
     const uint4 *tile_nbm;          //   the same interleaved with tile_nb's words (k_nb_merge; null: none)
@@ -944,6 +947,10 @@ AlignArgs make_args(const pa_index *idx, const pa_reads *r, const pa::DevParams 
     a.tile_lw = idx->tile_cls ? idx->tile_lw : nullptr;
     a.tile_nb = idx->tile_cls ? idx->tile_nb : nullptr;
     a.nb_spec = idx->nb_spec;
+    a.nb_split = idx->tile_nb1 ? idx->nb_split : ~0ull;
+    a.nb_base1 = idx->tile_nb1 ? (uint64_t)(uintptr_t)idx->tile_nb1 - idx->nb_split * (idx->nb_spec ? 8 : 4) : 0;
+    a.nbbig_ld = (const uint32_t *)(a.tile_nb ? a.tile_nb : (const void *)a.tile_lw);  // (a valid word 0 either way)
+    a.nbbig_mask = 0;
     a.gblk = idx->tile_gblk;
     a.bloom = idx->tile_cls ? idx->bloom : nullptr;
     a.bloom_lg = idx->bloom_lg;
@@ -1207,7 +1214,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
                 a.tile_big = idx->tile_big;
                 // the neighbour bits' set-size half for this mg (12 B per base;
                 // only with the 24-B neighbour bits, and when it fits)
-                if (idx->tile_nb && idx->nb_spec && !std::getenv("PA_NO_NBBIG")) {
+                if (idx->tile_nb && idx->nb_spec && !idx->tile_nb1 && !std::getenv("PA_NO_NBBIG")) {
                     const uint64_t nw = 3 * a.tile_n;
                     if (!idx->tile_nbbig) {
                         size_t free_b = 0, total_b = 0;
@@ -1228,6 +1235,7 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
                         idx->tile_nbbig_mg = a.prm.mg;
                     }
                     a.tile_nbbig = idx->tile_nbbig;
+                    if (a.tile_nbbig) a.nbbig_ld = a.tile_nbbig, a.nbbig_mask = ~0ull;
                     // interleaved with the neighbour words (48 B per base, when it fits; PA_NO_NBM=1: none)
                     if (idx->tile_nbbig && !std::getenv("PA_NO_NBM")) {
                         if (!idx->tile_nbm) {

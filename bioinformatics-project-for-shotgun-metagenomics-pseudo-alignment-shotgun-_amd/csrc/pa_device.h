@@ -38,6 +38,20 @@ struct Slot {
     uint32_t tpos;
 };
 
+// The one-substitution neighbour words of an index (tile_nb), in one piece or
+// two: a reference whose words find no single free range in the slab pool
+// (C5's 107 GiB after EXTSIM) takes them in two halves instead of stalling on
+// the driver's reclaim of freed memory.  Word i lies at base0 + i * wb below
+// `split`, at base1 + i * wb from there (base1 biased by -split * wb on the
+// host); one piece: split = ~0.
+struct NbW {
+    uint64_t base0, base1, split;
+    template <typename T>
+    __device__ __forceinline__ T *word(uint64_t i) const {
+        return (T *)((i < split ? base0 : base1) + i * sizeof(T));
+    }
+};
+
 // Class ids are < 2^31 (the build refuses more genome-set entries), so bit 31
 // of a slot's cls is free: for references of 2^32 .. 2^33 bases it holds bit
 // 32 of the key's concatenated first position (k_tpos_concat), whose low bits

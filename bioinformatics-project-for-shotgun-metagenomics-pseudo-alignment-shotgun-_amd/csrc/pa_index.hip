@@ -970,11 +970,10 @@ __global__ __launch_bounds__(256) void k_tile_rep(const uint64_t *__restrict__ p
 // window that is the reverse complement of the genome's k-mer but for one base
 // is then resolved by one bit, as a forward one by tile_nb.
 __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
-                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
+                           const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, NbW nbw, int full,
                            const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local,
                            int pass, const uint64_t *__restrict__ bloom, uint32_t bloom_lg, int rc) {
-    unsigned long long *nb = (unsigned long long *)nb_out;  // full: 64-bit words, present | specific << 32
-    uint32_t *nb32 = (uint32_t *)nb_out;                    // else 32-bit words, present
+    // full: 64-bit words, present | specific << 32; else 32-bit words, present (nbw: one or two pieces)
     const int sh = 64 - 2 * k;
     uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -993,11 +992,11 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
 #pragma unroll
                 for (int b = 0; b < 3; b++) {
                     if (full) {
-                        const unsigned long long m = nb[3 * (fo + j) + b] & (0x100000001ull << (k - 1 - j));
-                        if (m) atomicOr(&nb[3 * (t + j) + b], m);
+                        const unsigned long long m = *nbw.word<unsigned long long>(3 * (fo + j) + b) & (0x100000001ull << (k - 1 - j));
+                        if (m) atomicOr(nbw.word<unsigned long long>(3 * (t + j) + b), m);
                     } else {
-                        const uint32_t m = nb32[3 * (fo + j) + b] & (1u << (k - 1 - j));
-                        if (m) atomicOr(&nb32[3 * (t + j) + b], m);
+                        const uint32_t m = *nbw.word<uint32_t>(3 * (fo + j) + b) & (1u << (k - 1 - j));
+                        if (m) atomicOr(nbw.word<uint32_t>(3 * (t + j) + b), m);
                     }
                 }
             }
@@ -1028,9 +1027,9 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
             for (int b = 0; b < 3; b++) {
                 if (!((f >> b) & 1u)) continue;
                 if (full)
-                    atomicOr(&nb[3 * (t + j) + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                    atomicOr(nbw.word<unsigned long long>(3 * (t + j) + b), (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
                 else
-                    atomicOr(&nb32[3 * (t + j) + b], 1u << (k - 1 - j));
+                    atomicOr(nbw.word<uint32_t>(3 * (t + j) + b), 1u << (k - 1 - j));
             }
         }
     }
@@ -1042,10 +1041,8 @@ __global__ void k_nb_build(const uint64_t *__restrict__ pk, const uint32_t *__re
 // occurrence's bits, k consecutive words per substitution (bit k - 1 - j of
 // word 3 (fo + j) + b to the same bit of word 3 (t + j) + b).
 __global__ void k_nb_copy(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls, uint64_t n, int k,
-                          const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, void *nb_out, int full,
+                          const Slot<1> *__restrict__ table, HomeCfg hc, uint32_t G, NbW nbw, int full,
                           const uint32_t *__restrict__ class_genomes, const uint64_t *__restrict__ goff, int local) {
-    unsigned long long *nb = (unsigned long long *)nb_out;
-    uint32_t *nb32 = (uint32_t *)nb_out;
     const int sh = 64 - 2 * k;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
@@ -1061,11 +1058,11 @@ __global__ void k_nb_copy(const uint64_t *__restrict__ pk, const uint32_t *__res
 #pragma unroll
             for (int b = 0; b < 3; b++) {
                 if (full) {
-                    const unsigned long long m = nb[3 * (fo + j) + b] & (0x100000001ull << (k - 1 - j));
-                    if (m) atomicOr(&nb[3 * (t + j) + b], m);
+                    const unsigned long long m = *nbw.word<unsigned long long>(3 * (fo + j) + b) & (0x100000001ull << (k - 1 - j));
+                    if (m) atomicOr(nbw.word<unsigned long long>(3 * (t + j) + b), m);
                 } else {
-                    const uint32_t m = nb32[3 * (fo + j) + b] & (1u << (k - 1 - j));
-                    if (m) atomicOr(&nb32[3 * (t + j) + b], m);
+                    const uint32_t m = *nbw.word<uint32_t>(3 * (fo + j) + b) & (1u << (k - 1 - j));
+                    if (m) atomicOr(nbw.word<uint32_t>(3 * (t + j) + b), m);
                 }
             }
         }
@@ -1092,13 +1089,11 @@ constexpr bool kNbFirstOrder = PA_NB_FIRST_ORDER != 0;
 constexpr int kNbFirstChunk = 2;  // steps whose Bloom words are in flight together
 __global__ __launch_bounds__(256) void k_nb_first(const uint64_t *__restrict__ pk, const uint32_t *__restrict__ tile_cls,
                                                   uint64_t n, int k, const Slot<1> *__restrict__ table, HomeCfg hc,
-                                                  uint32_t G, void *nb_out, int full,
+                                                  uint32_t G, NbW nbw, int full,
                                                   const uint32_t *__restrict__ class_genomes,
                                                   const uint64_t *__restrict__ goff, int local,
                                                   const uint64_t *__restrict__ bloom, uint32_t bloom_lg, int rc) {
     __shared__ uint16_t pair_of[64 * 31];  // (p - t0) << 6 | window lane, p-major
-    unsigned long long *nb = (unsigned long long *)nb_out;
-    uint32_t *nb32 = (uint32_t *)nb_out;
     for (int q = threadIdx.x; q < 64 + k - 1; q += blockDim.x) {  // one thread per p: its windows
         const int lo = q - k + 1 > 0 ? q - k + 1 : 0, hi = q < 63 ? q : 63;
         int base = 0;  // pairs of the positions before q
@@ -1170,9 +1165,9 @@ __global__ __launch_bounds__(256) void k_nb_first(const uint64_t *__restrict__ p
                 for (int b = 0; b < 3; b++) {
                     if (!((f >> b) & 1u)) continue;
                     if (full)
-                        atomicOr(&nb[3 * p + b], (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
+                        atomicOr(nbw.word<unsigned long long>(3 * p + b), (cls3[b] < G ? 0x100000001ull : 1ull) << (k - 1 - j));
                     else
-                        atomicOr(&nb32[3 * p + b], 1u << (k - 1 - j));
+                        atomicOr(nbw.word<uint32_t>(3 * p + b), 1u << (k - 1 - j));
                 }
             }
         }
@@ -1720,6 +1715,13 @@ pa_status build_nb2(pa_index *idx, hipStream_t st);
 
 pa_status build_nb3(pa_index *idx, hipStream_t st);
 
+// The device view of an index's neighbour words (wb: 8 or 4 bytes per word).
+NbW nb_words(const pa_index *idx, uint64_t wb) {
+    const uint64_t b0 = (uint64_t)(uintptr_t)idx->tile_nb;
+    if (!idx->tile_nb1) return NbW{b0, 0, ~0ull};
+    return NbW{b0, (uint64_t)(uintptr_t)idx->tile_nb1 - idx->nb_split * wb, idx->nb_split};
+}
+
 // The reverse-complement neighbour bits (tile_rcnb, 12 B per base) when they
 // leave a quarter of the free memory; bb: the build-time Bloom filter of the
 // keys (nullable: every neighbour probed).
@@ -1737,18 +1739,19 @@ pa_status build_rcnb(pa_index *idx, hipStream_t st, const uint64_t *bb, uint32_t
         return PA_OK;  // (no room: the seedless reads are walked without them)
     }
     PA_HIP(hipMemsetAsync(idx->tile_rcnb, 0, n * 12 + 64, st));
+    const NbW rc_words{(uint64_t)(uintptr_t)idx->tile_rcnb, 0, ~0ull};
     for (int pass = 0; pass < 2; pass++)
         if (pass == 0 && kNbFirstOrder)
             hipLaunchKernelGGL(k_nb_first, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
-                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, (void *)idx->tile_rcnb, 0,
+                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, rc_words, 0,
                                idx->class_genomes, idx->goff, idx->tpos_local, bb, bb_lg, 1);
         else if (pass == 1)
             hipLaunchKernelGGL(k_nb_copy, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
-                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, (void *)idx->tile_rcnb, 0,
+                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, rc_words, 0,
                                idx->class_genomes, idx->goff, idx->tpos_local);
         else
             hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0, st,
-                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, (void *)idx->tile_rcnb, 0,
+                               idx->tile_pk, idx->tile_cls, n, k, table, idx->home, G, rc_words, 0,
                                idx->class_genomes, idx->goff, idx->tpos_local, pass, bb, bb_lg, 1);
     PA_HIP(hipGetLastError());
     idx->device_bytes += n * 12;
@@ -1803,10 +1806,39 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
         const bool full = n * 24 <= free_b / 4 * 3 && !(nb_half && nb_half[0] == '1') && !idx->force_large;
         const uint64_t wb = full ? 8 : 4;
         if (n * 3 * wb <= free_b / 4 * 3) {
-            B_HIP(pa::dev_malloc(&idx->tile_nb, n * 3 * wb + 64));
-            phase_mark("nb: alloc");
-            B_HIP(hipMemsetAsync(idx->tile_nb, 0, n * 3 * wb + 64, st));
+            // one piece where the pool or the free device memory has room for
+            // it; else two halves, each of which may (no reclaim stall: the
+            // driver's reclaim of memory freed earlier ran ~60 GB/s, 1.9 s for
+            // C5's words after EXTSIM); else one piece whatever it costs.
+            // PA_NB_SPLIT=1 forces the halves (tests)
+            const uint64_t words = 3 * n, split_w = words / 2;
+            const char *fs = std::getenv("PA_NB_SPLIT");
+            const bool force_split = fs && fs[0] == '1';
+            hipError_t ea = force_split ? hipErrorOutOfMemory : pa::dev_malloc_try(&idx->tile_nb, words * wb + 64);
+            if (ea != hipSuccess) {
+                (void)hipGetLastError();
+                idx->tile_nb = nullptr;
+                if (pa::dev_malloc_try(&idx->tile_nb, split_w * wb + 64) == hipSuccess &&
+                    pa::dev_malloc_try(&idx->tile_nb1, (words - split_w) * wb + 64) == hipSuccess) {
+                    idx->nb_split = split_w;
+                } else {
+                    (void)hipGetLastError();
+                    pa::dev_free(idx->tile_nb);
+                    pa::dev_free(idx->tile_nb1);
+                    idx->tile_nb = idx->tile_nb1 = nullptr;
+                    idx->nb_split = ~0ull;
+                    B_HIP(pa::dev_malloc(&idx->tile_nb, words * wb + 64));
+                }
+            }
+            phase_mark(idx->tile_nb1 ? "nb: alloc (two pieces)" : "nb: alloc");
+            if (idx->tile_nb1) {
+                B_HIP(hipMemsetAsync(idx->tile_nb, 0, split_w * wb + 64, st));
+                B_HIP(hipMemsetAsync(idx->tile_nb1, 0, (words - split_w) * wb + 64, st));
+            } else {
+                B_HIP(hipMemsetAsync(idx->tile_nb, 0, words * wb + 64, st));
+            }
             phase_mark("nb: clear");
+            const NbW nbw = nb_words(idx, wb);
             // a build-time Bloom filter of the keys (~16 bits per key, in
             // HBM; freed below): most of the 3k neighbours of a window are
             // absent and share the window's Bloom line (minimizer-chosen),
@@ -1820,16 +1852,16 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                 if (pass == 0 && kNbFirstOrder)
                     hipLaunchKernelGGL(k_nb_first, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
                                        st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                       idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
+                                       nbw, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
                                        bb, bb_lg, 0);
                 else if (pass == 1)
                     hipLaunchKernelGGL(k_nb_copy, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
                                        st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                       idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local);
+                                       nbw, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local);
                 else
                     hipLaunchKernelGGL(k_nb_build, dim3(grid_for(n) > 65536 ? 65536 : grid_for(n)), dim3(kBlock), 0,
                                        st, idx->tile_pk, idx->tile_cls, n, k, (const Slot<1> *)table, idx->home, G,
-                                       idx->tile_nb, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
+                                       nbw, full ? 1 : 0, idx->class_genomes, idx->goff, idx->tpos_local,
                                        pass, bb, bb_lg, 0);
                 phase_mark(pass == 0 ? "nb: first occurrences" : "nb: copies");
             }
@@ -2157,6 +2189,9 @@ void index_release(pa_index *idx) {
     idx->tile_big_mg = -1;
     pa::dev_free(idx->tile_nb);
     idx->tile_nb = nullptr;
+    pa::dev_free(idx->tile_nb1);
+    idx->tile_nb1 = nullptr;
+    idx->nb_split = ~0ull;
     pa::dev_free(idx->tile_rcnb);
     idx->tile_rcnb = nullptr;
     pa::dev_free(idx->tile_nbbig);
@@ -2252,6 +2287,8 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint, bool
     idx->nb_skip = 0;
     if (rc != PA_OK) {  // the index stays usable without its align-side view
         pa::dev_free(idx->tile_cls); pa::dev_free(idx->tile_pk); pa::dev_free(idx->tile_lw); pa::dev_free(idx->tile_nb);
+        pa::dev_free(idx->tile_nb1);
+        idx->tile_nb1 = nullptr, idx->nb_split = ~0ull, idx->rcnb_pending = 0;
         pa::dev_free(idx->tile_gblk); pa::dev_free(idx->bloom); pa::dev_free(idx->tile_rcp); pa::dev_free(idx->tile_rcnb);
         pa::dev_free(idx->mm_bits);
         idx->mm_bits = nullptr;

@@ -57,6 +57,10 @@ inline hipError_t dev_malloc(T **p, size_t n) {
     return dev_malloc_raw((void **)p, n);
 }
 hipError_t dev_free(void *p);
+// Like dev_malloc but never gives the pool's idle slabs back to the driver to
+// make room (whose reclaim stalls): hipErrorOutOfMemory when no free range of
+// the pool and no free device memory can hold n bytes.
+hipError_t dev_malloc_try(void **p, size_t n);
 hipError_t dev_mem_info(size_t *free_b, size_t *total_b);
 size_t dev_trim(int dev);
 void dev_pool_stats(int dev, size_t *slab_bytes, size_t *free_bytes);
@@ -106,6 +110,8 @@ struct pa_index {
     int64_t tile_big_mg = -1;          // the --max-genomes value tile_big was made for (-1: none)
     void *tile_nb = nullptr;           // [3 tile_n] one-substitution neighbour bits (k_nb_build), optional:
     int nb_spec = 0;                   //   1: 64-bit words, present | specific << 32; 0: 32-bit words, present
+    void *tile_nb1 = nullptr;          //   its second piece, words nb_split.. (null: one piece; pa_device.h NbW)
+    uint64_t nb_split = ~0ull;
     uint32_t *tile_rcnb = nullptr;     // [3 tile_n] the same for the neighbours' reverse complements (present), optional
     int rcnb_pending = 0;              //   1: left for the first pass that queues enough seedless reads (pa_align.hip)
     int rcnb_checks = 0;               //   passes that looked and found too few

@@ -801,11 +801,12 @@ __device__ __forceinline__ void lane_walk_150(const AlignArgs &a, const uint64_t
                 nv[u] = (uint64_t)v.x | ((uint64_t)v.y << 32);
                 ng[u] = v.z;
             } else {
-                __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
+                __builtin_memcpy(&v8, (const char *)((ni < a.nb_split ? (uint64_t)(uintptr_t)a.tile_nb : a.nb_base1) +
+                                                     (a.nb_spec ? 8 * ni : 4 * ni)), 8);
                 nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
             }
             if (MG && (NW != 1 || !a.tile_nbm)) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
-                const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
+                const uint32_t gv = a.nbbig_ld[ni & a.nbbig_mask];
                 ng[u] = a.tile_nbbig ? gv : 0u;
             } else if (!MG) {
                 ng[u] = 0u;
@@ -1101,10 +1102,11 @@ __device__ __forceinline__ void lane_walk_long(const AlignArgs &a, const uint64_
             // (one 8-B load either way, 4-B aligned, no branch: the 12-B form's
             // 32-bit words loaded under a branch waited one by one)
             uint64_t v8;
-            __builtin_memcpy(&v8, (const char *)a.tile_nb + (a.nb_spec ? 8 * ni : 4 * ni), 8);
+            __builtin_memcpy(&v8, (const char *)((ni < a.nb_split ? (uint64_t)(uintptr_t)a.tile_nb : a.nb_base1) +
+                                                 (a.nb_spec ? 8 * ni : 4 * ni)), 8);
             nv[u] = a.nb_spec ? v8 : (uint64_t)(uint32_t)v8;
             if (MG) {  // --max-genomes >= 2: present with a set > mg (no branch around the load)
-                const uint32_t gv = (a.tile_nbbig ? a.tile_nbbig : (const uint32_t *)a.tile_nb)[ni];
+                const uint32_t gv = a.nbbig_ld[ni & a.nbbig_mask];
                 ng[u] = a.tile_nbbig ? gv : 0u;
             } else {
                 ng[u] = 0u;

@@ -159,6 +159,37 @@ hipError_t dev_malloc_raw(void **p, size_t n) {
     return hipSuccess;
 }
 
+hipError_t dev_malloc_try(void **p, size_t n) {
+    Pool &P = pool();
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (!P.on || n < P.min_bytes) return dev_malloc_raw(p, n);
+    const size_t len = (n + kGranule - 1) / kGranule * kGranule;
+    std::lock_guard<std::mutex> g(P.mu);
+    size_t si = 0, off = 0;
+    if (!best_fit(P, dev, len, si, off)) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < len + (1ull << 30)) return hipErrorOutOfMemory;
+        void *b = nullptr;
+        e = hipMalloc(&b, len);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return hipErrorOutOfMemory;
+        }
+        Slab s;
+        s.dev = dev, s.base = (char *)b, s.size = len, s.free_bytes = len;
+        s.free[0] = len;
+        P.slabs.push_back(std::move(s));
+        si = P.slabs.size() - 1, off = 0;
+    }
+    Slab &s = P.slabs[si];
+    take(s, off, len);
+    *p = s.base + off;
+    P.live[*p] = Live{si, off, len};
+    return hipSuccess;
+}
+
 // A pooled range is reusable only once no queued work can still touch it:
 // hipFree waits for the device, so the pool does too before the range goes
 // back (kernels of the public async API on a caller's stream may still read a

@@ -464,6 +464,21 @@ def test_fast_kernel_vs_oracle_without_neighbour_bits(cfg, monkeypatch):
     test_fast_kernel_vs_oracle(cfg)
 
 
+SPLIT = [c for c in SYNTH if c[4] <= 31 and c[0] in (12, 25, 500)]
+
+
+@pytest.mark.parametrize("half", [False, True])
+@pytest.mark.parametrize("cfg", SPLIT, ids=[f"G{c[0]}_k{c[4]}_L{c[6]}" for c in SPLIT])
+def test_fast_kernel_vs_oracle_with_split_neighbour_words(cfg, half, monkeypatch):
+    """The neighbour words in two pieces (pa_device.h NbW: what a reference
+    whose words find no single free range of the slab pool gets, C5 after
+    EXTSIM); PA_NB_SPLIT=1 forces it, PA_NB_HALF=1 the 12-B present-only form."""
+    monkeypatch.setenv("PA_NB_SPLIT", "1")
+    if half:
+        monkeypatch.setenv("PA_NB_HALF", "1")
+    test_fast_kernel_vs_oracle(cfg)
+
+
 def test_neighbour_bits_deferred_then_built(tmp_path):
     """A FASTQ file of few reads is aligned before the neighbour bits exist
     (index_prepare's reads_hint); the align that brings the reads past
