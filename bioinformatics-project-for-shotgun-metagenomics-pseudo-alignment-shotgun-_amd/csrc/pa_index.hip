@@ -1807,15 +1807,22 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
         const uint64_t wb = full ? 8 : 4;
         if (n * 3 * wb <= free_b / 4 * 3) {
             // one piece where the pool or the free device memory has room for
-            // it; else two halves, each of which may (no reclaim stall: the
-            // driver's reclaim of memory freed earlier ran ~60 GB/s, 1.9 s for
-            // C5's words after EXTSIM); else one piece whatever it costs.
-            // PA_NB_SPLIT=1 forces the halves (tests)
-            const uint64_t words = 3 * n, split_w = words / 2;
+            // it; else two pieces -- the first in the pool's largest free
+            // range, the second in the free device memory -- when both fit
+            // without giving idle slabs back (the driver's reclaim of memory
+            // freed earlier runs ~60 GB/s: 1.9 s for C5's words after EXTSIM);
+            // else one piece whatever it costs.  PA_NB_SPLIT=1 forces two
+            // halves (tests)
+            const uint64_t words = 3 * n;
             const char *fs = std::getenv("PA_NB_SPLIT");
             const bool force_split = fs && fs[0] == '1';
             hipError_t ea = force_split ? hipErrorOutOfMemory : pa::dev_malloc_try(&idx->tile_nb, words * wb + 64);
-            if (ea != hipSuccess) {
+            // the first piece as large as the pool's largest free range (the
+            // second then from the free device memory), at least an eighth
+            const uint64_t lf = pa::dev_pool_largest_free();
+            uint64_t split_w = force_split ? words / 2 : (lf > (2ull << 20) ? (lf - (2ull << 20)) / wb : 0);
+            split_w = std::min<uint64_t>(split_w, words - words / 8);
+            if (ea != hipSuccess && split_w >= words / 8) {
                 (void)hipGetLastError();
                 idx->tile_nb = nullptr;
                 if (pa::dev_malloc_try(&idx->tile_nb, split_w * wb + 64) == hipSuccess &&
@@ -1829,11 +1836,14 @@ pa_status build_nb(pa_index *idx, hipStream_t st) {
                     idx->nb_split = ~0ull;
                     B_HIP(pa::dev_malloc(&idx->tile_nb, words * wb + 64));
                 }
+            } else if (ea != hipSuccess) {
+                (void)hipGetLastError();
+                B_HIP(pa::dev_malloc(&idx->tile_nb, words * wb + 64));
             }
             phase_mark(idx->tile_nb1 ? "nb: alloc (two pieces)" : "nb: alloc");
             if (idx->tile_nb1) {
-                B_HIP(hipMemsetAsync(idx->tile_nb, 0, split_w * wb + 64, st));
-                B_HIP(hipMemsetAsync(idx->tile_nb1, 0, (words - split_w) * wb + 64, st));
+                B_HIP(hipMemsetAsync(idx->tile_nb, 0, idx->nb_split * wb + 64, st));
+                B_HIP(hipMemsetAsync(idx->tile_nb1, 0, (words - idx->nb_split) * wb + 64, st));
             } else {
                 B_HIP(hipMemsetAsync(idx->tile_nb, 0, words * wb + 64, st));
             }

@@ -61,6 +61,7 @@ hipError_t dev_free(void *p);
 // make room (whose reclaim stalls): hipErrorOutOfMemory when no free range of
 // the pool and no free device memory can hold n bytes.
 hipError_t dev_malloc_try(void **p, size_t n);
+size_t dev_pool_largest_free();  // the largest free range of the current device's slabs
 hipError_t dev_mem_info(size_t *free_b, size_t *total_b);
 size_t dev_trim(int dev);
 void dev_pool_stats(int dev, size_t *slab_bytes, size_t *free_bytes);

@@ -538,7 +538,10 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             bool spec = false;
 #pragma unroll
             for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && cls_of(scls[i]) < a.G && stp32[i] != NONE;
-            act = (round == 0 && act != all && !spec) ? all & ~outer : 0u;
+#ifndef PA_LANE_R2_ONLY_UNSEEDED
+#define PA_LANE_R2_ONLY_UNSEEDED 0  // 1 (A/B): the second round only when the first found no seed at all
+#endif
+            act = (round == 0 && act != all && !spec && (!PA_LANE_R2_ONLY_UNSEEDED || f == 0)) ? all & ~outer : 0u;
 #if defined(PA_STATS) || defined(PA_DISSECT)
             if (a.dbg_mode == 14) act = 0;  // timing dissection: one seed round
 #endif

@@ -226,6 +226,19 @@ hipError_t dev_free(void *p) {
 // every idle slab (a request that fits none is met by trimming them), plus
 // the largest free range of a slab in use -- not the sum of scattered ranges,
 // which no single buffer can span.  Callers size tables and tiles on this.
+size_t dev_pool_largest_free() {
+    Pool &P = pool();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> g(P.mu);
+    size_t largest = 0;
+    for (const Slab &s : P.slabs) {
+        if (!s.base || s.dev != dev) continue;
+        for (const auto &r : s.free) largest = std::max(largest, r.second);
+    }
+    return largest;
+}
+
 hipError_t dev_mem_info(size_t *free_b, size_t *total_b) {
     hipError_t e = hipMemGetInfo(free_b, total_b);
     if (e != hipSuccess) return e;
