@@ -539,7 +539,10 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
 #pragma unroll
             for (int i = 0; i < NSEED; i++) spec |= bit(f, i) && cls_of(scls[i]) < a.G && stp32[i] != NONE;
 #ifndef PA_LANE_R2_ONLY_UNSEEDED
-#define PA_LANE_R2_ONLY_UNSEEDED 0  // 1 (A/B): the second round only when the first found no seed at all
+#define PA_LANE_R2_ONLY_UNSEEDED 0  // 1 (A/B): the second round only when the first found no seed at all --
+                                    // C4 3.94 -> 1.95, C2 3.71 -> 1.91 G reads/s (round 6, profiles/r06/ab_r2u.txt):
+                                    // a stretch named by a shared outer seed is a family's first member, and the
+                                    // walk on it sends most such reads to the wave kernel
 #endif
             act = (round == 0 && act != all && !spec && (!PA_LANE_R2_ONLY_UNSEEDED || f == 0)) ? all & ~outer : 0u;
 #if defined(PA_STATS) || defined(PA_DISSECT)
