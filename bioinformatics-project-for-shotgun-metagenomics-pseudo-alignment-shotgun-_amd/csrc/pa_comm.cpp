@@ -48,8 +48,28 @@ Rccl &rccl() {
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
+        // RCCL from the ROCm whose HIP runtime this process runs libpa.so on
+        // (the directory of the libamdhip64 that hipGetDeviceCount resolved
+        // to): a process that also maps torch's bundled runtime otherwise may
+        // get an RCCL of the other runtime, which sees no device
+        // ("pfn_hsa_system_get_info failed", round 6)
         const char *path = std::getenv("PA_RCCL_LIBRARY");
-        void *h = dlopen(path && *path ? path : "librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        void *h = nullptr;
+        if (path && *path) {
+            h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+        } else {
+            Dl_info info{};
+            if (dladdr((void *)&hipGetDeviceCount, &info) && info.dli_fname) {
+                std::string dir(info.dli_fname);
+                const size_t cut = dir.rfind('/');
+                if (cut != std::string::npos) {
+                    dir.resize(cut);
+                    for (const char *name : {"/librccl.so.1", "/librccl.so"})
+                        if (!h) h = dlopen((dir + name).c_str(), RTLD_NOW | RTLD_LOCAL);
+                }
+            }
+            if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        }
         if (!h) {
             r.err = std::string("RCCL not available: ") + dlerror();
             return;

@@ -12,6 +12,8 @@ reduction (pa_counters_reduce, the C ABI) is checked on one rank: an identity.
 """
 
 import os
+import sys
+import subprocess
 import socket
 
 import numpy as np
@@ -110,7 +112,18 @@ def test_two_ranks_gpu_reduce_equals_one_process():
 
 def test_rccl_counters_reduce_single_rank():
     """pa_counters_reduce through the C ABI on a one-rank communicator: the
-    collective runs (RCCL opened by libpa.so) and leaves the counters as they were."""
+    collective runs (RCCL opened by libpa.so) and leaves the counters as they
+    were.  In a fresh interpreter: this test process has mapped torch's
+    bundled HIP runtime beside ROCm's by now (the gloo tests), and RCCL's own
+    HSA lookups could then find the uninitialised one ("no ROCm-capable
+    device", round 6) -- a product process uses one runtime."""
+    if os.environ.get("PA_RCCL_TEST_CHILD") != "1":
+        r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+                            f"{os.path.abspath(__file__)}::test_rccl_counters_reduce_single_rank"],
+                           env=dict(os.environ, PA_RCCL_TEST_CHILD="1"), stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-3000:]
+        return
     gens, seq, qual, off = _data()
     index = N.Index(gens, 31)
     res = N.Result(index)
