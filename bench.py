@@ -834,7 +834,9 @@ def main():
         breakeven = {"neighbour_bits_s": nb_max, "saved_ns_per_read": saved * 1e9,
                      "cost_ns_per_base": per_base * 1e9,
                      "reads_per_base": per_base / saved if saved > 0 else None,
-                     "policy_reads_per_base": N.PA_NB_READS_PER_KBASE / 1000,
+                     "policy_reads_per_base": (N.PA_NB_READS_PER_KBASE if cfg["k"] <= 31 else
+                                               N.PA_NB_READS_PER_KBASE_2W if cfg["k"] <= 63 else
+                                               N.PA_NB_READS_PER_KBASE_3W) / 1000,
                      "basis": "neighbour bits' build time per genome window / align time they save per read "
                               "(job-index pass - serving-index pass, per read)"}
     out = {

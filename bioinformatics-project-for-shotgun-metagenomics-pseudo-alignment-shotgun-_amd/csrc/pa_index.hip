@@ -2270,14 +2270,14 @@ pa_status index_build_rcnb(pa_index *idx, hipStream_t st) {
 
 pa_status index_note_reads(pa_index *idx, uint64_t n, hipStream_t st) {
     idx->reads_seen += n;
-    if (!idx->nb_pending || !nb_repaid(idx->reads_seen, idx->tile_n)) return PA_OK;
+    if (!idx->nb_pending || !nb_repaid(idx->reads_seen, idx->tile_n, idx->nw)) return PA_OK;
     return build_nb(idx, st);
 }
 
 pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint, bool complete) {
     if (!idx->tiles_pending) {  // (tiles made: the pending neighbour bits, if the reads still to come repay them)
         if (complete && idx->nb_pending &&
-            (reads_hint == ~0ull || nb_repaid(idx->reads_seen + reads_hint, idx->tile_n))) {
+            (reads_hint == ~0ull || nb_repaid(idx->reads_seen + reads_hint, idx->tile_n, idx->nw))) {
             std::unique_ptr<PhaseTimer> own;
             if (!t_phase) own.reset(new PhaseTimer(st));
             PhaseScope ps(t_phase ? t_phase : own.get());
@@ -2290,7 +2290,7 @@ pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint, bool
     if (!t_phase) own.reset(new PhaseTimer(st));
     PhaseScope ps(t_phase ? t_phase : own.get());
     const uint64_t bases = idx->h_goff.empty() ? 0 : idx->h_goff.back();
-    idx->nb_skip = reads_hint != ~0ull && !nb_repaid(reads_hint, bases);
+    idx->nb_skip = reads_hint != ~0ull && !nb_repaid(reads_hint, bases, idx->nw);
     pa_status rc = idx->nw == 3   ? build_tiles_nw<3>(idx, st)
                    : idx->nw == 2 ? build_tiles_nw<2>(idx, st)
                                   : build_tiles_nw<1>(idx, st);  // (keys of one to three words)

@@ -194,8 +194,12 @@ pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream
 // the reads aligned pass that point): they cost ~0.5 ns per base and save
 // ~0.25 ns per read on C2 (3.43 vs 1.87 G reads/s; build 0.36 vs 0.24 s).
 constexpr uint64_t kNbReadsPerKBase = PA_NB_READS_PER_KBASE;
-// reads past the neighbour bits' break-even for an index of `bases` genome bases
-inline bool nb_repaid(uint64_t reads, uint64_t bases) { return reads >= (bases * kNbReadsPerKBase + 999) / 1000; }
+// reads past the neighbour bits' break-even for an index of `bases` genome
+// bases and keys of nw words (two- and three-word keys' bits cost more to make)
+inline bool nb_repaid(uint64_t reads, uint64_t bases, int nw = 1) {
+    const uint64_t per_k = nw >= 3 ? PA_NB_READS_PER_KBASE_3W : nw == 2 ? PA_NB_READS_PER_KBASE_2W : kNbReadsPerKBase;
+    return reads >= (bases * per_k + 999) / 1000;
+}
 // complete: also make neighbour bits left pending, when reads_hint (the reads
 // still to come; ~0: unknown) passes the break-even (pa_index_prepare[_ex]).
 pa_status index_prepare(pa_index *idx, hipStream_t st, uint64_t reads_hint = ~0ull, bool complete = false);

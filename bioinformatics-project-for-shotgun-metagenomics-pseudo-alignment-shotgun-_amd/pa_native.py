@@ -30,6 +30,7 @@ PA_BUILD_DEFER_TILES = 1
 PA_POS_REVERSE, PA_POS_RC_BIT = 1, 0x80000000
 PA_READS_UNKNOWN = 2 ** 64 - 1
 PA_NB_READS_PER_KBASE = 2500  # (include/pa.h: the neighbour bits' break-even, reads per 1000 genome bases)
+PA_NB_READS_PER_KBASE_2W, PA_NB_READS_PER_KBASE_3W = 10000, 18000  # (two- / three-word keys)
 
 # every symbol declared in include/pa.h
 EXPORTS = (

@@ -175,15 +175,18 @@ pa_status pa_index_prepare(pa_index *idx, void *stream);
 /* The same for a job of about expected_reads reads (PA_READS_UNKNOWN: as
  * pa_index_prepare).  The one-substitution neighbour bits (DESIGN.md section
  * 3) cost time per genome base and save time per read: below the break-even
- * (PA_NB_READS_PER_KBASE reads per 1000 genome bases) they are left out, and made by
+ * (PA_NB_READS_PER_KBASE[_2W/_3W] reads per 1000 genome bases) they are left out, and made by
  * the align that brings the reads aligned with this index past that point --
  * or by a later call of this function whose expected_reads (the reads still to
  * come) passes it.  Results never depend on them.  Returns when done. */
 #define PA_READS_UNKNOWN UINT64_MAX
 /* the measured break-even (bench.py neighbour_bits_breakeven, MI355X, round 6,
- * reverse-complement bits made lazily: C2 1.71, C4 2.03, C5 4.28 reads per
- * genome base) */
+ * reverse-complement bits made lazily), reads per 1000 genome bases: keys of
+ * one word (k <= 31; C2 1.45, C4 2.05, C5 2.80 reads per base), two words
+ * (31 < k <= 63: c2k63 10.3) and three (63 < k <= 95: c2k75 18.5) */
 #define PA_NB_READS_PER_KBASE 2500
+#define PA_NB_READS_PER_KBASE_2W 10000
+#define PA_NB_READS_PER_KBASE_3W 18000
 pa_status pa_index_prepare_ex(pa_index *idx, uint64_t expected_reads, void *stream);
 void pa_index_free(pa_index *idx);
 pa_status pa_index_get_info(const pa_index *idx, pa_index_info *out);

@@ -58,7 +58,7 @@ def test_version_and_error_string():
 
 def test_header_constants_match_binding():
     text = open(os.path.join(REPO, "include", "pa.h")).read()
-    for name in ("PA_NB_READS_PER_KBASE", "PA_MAX_K"):
+    for name in ("PA_NB_READS_PER_KBASE", "PA_NB_READS_PER_KBASE_2W", "PA_NB_READS_PER_KBASE_3W", "PA_MAX_K"):
         m = re.search(rf"#define {name} (\d+)", text)
         assert m and int(m.group(1)) == getattr(N, name), name
 
