@@ -49,6 +49,11 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
+// k_align_lane's queue segments (AlignArgs::na_seg): one per wave of its
+// grid, 64 entries per chunk of reads the wave takes; the queues hold the
+// reads of a batch plus one chunk per wave of slack.
+constexpr uint32_t kSegMaxWaves = 16384;
+constexpr uint64_t kSegSlack = 64ull * kSegMaxWaves;
 constexpr uint32_t kLdsGenomeCap = 2048;  // per-workgroup LDS counters up to this many genomes
 
 enum : uint32_t { F_MRQ = 1, F_MKQ = 2, F_MG = 4 };
@@ -115,6 +120,11 @@ struct AlignArgs {
     uint32_t *queue_na2;                   // k_rc_seeds / k_align_lane_rc: the reads to test window by window
     unsigned long long *queue_na2_count;   //   (k_align_lane_na)
     uint64_t na_min;                       // fewer than this: k_align_lane_na hands them to the wave kernel
+    uint32_t na_seg;                       // k_align_lane queues its seedless reads (queue_na, queue_na_keys) in
+    uint32_t *seg_cnt;                     //   per-wave segments, without atomics: wave s of its grid writes
+    uint32_t nseg;                         //   entries s * seg_cap ... and their number to seg_cnt[s]; k_rc_seeds
+    uint64_t seg_cap;                      //   takes them (nseg: the grid's waves)
+    uint64_t queue_cap;                    // entries of every queue
     const uint4 *qmask;                    // (quality filters) per read: windows failing --min-kmer-quality
     const uint8_t *qdrop;                  //   and 1 if the read fails --min-read-quality (k_quality_masks)
     // wave kernel input: a list of read indices (null: reads 0 .. n-1)
@@ -809,12 +819,13 @@ struct KernelTimer {
 // nw: key words (2: 31 < k <= 63, 3: 63 < k <= 95 -- the 150-bp shape, no
 // reverse-strand path: reads without a seed go to the wave kernel).
 constexpr uint64_t kRcnbMinReads = 32768;  // seedless reads in a pass that make the reverse-complement bits worth it
-pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullptr, bool long_reads = false,
+pa_status launch_lane(const AlignArgs &a0, hipStream_t st, pa_index *prof = nullptr, bool long_reads = false,
                       int nw = 1) {
-    const bool need_q = (a.prm.flags & (F_MRQ | F_MKQ)) != 0;
-    const bool win_q = (a.prm.flags & F_MKQ) != 0;
-    const bool mg = (a.prm.flags & F_MG) != 0;
+    const bool need_q = (a0.prm.flags & (F_MRQ | F_MKQ)) != 0;
+    const bool win_q = (a0.prm.flags & F_MKQ) != 0;
+    const bool mg = (a0.prm.flags & F_MG) != 0;
     const bool nm4 = long_reads && !win_q && nw == 1;
+    AlignArgs a = a0;
     const size_t shm = lane_lds_bytes(a.G, nm4 ? 4 : 2);
     auto kern = nw == 3
                     ? (win_q ? (mg ? k_align_lane<true, true, true, 2, 3> : k_align_lane<true, true, false, 2, 3>)
@@ -837,6 +848,18 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
     const uint64_t want = (a.n + kBlock - 1) / kBlock;
     const uint64_t resident = (uint64_t)std::max(1, per_cu) * (uint64_t)cus;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(want, resident));
+    // the seedless reads for k_rc_seeds in per-wave queue segments: one
+    // atomic per wave and chunk on the queue's counter serialised, and cost
+    // c2rc (half its reads seedless) 0.27 ms per 10 M reads (PA_NA_SEG=0: the
+    // flat queue, A/B)
+    {
+        const char *e = std::getenv("PA_NA_SEG");
+        const uint64_t waves = (uint64_t)grid * kWaves, chunks = (a.n + 63) / 64;
+        a.nseg = (uint32_t)waves;
+        a.seg_cap = 64 * ((chunks + waves - 1) / waves);
+        a.na_seg = a.queue_na && a.queue_na_keys && a.seg_cnt && !nm4 && nw == 1 && waves <= kSegMaxWaves &&
+                   waves * a.seg_cap <= a.queue_cap && !(e && e[0] == '0');
+    }
     {
         KernelTimer kt(prof, st, PA_PROF_LANE);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), shm, st, a);
@@ -863,9 +886,10 @@ pa_status launch_lane(const AlignArgs &a, hipStream_t st, pa_index *prof = nullp
         if (a.queue_na_keys) {  // reverse-complement seeds, the reverse-strand walk; the rest on to k_align_lane_na
             {
                 KernelTimer kt(prof, st, PA_PROF_RC_SEEDS);
-                hipLaunchKernelGGL(k_rc_seeds, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(
-                                                        (a.n + kBlock * 4 - 1) / (kBlock * 4), 8192))),
-                                   dim3(kBlock), 0, st, b);
+                const unsigned sgrid = a.na_seg ? (a.nseg + kSegGroup - 1) / kSegGroup  // (a group of segments per block)
+                                                : (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(
+                                                      (a.n + kBlock * 4 - 1) / (kBlock * 4), 8192));
+                hipLaunchKernelGGL(k_rc_seeds, dim3(sgrid), dim3(kBlock), 0, st, b);
                 PA_HIP(hipGetLastError());
             }
             auto rc = win_q ? (mg ? k_align_lane_rc<true, true, true> : k_align_lane_rc<true, true, false>)
@@ -1042,6 +1066,8 @@ pa_status ensure_qmask(pa_index *idx, uint64_t n) {
 }
 
 pa_status reserve_queues(pa_index *idx, uint64_t n) {
+    if (!idx->seg_cnt) PA_HIP(pa::dev_malloc(&idx->seg_cnt, (uint64_t)kSegMaxWaves * 4));
+    n += kSegSlack;
     if (idx->queue_cap >= n) return PA_OK;
     pa::dev_free(idx->queue);
     pa::dev_free(idx->queue_hard);
@@ -1292,6 +1318,8 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.queue_rc = idx->queue_rc;
             a.queue_rc_anc = idx->queue_rc_anc;
             a.queue_rc_count = idx->na_count + 1;
+            a.seg_cnt = idx->seg_cnt;
+            a.queue_cap = idx->queue_cap;
             a.queue_na2 = idx->queue_na2;
             a.queue_na2_count = idx->na_count + 2;
             a.na_min = 32768;  // (PA_NA_MIN: tests)

@@ -2234,6 +2234,8 @@ void index_release(pa_index *idx) {
     idx->queue_rc = nullptr;
     idx->queue_rc_anc = nullptr;
     pa::dev_free(idx->na_count);
+    pa::dev_free(idx->seg_cnt);
+    idx->seg_cnt = nullptr;
     pa::dev_free(idx->qmask);
     pa::dev_free(idx->qdrop);
     idx->qmask = nullptr;

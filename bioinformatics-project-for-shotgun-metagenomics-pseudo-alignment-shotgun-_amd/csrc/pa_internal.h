@@ -144,7 +144,8 @@ struct pa_index {
     uint8_t *qdrop = nullptr;          // per read: fails --min-read-quality
     uint64_t qmask_cap = 0;
     unsigned long long *na_count = nullptr;
-    uint64_t queue_cap = 0;
+    uint32_t *seg_cnt = nullptr;       // [kSegMaxWaves] the lane kernel's per-wave queue segments (pa_align.hip)
+    uint64_t queue_cap = 0;            // entries of every queue (the reads of a batch + kSegSlack)
     uint64_t *counters = nullptr;      // [0] queue length, [1] deferred total, [2] error flags, [3] hard reads,
                                        // [4..31] PA_STATS counters
     // profiling

@@ -1419,6 +1419,11 @@ void k_align_lane(AlignArgs a) {
     // waves for a second walk.  Every decision below is wave-uniform.
     const uint64_t n_chunks = (a.n + 63) / 64, wave_stride = (uint64_t)gridDim.x * kWaves;
     uint64_t chunk = (uint64_t)blockIdx.x * kWaves + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // this wave's segment of the seedless reads' queue (a.na_seg): entries
+    // seg_base ... seg_base + seg_na (scalar)
+    const uint32_t wave_id = (uint32_t)chunk;
+    const uint64_t seg_base = (uint64_t)wave_id * a.seg_cap;
+    uint32_t seg_na = 0;
     uint32_t n_again = 0;  // entries in LW.again_r / again_a
     while (true) {
         uint32_t r = ~0u;  // (a batch holds < 2^32 reads: pa::align)
@@ -1575,7 +1580,15 @@ void k_align_lane(AlignArgs a) {
         }
         const bool na = S.kind == LANE_NOANCHOR;
         const uint64_t nab = __ballot(na);
-        if (nab) {  // one queue allocation per wave
+        if (NM == 2 && a.na_seg) {  // into this wave's segment, with the keys k_rc_seeds probes
+            if (na) {
+                const uint64_t e = seg_base + seg_na + lanes_below(nab);
+                a.queue_na[e] = r;
+                a.queue_na_keys[2 * e] = S.P[0];
+                a.queue_na_keys[2 * e + 1] = S.P[1];
+            }
+            seg_na += (uint32_t)__popcll(nab);
+        } else if (nab) {  // one queue allocation per wave
             uint64_t qbase = 0;
             if (lane == __builtin_ctzll(nab)) qbase = atomicAdd(a.queue_na_count, (unsigned long long)__popcll(nab));
             qbase = shfl64(qbase, __builtin_ctzll(nab));
@@ -1614,6 +1627,10 @@ void k_align_lane(AlignArgs a) {
         if (WIN_Q) n_qf += wave_sum(settled ? S.qf : 0u);
     }
     if (lane == 0) {
+        if (NM == 2 && a.na_seg) {  // every wave of the grid writes its segment's count
+            a.seg_cnt[wave_id] = seg_na;
+            if (seg_na) atomicAdd(a.queue_na_count, (unsigned long long)seg_na);
+        }
         if (n_uniq) atomicAdd(&a.stats[0], (unsigned long long)n_uniq);
         if (n_amb) atomicAdd(&a.stats[1], (unsigned long long)n_amb);
         if (n_unm) atomicAdd(&a.stats[2], (unsigned long long)n_unm);
@@ -2207,6 +2224,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PA_NA_WA
 // the read, keeps the reads k_align_lane_rc cannot walk out of its waves (it
 // took ~0.2 ns per such read to load, pack and reject it).
 constexpr int kSeedReads = 4;  // reads per thread (their probes in flight together)
+constexpr uint32_t kSegGroup = 4;  // (a.na_seg) k_align_lane queue segments per block, taken as one run
 __global__ __launch_bounds__(kBlock) void k_rc_seeds(AlignArgs a) {
     // queue slots are taken per block (LDS counters, one global atomic per
     // queue and block of kBlock * kSeedReads reads): one atomic per wave
@@ -2214,10 +2232,33 @@ __global__ __launch_bounds__(kBlock) void k_rc_seeds(AlignArgs a) {
     // for 5 M reads)
     __shared__ uint32_t cnt[2];
     __shared__ unsigned long long base[2];
-    const uint64_t n = *a.queue_na_count;
-    const bool forward = n < a.na_min;  // (few such reads: all on to k_align_lane_na, which hands them on)
+    const uint64_t n_all = *a.queue_na_count;
+    const bool forward = n_all < a.na_min;  // (few such reads: all on to k_align_lane_na, which hands them on)
     constexpr uint64_t kChunk = (uint64_t)kBlock * kSeedReads;
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < n; c0 += (uint64_t)gridDim.x * kChunk) {
+    // the reads: one flat queue_na, or (a.na_seg) k_align_lane's per-wave
+    // segments of it, kSegGroup segments per block taken as one run (entry i
+    // of segment sg at sg * seg_cap + i; a block per segment cost C4 ~40 us
+    // of block starts and queue atomics for its few seedless reads)
+    const bool segd = a.na_seg != 0;
+    const uint32_t nunits = segd ? (a.nseg + kSegGroup - 1) / kSegGroup : 1u;
+#pragma unroll 1
+    for (uint32_t u = segd ? blockIdx.x : 0u; u < nunits; u += segd ? gridDim.x : 1u) {
+    uint32_t pc[kSegGroup + 1];  // the group's segments' entries, running sums
+    pc[0] = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < kSegGroup; g++)
+        pc[g + 1] = pc[g] + (segd && u * kSegGroup + g < a.nseg ? a.seg_cnt[u * kSegGroup + g] : 0u);
+    const uint64_t n = segd ? (uint64_t)pc[kSegGroup] : n_all;
+    auto qi = [&](uint64_t i) -> uint64_t {  // the queue index of the run's entry i
+        if (!segd) return i;
+        uint32_t g = 0, b0 = 0;
+#pragma unroll
+        for (uint32_t h = 1; h < kSegGroup; h++)
+            if (i >= pc[h]) g = h, b0 = pc[h];
+        return (uint64_t)(u * kSegGroup + g) * a.seg_cap + (i - b0);
+    };
+    for (uint64_t c0 = segd ? 0ull : (uint64_t)blockIdx.x * kChunk; c0 < n;
+         c0 += segd ? kChunk : (uint64_t)gridDim.x * kChunk) {
         if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
         __syncthreads();
         // R' window 0 first (found for ~86 % of reverse-strand reads at 0.5 %
@@ -2230,7 +2271,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_seeds(AlignArgs a) {
             const uint64_t i = c0 + (uint64_t)j * kBlock + threadIdx.x;
             sk[j] = 0;
             if (i < n && !forward) {
-                sk[j] = a.queue_na_keys[2 * i];
+                sk[j] = a.queue_na_keys[2 * qi(i)];
                 act |= 1u << j;
             }
         }
@@ -2246,7 +2287,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_seeds(AlignArgs a) {
                 walk |= 1u << j;
                 seed[j] = first_pos(cl[j], tp[j], a.G, a.class_genomes, a.goff, a.tpos_local);
             } else if (bit(act, j)) {
-                sk[j] = a.queue_na_keys[2 * i + 1];
+                sk[j] = a.queue_na_keys[2 * qi(i) + 1];
                 act1 |= 1u << j;
             }
         }
@@ -2273,7 +2314,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_seeds(AlignArgs a) {
         for (int j = 0; j < kSeedReads; j++) {
             const uint64_t i = c0 + (uint64_t)j * kBlock + threadIdx.x;
             if (i >= n) continue;
-            const uint32_t r = a.queue_na[i];
+            const uint32_t r = a.queue_na[qi(i)];
             if (bit(walk, j)) {
                 a.queue_rc[base[0] + slot[j]] = r;
                 a.queue_rc_anc[base[0] + slot[j]] = seed[j];
@@ -2282,6 +2323,7 @@ __global__ __launch_bounds__(kBlock) void k_rc_seeds(AlignArgs a) {
             }
         }
         __syncthreads();  // (cnt / base are reset by the next chunk)
+    }
     }
 }
 

@@ -17,11 +17,11 @@ for m in $MODES; do
   PA_LIBRARY=$P/libpa_dissect.so PA_DBG_MODE=$m timeout -k 10 300 $B --steps 20 --warmup 3 > $OUT/m$m.json 2> $OUT/m$m.err || { tail -3 $OUT/m$m.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('$OUT/m$m.json')); r=d['roofline']
-print('mode $m pass', round(r['algorithmic']['survey_8d']['pass_ms'],3), {k: round(v['ms_avg'],3) for k, v in r['kernels'].items()})"
+print('mode $m pass', round(r['algorithmic']['survey_8d']['pass_ms'],3), {k: round(v,3) for k, v in r['per_rank'][0]['kernels_ms'].items() if v > 0.02})"
 done
 for v in $VARIANTS; do
   env ${v//,/ } timeout -k 10 300 $B --steps 20 --warmup 3 > $OUT/v.json 2> $OUT/v.err || { tail -3 $OUT/v.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('$OUT/v.json')); r=d['roofline']
-print('$v', round(d['value']/1e6,1), 'Mreads/s pass', round(r['algorithmic']['survey_8d']['pass_ms'],3), {k: round(v['ms_avg'],3) for k, v in r['kernels'].items()})"
+print('$v', round(d['value']/1e6,1), 'Mreads/s pass', round(r['algorithmic']['survey_8d']['pass_ms'],3), {k: round(v,3) for k, v in r['per_rank'][0]['kernels_ms'].items() if v > 0.02})"
 done

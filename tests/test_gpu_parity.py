@@ -904,16 +904,19 @@ def test_unanchored_reads_vs_oracle(ps, noanchor, k, monkeypatch):
 
 @pytest.mark.parametrize("ps", [dict(), dict(m=0, p=0), dict(mrq=53, mkq=58, mg=10), dict(mg=2), dict(mkq=61)],
                          ids=["default", "m0p0", "c3raw", "mg2", "mkq61"])
-@pytest.mark.parametrize("rcwalk", ["1", "0"])
+@pytest.mark.parametrize("rcwalk", ["1", "1-flat", "0"])
 def test_reverse_strand_walk_vs_oracle(ps, rcwalk, monkeypatch):
     """Reads on the reverse strand (60 %), walked on it by k_align_lane_rc
     (PA_NA_RCWALK=1: the reverse-complement plane shows most of their windows
-    absent) or checked window by window by k_align_lane_na (0), against
+    absent; their seeds probed by k_rc_seeds over k_align_lane's per-wave
+    queue segments, or -- "1-flat", PA_NA_SEG=0 -- over one flat queue) or
+    checked window by window by k_align_lane_na (0), against
     genomes holding inverted repeats (a stretch followed later by its reverse
     complement: windows whose reverse complement IS a key, plane bit set) and
     palindromic runs; equal to the oracle (src/kmer.py:419-429)."""
     monkeypatch.setenv("PA_NA_MIN", "0")
-    monkeypatch.setenv("PA_NA_RCWALK", rcwalk)
+    monkeypatch.setenv("PA_NA_RCWALK", rcwalk[0])
+    monkeypatch.setenv("PA_NA_SEG", "0" if rcwalk.endswith("flat") else "1")
     gens = synth.family_genomes(10, 30000, seed=81, family_size=3, sub_rate=0.01, conserved_len=500,
                                 n_rate=2e-4, n_run=8)
     comp = np.zeros(256, dtype=np.uint8)
