@@ -615,8 +615,13 @@ __device__ __forceinline__ void lane_prep(const AlignArgs &a, uint64_t r, unsign
             // per stretch), ranked on the read's first kRankWords x 32 bases:
             // the choice only steers the walk (any stretch gives the exact
             // result), and the genome words of three whole reads in flight
-            // made the kernel spill
-            constexpr int NR = NM == 2 ? PA_LANE_RANK_WORDS : 3;  // (the 250-bp shape: its registers)
+            // made the kernel spill.  The 250-bp shape ranks on 160 of its
+            // bases (round 6: c2l250 1.58 -> 1.65 G reads/s vs 96; all 250:
+            // 28 B/lane of scratch, 1.63)
+#ifndef PA_LANE_RANK_WORDS4
+#define PA_LANE_RANK_WORDS4 5
+#endif
+            constexpr int NR = NM == 2 ? PA_LANE_RANK_WORDS : PA_LANE_RANK_WORDS4;  // (the 250-bp shape: its registers)
             const uint32_t rlen = len < 32u * NR ? len : 32u * NR;
             const bool f0 = lane_fits(a, len, e0), f1 = lane_fits(a, len, e1), f2 = e2 != INT64_MIN && lane_fits(a, len, e2);
             uint64_t g0[NR + 1], g1[NR + 1], g2[NR + 1], u3[3];
