@@ -270,6 +270,8 @@ def counter_pass(args, cfg, kept_path, save_dir=None):
            "--reads-per-gpu", str(cfg["reads_per_gpu"]), "--steps", "2", "--warmup", "1"]
     if args.genome_len:
         cmd += ["--genome-len", str(args.genome_len)]
+    if args.read_len:
+        cmd += ["--read-len", str(args.read_len)]
     if args.params is not None:
         cmd += ["--params", args.params]
     if kept_path:
@@ -527,6 +529,7 @@ def main():
                     help="workload (default c4: the metric's configuration, BASELINE.json configs[3])")
     ap.add_argument("--reads-per-gpu", type=int, default=None)
     ap.add_argument("--genome-len", type=int, default=None, help="override the genome length (experiments)")
+    ap.add_argument("--read-len", type=int, default=None, help="override the read length (experiments)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-traffic", action="store_true", help="skip the in-run counter pass (traffic, SQ shares)")
@@ -562,6 +565,9 @@ def main():
     if args.genome_len:
         cfg["genome_len"] = args.genome_len
         cfg["name"] += f" [genome_len overridden: {args.genome_len}]"
+    if args.read_len:
+        cfg["read_len"] = args.read_len
+        cfg["name"] += f" [read_len overridden: {args.read_len}]"
 
     import torch
     rank, world, local = pa_dist.init_process_group(args.dist_backend)

@@ -1325,7 +1325,12 @@ pa_status align(pa_index *idx, const pa_reads *r, const DevParams &p_in, uint64_
             a.na_min = 32768;  // (PA_NA_MIN: tests)
             if (const char *e = std::getenv("PA_NA_MIN")) a.na_min = std::strtoull(e, nullptr, 10);
             if (na) PA_HIP(hipMemsetAsync(idx->na_count, 0, 24, st));
-            PA_TRY(launch_lane(a, st, idx, r->max_len > (uint32_t)kLaneMaxLen, idx->nw));
+            // the 250-bp shape when any read is longer than the 150-bp one
+            // takes: 176 bases or 128 windows (round 6: reads of 159-176 bases
+            // at k = 31 went whole to the wave kernel, 0.15 G reads/s)
+            const bool long_reads = r->max_len > (uint32_t)kLaneMaxLen ||
+                                    (r->max_len >= idx->k && r->max_len - idx->k + 1 > (uint32_t)kLaneMaxW);
+            PA_TRY(launch_lane(a, st, idx, long_reads, idx->nw));
             a.rlist = idx->queue_hard;
             a.rlist_count = a.queue_hard_count;
         }

@@ -4,13 +4,14 @@
 # PA_DBG_MODE: 13 packing, 14 one seed round, 10 seeds, 11 walk, 12 no second
 # walk; results invalid by design), then any env variants of libpa.so.
 #   CFG=c2mix MODES="13 14 10 11 12 0" VARIANTS="PA_LANE_MAXPEND=48" bash scripts/diag.sh <tag>
+# (BARGS: more bench arguments, e.g. "--read-len 176")
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 P=$R/bioinformatics-project-for-shotgun-metagenomics-pseudo-alignment-shotgun-_amd
 OUT=$R/gpurun_out/diag_$1
 mkdir -p $OUT
 cd $R
-B="python bench.py --config $CFG --no-cpu-baseline --no-traffic --no-e2e"
+B="python bench.py --config $CFG --no-cpu-baseline --no-traffic --no-e2e $BARGS"
 PA_LIBRARY=$P/libpa_stats.so timeout -k 10 300 $B --steps 1 --warmup 0 > $OUT/stats.json 2> $OUT/stats.err || { tail -3 $OUT/stats.err; exit 1; }
 grep pa_stats $OUT/stats.err | tail -5
 for m in $MODES; do

@@ -572,11 +572,11 @@ def test_synthesized_reads_parity():
         assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist()
 
 
-@pytest.mark.parametrize("read_len", [177, 250, 272, 300, 700, 1500])
+@pytest.mark.parametrize("read_len", [158, 159, 166, 176, 177, 250, 272, 300, 700, 1500])
 def test_synthesized_long_reads_parity(read_len):
     """Device-synthesized reads longer than the 150-bp lane shape takes (the
-    256-window shape, the wave kernel past 272 bases, the exact kernel past
-    256 windows) against the oracle."""
+    256-window shape from 129 windows or 177 bases on, the wave kernel past
+    272 bases, the exact kernel past 256 windows) against the oracle."""
     gens = synth.family_genomes(20, 60000, seed=7, family_size=5, sub_rate=0.01, conserved_len=1000)
     index = N.Index(gens, 31)
     reads = N.Reads.synthesize(index, 30000, read_len, first_read=0, seed=3, sub_rate=0.008)
