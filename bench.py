@@ -530,6 +530,9 @@ def main():
     ap.add_argument("--reads-per-gpu", type=int, default=None)
     ap.add_argument("--genome-len", type=int, default=None, help="override the genome length (experiments)")
     ap.add_argument("--read-len", type=int, default=None, help="override the read length (experiments)")
+    ap.add_argument("--job-table", choices=("auto", "full"), default="auto",
+                    help="the job index's k-mer table: compact below the break-even (auto, as the CLI) or the "
+                         "serving index's (full: the line's neighbour-bit break-even is then measurable)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-traffic", action="store_true", help="skip the in-run counter pass (traffic, SQ shares)")
@@ -618,10 +621,15 @@ def main():
         Returns (index, kept genomes, timings)."""
         nonlocal kept_path
         t_all = t0 = time.perf_counter()
-        ix = N.Index(all_genomes, cfg["k"], device=local, stream=stream, defer_tiles=True)
+        # the job's table compact (PA_BUILD_COMPACT: 2 slots per genome window)
+        # below the break-even PA_COMPACT_READS_PER_BASE, as the CLI's jobs
+        bases = sum(len(g) for g in all_genomes)
+        compact = (expected_reads is not None and args.job_table == "auto" and
+                   expected_reads < N.PA_COMPACT_READS_PER_BASE * bases)
+        ix = N.Index(all_genomes, cfg["k"], device=local, stream=stream, defer_tiles=True, compact=compact)
         torch.cuda.synchronize(dev)
-        tm = {"first_build_s": time.perf_counter() - t0, "bases_built": sum(len(g) for g in all_genomes),
-              "extsim": None}
+        tm = {"first_build_s": time.perf_counter() - t0, "bases_built": bases, "extsim": None,
+              "compact_table": compact}
         kept = all_genomes
         if kept_from_file is not None:
             kept = [all_genomes[i] for i in kept_from_file]
@@ -739,7 +747,8 @@ def main():
         p_el, p_kern = timed_passes(np_)
         product = {"passes": np_, "pass_s": p_el / np_, "reads_per_s": world * npg * np_ / p_el,
                    "kernels_ms": {k: v[0] / v[1] for k, v in p_kern.items() if v[1]},
-                   "device_bytes": job_bytes, "valid": int(jix.info().device_bytes) == job_bytes}
+                   "device_bytes": job_bytes, "valid": int(jix.info().device_bytes) == job_bytes,
+                   "compact_table": job_tm["compact_table"], "table_slots": int(jix.info().table_slots)}
         for h in ("result", "reads", "index"):
             cur.pop(h).close()
         torch.cuda.synchronize(dev)
@@ -829,12 +838,18 @@ def main():
                "plan_8_gpus": {"reads": 8 * npg, "job_reads_per_s": 8 * npg / job_s,
                                "basis": "8 ranks each building the same replica and aligning its npg reads in the "
                                         "same time as this rank (weak scaling, one latency-bound all-reduce)"},
+               "compact_table": product["compact_table"],
                "basis": ("the index built for this rank's reads (pa_index_prepare_ex with expected_reads = npg: "
-                         "neighbour bits only past their break-even) from genomes in host memory, plus one align "
-                         "pass of the npg device-resident reads on it; max over ranks")}
+                         "neighbour bits only past their break-even; the compact k-mer table, PA_BUILD_COMPACT, "
+                         "below PA_COMPACT_READS_PER_BASE -- as the CLI builds them) from genomes in host memory, "
+                         "plus one align pass of the npg device-resident reads on it; max over ranks")}
     serving_pass_s = elapsed / args.steps
     breakeven = None
-    if product is not None and product["valid"] and nb_built:
+    if product is not None and product["compact_table"]:
+        breakeven = {"basis": "not measured in this line: the job index has the compact k-mer table "
+                              "(PA_BUILD_COMPACT), so job vs serving index differ in more than the neighbour "
+                              "bits; bench.py --job-table full measures it (round-6 figures: include/pa.h)"}
+    elif product is not None and product["valid"] and nb_built:
         saved = (product["pass_s"] - serving_pass_s) / npg
         per_base = nb_max / max(int(info.total_windows), 1)
         breakeven = {"neighbour_bits_s": nb_max, "saved_ns_per_read": saved * 1e9,

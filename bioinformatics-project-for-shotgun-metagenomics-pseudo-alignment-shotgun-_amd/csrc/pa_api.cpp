@@ -121,6 +121,7 @@ pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t 
                             int64_t k, uint32_t flags, void *stream, pa_index **out) {
     PA_CHECK(out != nullptr, PA_EINVAL, "out must not be NULL");
     *out = nullptr;
+    PA_CHECK((flags & ~(PA_BUILD_DEFER_TILES | PA_BUILD_COMPACT)) == 0, PA_EINVAL, "unknown build flag bits");
     PA_CHECK(genome_off != nullptr, PA_EINVAL, "genome_off must not be NULL");
     PA_CHECK(k <= PA_MAX_K, PA_EUNSUPPORTED, "k-mer length above PA_MAX_K (255) is not supported");
     PA_CHECK(n_genomes <= PA_MAX_GENOMES, PA_EUNSUPPORTED,
@@ -141,6 +142,7 @@ pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t 
     pa_index *idx = new (std::nothrow) pa_index();
     PA_CHECK(idx != nullptr, PA_ENOMEM, "out of host memory");
     idx->device = device;
+    idx->compact_table = (flags & PA_BUILD_COMPACT) != 0;
     pa_status rc = pa::index_build(idx, genomes, genome_off, n_genomes, k, as_stream(stream),
                                    (flags & PA_BUILD_DEFER_TILES) != 0);
     if (rc != PA_OK) {
@@ -159,7 +161,9 @@ pa_status pa_index_reduce(pa_index *idx, const uint32_t *keep, uint32_t n_keep, 
         PA_CHECK(keep[i] < idx->n_genomes, PA_EINVAL, "genome number out of range");
         PA_CHECK(i == 0 || keep[i] > keep[i - 1], PA_EINVAL, "genome numbers must be ascending");
     }
+    PA_CHECK((flags & ~(PA_BUILD_DEFER_TILES | PA_BUILD_COMPACT)) == 0, PA_EINVAL, "unknown build flag bits");
     PA_HIP(hipSetDevice(idx->device));
+    idx->compact_table = (flags & PA_BUILD_COMPACT) != 0;
     PA_TRY(pa::index_reduce(idx, keep, n_keep, as_stream(stream), (flags & PA_BUILD_DEFER_TILES) != 0));
     return PA_OK;
 }

@@ -2391,7 +2391,10 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     const uint64_t reserve = windows * 4 + (1ull << 30);
     auto fits = [&](uint64_t c) { return c * per_slot + reserve <= (uint64_t)free_b; };
     uint64_t cap = 0;
-    if ((4 * windows + 64) * (uint64_t)sb <= free_b / 3 && fits(4 * windows + 64))
+    // (PA_BUILD_COMPACT: 2 per window, 2 per distinct k-mer at most -- the
+    // scans of the table and its first touches shrink with it; aligns ~2 %
+    // slower, C4 job +13 %, C2 +15 %)
+    if (!idx->compact_table && (4 * windows + 64) * (uint64_t)sb <= free_b / 3 && fits(4 * windows + 64))
         cap = 4 * windows + 64;
     else if (fits(2 * windows + 64))
         cap = 2 * windows + 64;
@@ -2443,6 +2446,7 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         // profiles/r05/ab_c5_table.txt -- and build ~1.5 s slower: the larger table leaves the
         // neighbour words no free range in the slab pool, whose trim then stalls a hipMalloc)
         double mults[4] = {4.0, 2.5, 2.0, 1.43};
+        if (idx->compact_table) mults[0] = mults[1] = 2.0;
         if (const char *e = std::getenv("PA_CAP_DISTINCT")) {  // A/B: this many slots per distinct k-mer first
             const double m = std::atof(e);
             if (m >= 1.2 && m <= 8.0) mults[0] = m, mults[1] = 2.0, mults[2] = 1.43;
@@ -2519,6 +2523,7 @@ pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream
     const int64_t k = idx->k;
     const int device = idx->device;
     const bool profile = idx->profile;  // (set through the C ABI: kept across the rebuild)
+    const int compact = idx->compact_table;  // (pa_index_reduce's flags)
     // pa.h: on failure the index holds nothing and may only be freed -- so a
     // failed copy never leaves half-compacted codes behind a valid-looking index
     auto empty_index = [&]() {
@@ -2526,6 +2531,7 @@ pa_status index_reduce(pa_index *idx, const uint32_t *sel, uint32_t n, hipStream
         *idx = pa_index();
         idx->device = device;
         idx->profile = profile;
+        idx->compact_table = compact;
     };
     auto fail = [&](hipError_t err, uint8_t *scratch) -> pa_status {
         (void)hipStreamSynchronize(st);  // (the queued copies may still read or write scratch)

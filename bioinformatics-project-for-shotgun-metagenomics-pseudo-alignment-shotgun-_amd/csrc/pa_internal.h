@@ -99,6 +99,7 @@ struct pa_index {
     uint64_t distinct_estimate = 0;    // HyperLogLog estimate (+3 %) when the table was sized on it, else 0
     int released = 0;                  // a failed pa_index_reduce emptied it: it may only be freed
     int force_large = 0;               // PA_LAYOUT=large: the layout of a reference too large for the default one
+    int compact_table = 0;             // PA_BUILD_COMPACT: 2 slots per genome window (a job of few reads)
     // genome tiling (single-word keys, < 2^32 genome bases): the genomes as one
     // concatenated 2-bit string plus the class of the k-mer starting at every
     // position (NONE where no indexed window starts); slots point into it (tpos)

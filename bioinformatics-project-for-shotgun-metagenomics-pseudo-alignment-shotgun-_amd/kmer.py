@@ -201,7 +201,11 @@ class KmerReference:
     """Device-resident k-mer reference of a FASTA container (src/kmer.py:109-351)."""
 
     def __init__(self, k: int, fasta_record_container: FASTARecordContainer, filter_similar: bool = False,
-                 similarity_threshold: float = 0.95, device: Optional[int] = None) -> None:
+                 similarity_threshold: float = 0.95, device: Optional[int] = None, *,
+                 compact_table: bool = False) -> None:
+        """compact_table (not in the reference): the k-mer table at 2 slots per
+        genome window (PA_BUILD_COMPACT) -- for a job of few reads per genome
+        base, as the CLI's dumpalign / align jobs are (main.create_reference)."""
         if filter_similar and not (0 <= similarity_threshold <= 1):
             raise ValueError("similarity_threshold must be between 0 and 1")
         if not isinstance(k, int):
@@ -213,6 +217,7 @@ class KmerReference:
         self._ref_kmers: Optional[Dict[str, Dict[Record, Set[int]]]] = None  # the dict of a reference-written .kdb
         self.kmer_len: int = k
         self._device = N.default_device() if device is None else int(device)
+        self._compact = bool(compact_table)
         self._build()
         if filter_similar:
             self._filter_similar_genomes(similarity_threshold)
@@ -224,7 +229,8 @@ class KmerReference:
         # an index that EXTSIM then rebuilds from the kept genomes never needs it
         packed, self._packed = getattr(self, "_packed", None), None  # (only for the first build)
         self._index = N.Index(None if packed is not None else [g["genome"] for g in self.genomes], self.kmer_len,
-                              device=self._device, defer_tiles=True, packed=packed)
+                              device=self._device, defer_tiles=True, packed=packed,
+                              compact=getattr(self, "_compact", False))
         self._view: Optional[Dict[str, Dict[Record, Set[int]]]] = None
 
     @property

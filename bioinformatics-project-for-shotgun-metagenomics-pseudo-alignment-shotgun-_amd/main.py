@@ -163,12 +163,33 @@ def _load_reference(reference_file: str) -> KmerReference:
         sys.exit("Error: Incorrect format of input file.")
 
 
+def compact_for_job(reads_file: Optional[str], container, shards: int = 1) -> bool:
+    """The reference of a one-FASTQ job gets the compact k-mer table
+    (PA_BUILD_COMPACT) when the job has fewer than PA_COMPACT_READS_PER_BASE
+    reads per genome base -- the reads counted high, one per 64 bytes of the
+    file (4x that for gzip), over `shards` replicas."""
+    env = os.environ.get("PA_COMPACT_TABLE")  # (A/B: 0 / 1 overrides the policy)
+    if env in ("0", "1"):
+        return env == "1"
+    if not reads_file:
+        return False
+    import pa_native as N
+    try:
+        size = os.path.getsize(reads_file)
+    except OSError:
+        return False
+    reads = (size * (4 if reads_file.endswith(".gz") else 1)) // 64 // max(shards, 1)
+    bases = sum(len(g["genome"]) for g in container)
+    return reads < N.PA_COMPACT_READS_PER_BASE * bases
+
+
 def create_reference(fasta_file: str, kmer_size: int, filter_similar: bool = False,
-                     similarity_threshold: float = 0.95) -> KmerReference:
+                     similarity_threshold: float = 0.95, reads_file: Optional[str] = None) -> KmerReference:
     container = FASTAFile(fasta_file).container
     _stage("fasta parsed")
     return KmerReference(kmer_size, container, filter_similar=filter_similar,
-                         similarity_threshold=similarity_threshold)
+                         similarity_threshold=similarity_threshold,
+                         compact_table=compact_for_job(reads_file, container))
 
 
 def _prefetch_reads(reads_file: str):
@@ -274,7 +295,8 @@ def _dumpalign_sharded(args: argparse.Namespace, filt) -> Optional[PseudoAlignme
     container = FASTAFile(args.genomefile).container
     _stage("fasta parsed")
     refs = pa_shard.build_replicas(args.kmer_size, container, devices, args.filter_similar,
-                                   args.similarity_threshold)
+                                   args.similarity_threshold,
+                                   compact_table=compact_for_job(args.reads, container, len(devices)))
     _stage(f"{len(refs)} references built")
     pa = pa_shard.align_sharded(refs, args.reads, *filt)
     _stage("reads aligned (sharded)" if pa is not None else "sharded path not taken")
@@ -309,7 +331,8 @@ def _run(args: argparse.Namespace) -> None:
             ref = _load_reference(args.referencefile)
         else:
             validate_file_readable(args.genomefile, "Genome FASTA")
-            ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
+            ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold,
+                                   reads_file=args.reads)
             # saved unconditionally, as src/main.py:370 does: without -r that is
             # gzip.open(None), a TypeError the reference does not catch
             # (src/main.py:401), so the command ends with a traceback and exit
@@ -330,7 +353,8 @@ def _run(args: argparse.Namespace) -> None:
                 _print_json(sharded.get_summary())
                 return
             pf = _prefetch_reads(args.reads)
-            ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold)
+            ref = create_reference(args.genomefile, args.kmer_size, args.filter_similar, args.similarity_threshold,
+                                   reads_file=args.reads)
             _print_json(create_alignment_from_reference(ref, args.reads, *filt, prefetch=pf).get_summary())
         elif args.alignfile:
             validate_file_readable(args.alignfile, "Alignment output")

@@ -27,6 +27,8 @@ PA_COMM_ID_BYTES = 128
 HAS_MRQ, HAS_MKQ, HAS_MG = 1, 2, 4
 NO_FIRST_KEY = np.uint64(2 ** 63 - 1)  # PA_NO_FIRST_KEY
 PA_BUILD_DEFER_TILES = 1
+PA_BUILD_COMPACT = 2
+PA_COMPACT_READS_PER_BASE = 3  # (include/pa.h: the measured break-even of the compact table)
 PA_POS_REVERSE, PA_POS_RC_BIT = 1, 0x80000000
 PA_READS_UNKNOWN = 2 ** 64 - 1
 PA_NB_READS_PER_KBASE = 2500  # (include/pa.h: the neighbour bits' break-even, reads per 1000 genome bases)
@@ -386,10 +388,13 @@ class Index:
     """A device-resident k-mer index (pa_index)."""
 
     def __init__(self, genomes: Sequence, k: int, device: Optional[int] = None, stream=None,
-                 defer_tiles: bool = False, packed: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+                 defer_tiles: bool = False, packed: Optional[Tuple[np.ndarray, np.ndarray]] = None,
+                 compact: bool = False):
         """defer_tiles: build the table and genome sets only (PA_BUILD_DEFER_TILES);
         the align-side view is made by prepare() or the first align.  packed:
-        the genomes already concatenated (uint8 bytes, uint64 offsets)."""
+        the genomes already concatenated (uint8 bytes, uint64 offsets).
+        compact: the table at 2 slots per genome window (PA_BUILD_COMPACT: a
+        job of few reads per genome base; kept by reduce())."""
         t0 = time.perf_counter()
         buf, off = packed if packed is not None else concat(genomes)
         t1 = time.perf_counter()
@@ -398,13 +403,15 @@ class Index:
         h = P()
         kk = max(min(self.k, 2 ** 62), -2 ** 62)
         _check(lib().pa_index_build_ex(self.device, buf.ctypes.data_as(ctypes.c_char_p) if buf.size else None,
-                                       _ptr(off), len(off) - 1, kk, PA_BUILD_DEFER_TILES if defer_tiles else 0,
-                                       _stream(stream), ctypes.byref(h)))
+                                       _ptr(off), len(off) - 1, kk,
+                                       (PA_BUILD_DEFER_TILES if defer_tiles else 0) |
+                                       (PA_BUILD_COMPACT if compact else 0), _stream(stream), ctypes.byref(h)))
         if _TIMING:
             print(f"[pa_index] concat {1e3 * (t1 - t0):.1f} ms, pa_index_build_ex {1e3 * (time.perf_counter() - t1):.1f} "
                   "ms", file=sys.stderr, flush=True)
         self._h = h
         self.n_genomes = len(off) - 1
+        self.compact = bool(compact)
 
     @property
     def handle(self):
@@ -416,8 +423,9 @@ class Index:
         the EXTSIM rebuild without uploading the kept genomes again.  On an
         error the index is left empty and closed."""
         sel = np.ascontiguousarray(np.asarray(keep, dtype=np.uint32))
-        st = lib().pa_index_reduce(self._h, _ptr(sel), len(sel), PA_BUILD_DEFER_TILES if defer_tiles else 0,
-                                   _stream(stream))
+        st = lib().pa_index_reduce(self._h, _ptr(sel), len(sel),
+                                   (PA_BUILD_DEFER_TILES if defer_tiles else 0) |
+                                   (PA_BUILD_COMPACT if self.compact else 0), _stream(stream))
         if st != PA_OK and st != PA_EINVAL:
             self.close()
         _check(st)

@@ -133,14 +133,15 @@ def _run_threads(fns) -> list:
 
 
 def build_replicas(k: int, container, devices: Sequence[int], filter_similar: bool = False,
-                   similarity_threshold: float = 0.95):
+                   similarity_threshold: float = 0.95, compact_table: bool = False):
     """One KmerReference per device, built concurrently on host threads
     (KmerReference(k, container, ..., device=d) each: the same genomes, the same
-    EXTSIM outcome)."""
+    EXTSIM outcome; compact_table: PA_BUILD_COMPACT, main.compact_for_job)."""
     from kmer import KmerReference
     N.lib()  # (bound once, before the threads)
     return _run_threads([lambda d=d: KmerReference(k, container, filter_similar=filter_similar,
-                                                   similarity_threshold=similarity_threshold, device=d)
+                                                   similarity_threshold=similarity_threshold, device=d,
+                                                   compact_table=compact_table)
                          for d in devices])
 
 

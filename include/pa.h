@@ -158,6 +158,15 @@ pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *ge
  * filters: src/kmer.py:113-133, 252-263) before it is rebuilt from the kept
  * genomes.  pa_index_build = pa_index_build_ex(..., 0, ...). */
 #define PA_BUILD_DEFER_TILES 1u
+/* PA_BUILD_COMPACT: the k-mer table at 2 slots per genome window (default 4;
+ * sized on the distinct k-mers: 2 per k-mer at most) -- builds faster, aligns
+ * slightly slower (MI355X, round 6: C4 build 0.453 -> 0.395 s, its align pass
+ * +4 %; C2 0.057 -> 0.048 s, +3 %).  For a job of fewer than
+ * PA_COMPACT_READS_PER_BASE reads per genome base (the measured break-even,
+ * 3-5): the CLI's dumpalign job, bench.py's job index.  Results never depend
+ * on it.  Kept by pa_index_reduce when given again in its flags. */
+#define PA_BUILD_COMPACT 2u
+#define PA_COMPACT_READS_PER_BASE 3
 pa_status pa_index_build_ex(int32_t device, const char *genomes, const uint64_t *genome_off, uint32_t n_genomes,
                             int64_t k, uint32_t flags, void *stream, pa_index **out);
 /* Rebuild an index over some of its own genomes, in place: their 2-bit codes

@@ -23,5 +23,6 @@ ks={k: round(v['ms_avg'], 3) for k, v in r.get('kernels', {}).items()} or r['per
 ps=d.get('parity_sample') or {}
 print('$CFG $v', round(d['value']/1e6,1), 'Mreads/s, ms', round(d['ms_per_step'],3), 'index', round(ix['build_s'],2), 's', st,
       'kernels', {k: round(v, 3) for k, v in ks.items() if v > 0.02}, 'job', d['job_counters']['sha256'][:12],
+      'job s', round(d['job']['job_s'], 4), 'job pass ms', round(d['job']['align_pass_s'] * 1e3, 2),
       'parity', ps.get('bit_exact'), ps.get('reads'))"
 done

@@ -980,3 +980,38 @@ def test_quality_masks_every_k_vs_oracle(k):
         ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
         assert got == [o.stats.tolist(), o.unique.tolist(), o.ambiguous.tolist(), ofk.tolist()], (mrq, mkq)
         assert (mrq is None or o.stats[3] > 0) and (mkq is None or o.stats[4] > 0)
+
+
+@pytest.mark.parametrize("reduce", [False, True])
+def test_compact_table_vs_oracle(reduce):
+    """PA_BUILD_COMPACT (2 slots per genome window, the CLI's job table): the
+    same counts as the oracle, with and without an EXTSIM-style rebuild
+    (pa_index_reduce keeps the flag), and half the slots of the default table."""
+    gens = synth.family_genomes(16, 40000, seed=91, family_size=4, sub_rate=0.01, conserved_len=700,
+                                n_rate=2e-4, n_run=8)
+    full = N.Index(gens, 31)
+    index = N.Index(gens, 31, compact=True, defer_tiles=reduce)
+    keep = list(range(0, 16, 2)) if reduce else list(range(16))
+    if reduce:
+        index.reduce(keep)
+        full.close()
+        full = N.Index([gens[i] for i in keep], 31)
+    assert index.info().table_slots * 2 <= full.info().table_slots + 64
+    kept = [gens[i] for i in keep]
+    oix = O.OracleIndex(kept, 31)
+    reads = N.Reads.synthesize(index, 40000, 150, first_read=0, seed=92, sub_rate=0.01, rc_rate=0.3,
+                               foreign_rate=0.1)
+    s, q, off = reads.download()
+    for ps in (dict(), dict(mrq=58, mkq=60, mg=2), dict(m=0, p=0)):
+        prm = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+        res = N.Result(index)
+        N.align(index, reads, N.Params.make(prm["m"], prm["p"], prm["mrq"], prm["mkq"], prm["mg"]), 5, res)
+        stats, uq, am, fk = res.fetch()
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=prm["m"], p=prm["p"], mrq=prm["mrq"], mkq=prm["mkq"],
+                      mg=prm["mg"], read_base=5, detail=False)
+        assert stats.tolist() == o.stats.tolist(), ps
+        assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
+        ofk = np.where(o.first_key == np.iinfo(np.uint64).max, N.NO_FIRST_KEY, o.first_key)
+        assert fk.tolist() == ofk.tolist(), ps
+    full.close()
+    index.close()

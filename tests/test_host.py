@@ -58,9 +58,32 @@ def test_version_and_error_string():
 
 def test_header_constants_match_binding():
     text = open(os.path.join(REPO, "include", "pa.h")).read()
-    for name in ("PA_NB_READS_PER_KBASE", "PA_NB_READS_PER_KBASE_2W", "PA_NB_READS_PER_KBASE_3W", "PA_MAX_K"):
+    for name in ("PA_NB_READS_PER_KBASE", "PA_NB_READS_PER_KBASE_2W", "PA_NB_READS_PER_KBASE_3W", "PA_MAX_K",
+                 "PA_COMPACT_READS_PER_BASE"):
         m = re.search(rf"#define {name} (\d+)", text)
         assert m and int(m.group(1)) == getattr(N, name), name
+    for name in ("PA_BUILD_DEFER_TILES", "PA_BUILD_COMPACT"):
+        m = re.search(rf"#define {name} (\d+)u", text)
+        assert m and int(m.group(1)) == getattr(N, name), name
+
+
+def test_compact_table_policy(tmp_path):
+    """The CLI's job gets the compact k-mer table below PA_COMPACT_READS_PER_BASE
+    reads per genome base (reads counted high: one per 64 bytes of the FASTQ,
+    4x that for gzip, split over the shards); no reads file: the default table."""
+    import main
+    genomes = [{"genome": "ACGT" * 2500}, {"genome": "A" * 10000}]  # 20 000 bases
+    fq = tmp_path / "r.fq"
+    fq.write_bytes(b"x" * (64 * 59999))  # ~60 k reads < 3 x 20 000
+    assert main.compact_for_job(str(fq), genomes)
+    fq.write_bytes(b"x" * (64 * 60000))
+    assert not main.compact_for_job(str(fq), genomes)
+    assert main.compact_for_job(str(fq), genomes, shards=2)
+    gz = tmp_path / "r.fq.gz"
+    gz.write_bytes(b"x" * (16 * 60000))
+    assert not main.compact_for_job(str(gz), genomes)
+    assert not main.compact_for_job(None, genomes)
+    assert not main.compact_for_job(str(tmp_path / "missing.fq"), genomes)
 
 
 def test_library_built_from_this_checkout():
