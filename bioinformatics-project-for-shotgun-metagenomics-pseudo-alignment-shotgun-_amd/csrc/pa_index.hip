@@ -2391,9 +2391,8 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     const uint64_t reserve = windows * 4 + (1ull << 30);
     auto fits = [&](uint64_t c) { return c * per_slot + reserve <= (uint64_t)free_b; };
     uint64_t cap = 0;
-    // (PA_BUILD_COMPACT: 2 per window, 2 per distinct k-mer at most -- the
-    // scans of the table and its first touches shrink with it; aligns ~2 %
-    // slower, C4 job +13 %, C2 +15 %)
+    // (PA_BUILD_COMPACT: 2 per window -- the scans of the table and its first
+    // touches shrink with it; aligns ~2-4 % slower, C4 job +13 %, C2 +15 %)
     if (!idx->compact_table && (4 * windows + 64) * (uint64_t)sb <= free_b / 3 && fits(4 * windows + 64))
         cap = 4 * windows + 64;
     else if (fits(2 * windows + 64))
@@ -2445,8 +2444,10 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
         // (2.5 before 2: C5's kept 2.65 G k-mers at load 0.39 instead of 0.48 run 4-7 % faster,
         // profiles/r05/ab_c5_table.txt -- and build ~1.5 s slower: the larger table leaves the
         // neighbour words no free range in the slab pool, whose trim then stalls a hipMalloc)
+        // (PA_BUILD_COMPACT does not apply here: C5's job index at 2 per k-mer
+        // built no faster, 4.58 vs 4.47 s, and the serving index built after
+        // it in the same process, placed in its freed slabs, aligned 10 % slower)
         double mults[4] = {4.0, 2.5, 2.0, 1.43};
-        if (idx->compact_table) mults[0] = mults[1] = 2.0;
         if (const char *e = std::getenv("PA_CAP_DISTINCT")) {  // A/B: this many slots per distinct k-mer first
             const double m = std::atof(e);
             if (m >= 1.2 && m <= 8.0) mults[0] = m, mults[1] = 2.0, mults[2] = 1.43;
