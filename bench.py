@@ -628,8 +628,9 @@ def main():
                    expected_reads < N.PA_COMPACT_READS_PER_BASE * bases)
         ix = N.Index(all_genomes, cfg["k"], device=local, stream=stream, defer_tiles=True, compact=compact)
         torch.cuda.synchronize(dev)
+        ii = ix.info()  # (the library takes the flag for one-word keys on window-sized tables only)
         tm = {"first_build_s": time.perf_counter() - t0, "bases_built": bases, "extsim": None,
-              "compact_table": compact}
+              "compact_table": bool(compact and int(ii.table_slots) == (2 * int(ii.total_windows) + 64 + 3) // 4 * 4)}
         kept = all_genomes
         if kept_from_file is not None:
             kept = [all_genomes[i] for i in kept_from_file]

@@ -2391,9 +2391,12 @@ pa_status index_build(pa_index *idx, const char *genomes, const uint64_t *goff, 
     const uint64_t reserve = windows * 4 + (1ull << 30);
     auto fits = [&](uint64_t c) { return c * per_slot + reserve <= (uint64_t)free_b; };
     uint64_t cap = 0;
-    // (PA_BUILD_COMPACT: 2 per window -- the scans of the table and its first
-    // touches shrink with it; aligns ~2-4 % slower, C4 job +13 %, C2 +15 %)
-    if (!idx->compact_table && (4 * windows + 64) * (uint64_t)sb <= free_b / 3 && fits(4 * windows + 64))
+    // (PA_BUILD_COMPACT: 2 per window for one-word keys -- the scans of the
+    // table and its first touches shrink with it; aligns ~2-4 % slower, C4 job
+    // +13 %, C2 +15 %; two- and three-word keys, inserted one window at a
+    // time, built slower at that load: k = 63 0.171 -> 0.196 s)
+    const bool compact = idx->compact_table && idx->nw == 1;
+    if (!compact && (4 * windows + 64) * (uint64_t)sb <= free_b / 3 && fits(4 * windows + 64))
         cap = 4 * windows + 64;
     else if (fits(2 * windows + 64))
         cap = 2 * windows + 64;

@@ -159,8 +159,8 @@ pa_status pa_index_build(int32_t device, const char *genomes, const uint64_t *ge
  * genomes.  pa_index_build = pa_index_build_ex(..., 0, ...). */
 #define PA_BUILD_DEFER_TILES 1u
 /* PA_BUILD_COMPACT: the k-mer table at 2 slots per genome window (default 4;
- * a table sized on the distinct k-mers, too large for 2 per window, is not
- * changed) -- builds faster, aligns
+ * for k <= 31: longer keys, and a table sized on the distinct k-mers, too
+ * large for 2 per window, are not changed) -- builds faster, aligns
  * slightly slower (MI355X, round 6: C4 build 0.453 -> 0.395 s, its align pass
  * +4 %; C2 0.057 -> 0.048 s, +3 %).  For a job of fewer than
  * PA_COMPACT_READS_PER_BASE reads per genome base (the measured break-even,
