@@ -329,6 +329,7 @@ __global__ __launch_bounds__(256) void k_build_insert1(const uint8_t *__restrict
                              : sv[i].x;
             // settle every window's slot (probing on past other keys: rare at the build's load)
             uint64_t pos[kInsBatch], m[kInsBatch];
+            uint32_t claimed = 0;  // fresh keys: their bookkeeping word is stored, not CASed (below)
 #pragma unroll
             for (int i = 0; i < kInsBatch; i++) {
                 pos[i] = hp[i], m[i] = sv[i].y;
@@ -336,6 +337,7 @@ __global__ __launch_bounds__(256) void k_build_insert1(const uint8_t *__restrict
                 if (sv[i].x == EMPTY && got[i] == EMPTY) {  // claimed: a fresh key
                     fresh++;
                     m[i] = ~0ull;
+                    claimed |= 1u << i;
                     continue;
                 }
                 if (got[i] == kk[i]) {
@@ -354,6 +356,7 @@ __global__ __launch_bounds__(256) void k_build_insert1(const uint8_t *__restrict
                             fresh++;
                             mm = ~0ull;
                             found = true;
+                            claimed |= 1u << i;
                         } else if (o == kk[i]) {
                             mm = ld_agent(meta_of(table, p));
                             found = true;
@@ -371,13 +374,21 @@ __global__ __launch_bounds__(256) void k_build_insert1(const uint8_t *__restrict
                     ok &= ~(1u << i);
                 }
             }
-            // count g for every slot: the batch's CASes issued together, then
-            // the (rare) failed ones again one by one
+            // count g for every slot: a key this thread claimed gets its word
+            // {g, one genome} by a plain store -- only windows of the same
+            // genome can race for it, and they write or CAS that same value
+            // (a third of the pass's atomics: one per distinct k-mer) -- the
+            // others' CASes issued together, then the (rare) failed ones again
+            // one by one
             uint64_t old[kInsBatch];
             uint32_t want = 0;
 #pragma unroll
             for (int i = 0; i < kInsBatch; i++) {
                 old[i] = m[i];
+                if (claimed >> i & 1) {
+                    *meta_of(table, pos[i]) = ((uint64_t)0xFFFFFFFEu << 32) | mark;
+                    continue;
+                }
                 if ((ok >> i & 1) && (uint32_t)m[i] > mark) {
                     want |= 1u << i;
                     const uint64_t nv = ((uint64_t)((uint32_t)(m[i] >> 32) - 1u) << 32) | mark;
