@@ -283,7 +283,7 @@ __device__ __forceinline__ uint32_t count_genome(Slot<1> *t, uint64_t pos, uint6
 __global__ __launch_bounds__(256) void k_build_insert1(const uint8_t *__restrict__ codes, uint64_t gstart,
                                                        uint64_t nwin, int k, uint64_t mask0, uint32_t g,
                                                        Slot<1> *table, HomeCfg hc, unsigned long long *n_kmers,
-                                                       uint32_t *err, int wpt) {
+                                                       uint32_t *err, int wpt, uint32_t *__restrict__ lpos) {
     const uint64_t cap = hc.cap;
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
     uint32_t fresh = 0;
@@ -396,9 +396,21 @@ __global__ __launch_bounds__(256) void k_build_insert1(const uint8_t *__restrict
                                        (unsigned long long)nv);
                 }
             }
+            // (lpos: each window's place in its slot's genome list -- the
+            // genomes counted before g -- when this window counted g, else
+            // ~0u: pass 2 then appends without a CAS, k_build_fill1)
+            uint32_t lp[kInsBatch];
 #pragma unroll
-            for (int i = 0; i < kInsBatch; i++)
-                if ((want >> i & 1) && old[i] != m[i]) count_genome(table, pos[i], old[i], mark);
+            for (int i = 0; i < kInsBatch; i++) {
+                lp[i] = (claimed >> i & 1) ? 0u : ~0u;
+                if (want >> i & 1)
+                    lp[i] = old[i] == m[i] ? ~(uint32_t)(m[i] >> 32) : count_genome(table, pos[i], old[i], mark);
+            }
+            if (lpos) {
+#pragma unroll
+                for (int i = 0; i < kInsBatch; i++)
+                    if (wb + i < w1) lpos[gstart + wb + i] = lp[i];
+            }
         }
     }
     fresh = wave_sum_u32(fresh);
@@ -447,7 +459,8 @@ __global__ void k_hll(const uint8_t *__restrict__ codes, uint64_t gstart, uint64
 // down again, so it holds ~deg once the lists are full).
 template <int NW>
 __global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t cap, uint64_t *off,
-                                                    unsigned long long *bump, unsigned long long *n_multi) {
+                                                    unsigned long long *bump, unsigned long long *n_multi,
+                                                    int keep_deg) {
     __shared__ unsigned long long s_red[2][4];
     __shared__ unsigned long long s_base;
     __shared__ uint32_t s_wave[4];
@@ -499,7 +512,7 @@ __global__ __launch_bounds__(256) void k_build_prep(Slot<NW> *table, uint64_t ca
         if (d >= 2) {
             off[s] = run + before + incl - d;
             table[s].cls = 0xFFFFFFFFu;
-            table[s].tpos = 0xFFFFFFFFu;
+            if (!keep_deg) table[s].tpos = 0xFFFFFFFFu;  // (keep_deg: pass 2 appends by the windows' lpos)
         }
         run += total;
         __syncthreads();  // s_wave is rewritten by the next chunk
@@ -550,7 +563,8 @@ __global__ void k_build_fill(const uint8_t *__restrict__ codes, uint64_t gstart,
 __global__ __launch_bounds__(256) void k_build_fill1(const uint8_t *__restrict__ codes, uint64_t gstart,
                                                      uint64_t nwin, int k, uint64_t mask0, uint32_t g,
                                                      Slot<1> *table, HomeCfg hc, uint32_t G,
-                                                     const uint64_t *__restrict__ off, uint32_t *lists, int wpt) {
+                                                     const uint64_t *__restrict__ off, uint32_t *lists, int wpt,
+                                                     const uint32_t *__restrict__ lpos) {
     const uint64_t cap = hc.cap;
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * wpt;
     if (w0 >= nwin) return;
@@ -567,20 +581,42 @@ __global__ __launch_bounds__(256) void k_build_fill1(const uint8_t *__restrict__
     const uint32_t mark = ~(g + 1);
     for (uint64_t wb = w0; wb < w1; wb += kInsBatch) {
         uint64_t kk[kInsBatch], hp[kInsBatch];
-        uint32_t ok = 0;
+        uint32_t ok = 0, lp[kInsBatch];
 #pragma unroll
         for (int i = 0; i < kInsBatch; i++) {
-            kk[i] = 0, hp[i] = 0;
+            kk[i] = 0, hp[i] = 0, lp[i] = ~0u;
             if (wb + i < w1) {
                 const uint32_t c = s[wb + i - w0 + k - 1];
                 run = c > 3 ? 0 : run + 1;
                 key_push(key, c & 3, mask0);
-                if (run >= k) {
+                if (lpos) lp[i] = lpos[gstart + wb + i];
+                // (with lpos: only the window that counted g for its slot appends it)
+                if (run >= k && (!lpos || lp[i] != ~0u)) {
                     kk[i] = key.w[0];
                     hp[i] = home_of(key, key_hash(key), hc);
                     ok |= 1u << i;
                 }
             }
+        }
+        if (lpos) {  // the list places pass 1 took: no CAS, the slot found and its list written
+            if (!ok) continue;
+            ulonglong2 sv[kInsBatch];
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++)
+                if (ok >> i & 1) sv[i] = *(const ulonglong2 *)&table[hp[i]];
+#pragma unroll
+            for (int i = 0; i < kInsBatch; i++) {
+                if (!(ok >> i & 1)) continue;
+                uint64_t p = hp[i], cur = sv[i].x;
+                uint32_t cls = (uint32_t)sv[i].y;
+                while (cur != kk[i] && cur != EMPTY) {
+                    p = (p + 1 == cap) ? 0 : p + 1;
+                    const ulonglong2 v = *(const ulonglong2 *)&table[p];
+                    cur = v.x, cls = (uint32_t)v.y;
+                }
+                if (cur == kk[i] && cls >= G) lists[off[p] + lp[i]] = g;  // (multi slots only)
+            }
+            continue;
         }
         ulonglong2 sv[kInsBatch];
 #pragma unroll
@@ -1556,12 +1592,12 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
     const uint64_t mask0 = (2 * k - 64 * (NW - 1)) >= 64 ? ~0ull : ((1ull << (2 * k - 64 * (NW - 1))) - 1);
     const uint64_t cap = idx->cap;
     Slot<NW> *table = (Slot<NW> *)idx->table;
-    uint32_t *lists = nullptr, *cs_id = nullptr, *err = nullptr;
+    uint32_t *lists = nullptr, *cs_id = nullptr, *err = nullptr, *lpos = nullptr;
     uint64_t *off = nullptr, *cs_key = nullptr, *cs_rep = nullptr, *rep_of = nullptr;
     unsigned long long *cnt = nullptr;  // [0] n_kmers [1] bump [2] n_multi [3] n_cls [4] bump2
     pa_status rc = PA_OK;
     auto cleanup = [&]() {
-        pa::dev_free(off); pa::dev_free(lists);
+        pa::dev_free(off); pa::dev_free(lists); pa::dev_free(lpos);
         pa::dev_free(cs_key); pa::dev_free(cs_rep); pa::dev_free(cs_id); pa::dev_free(rep_of); pa::dev_free(cnt); pa::dev_free(err);
     };
 #define B_HIP(call)                                                                                 \
@@ -1576,6 +1612,20 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
     B_HIP(pa::dev_malloc(&off, cap * 8));
     B_HIP(pa::dev_malloc(&cnt, 8 * 8));
     B_HIP(pa::dev_malloc(&err, 4));
+    // each window's place in its slot's genome list, taken in pass 1 (4 B per
+    // base, while it fits an eighth of the free memory; PA_BUILD_LPOS=0: pass
+    // 2 takes the places by CAS, as for keys of more than one word)
+    {
+        const char *e = std::getenv("PA_BUILD_LPOS");
+        size_t fb = 0, tb = 0;
+        const uint64_t total = idx->h_goff[G];  // (lpos is indexed by the concatenated position, as codes)
+        if (NW == 1 && kBatchedInsert && total > 0 && !(e && e[0] == '0') &&
+            pa::dev_mem_info(&fb, &tb) == hipSuccess && total * 4 <= fb / 8 &&
+            pa::dev_malloc_try((void **)&lpos, total * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            lpos = nullptr;
+        }
+    }
     B_HIP(hipMemsetAsync(cnt, 0, 8 * 8, st));
     B_HIP(hipMemsetAsync(err, 0, 4, st));
     // pass 1
@@ -1586,14 +1636,14 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
         if (NW == 1 && kBatchedInsert)
             hipLaunchKernelGGL(k_build_insert1, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
                                idx->codes, idx->h_goff[g], nwin, k, mask0, g, (Slot<1> *)table, idx->home, cnt + 0,
-                               err, wpt);
+                               err, wpt, lpos);
         else
             hipLaunchKernelGGL(k_build_insert<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
                                idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, cnt + 0, err, wpt);
     }
     B_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_build_prep<NW>, dim3(grid_for(cap, kBlock) > 65536 ? 65536 : grid_for(cap)), dim3(kBlock), 0,
-                       st, table, cap, off, cnt + 1, cnt + 2);
+                       st, table, cap, off, cnt + 1, cnt + 2, lpos != nullptr ? 1 : 0);
     B_HIP(hipGetLastError());
     unsigned long long h_cnt[8];
     uint32_t h_err = 0;
@@ -1617,7 +1667,7 @@ pa_status build_nw(pa_index *idx, hipStream_t st) {
             if (NW == 1 && kBatchedInsert)
                 hipLaunchKernelGGL(k_build_fill1, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
                                    idx->codes, idx->h_goff[g], nwin, k, mask0, g, (Slot<1> *)table, idx->home, G, off,
-                                   lists, wpt);
+                                   lists, wpt, lpos);
             else
                 hipLaunchKernelGGL(k_build_fill<NW>, dim3(grid_for((nwin + wpt - 1) / wpt)), dim3(kBlock), 0, st,
                                    idx->codes, idx->h_goff[g], nwin, k, mask0, g, table, idx->home, G, off, lists,

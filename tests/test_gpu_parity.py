@@ -1015,3 +1015,30 @@ def test_compact_table_vs_oracle(reduce):
         assert fk.tolist() == ofk.tolist(), ps
     full.close()
     index.close()
+
+
+@pytest.mark.parametrize("lpos", ["1", "0"])
+def test_build_list_places_vs_oracle(lpos, monkeypatch):
+    """The genome lists of multi-genome k-mers appended by the places pass 1
+    took (PA_BUILD_LPOS=1, no CAS in pass 2) or by pass 2's CASes (0): the
+    same genome sets, so the same counts as the oracle, on families whose
+    members share most k-mers and repeat some within a genome."""
+    monkeypatch.setenv("PA_BUILD_LPOS", lpos)
+    gens = synth.family_genomes(24, 30000, seed=93, family_size=6, sub_rate=0.005, conserved_len=2000,
+                                n_rate=2e-4, n_run=8)
+    for g in gens[:6]:  # repeats inside a genome: a stretch copied further on
+        g[20000:20400] = g[1000:1400]
+    index = N.Index(gens, 31)
+    oix = O.OracleIndex(gens, 31)
+    reads = N.Reads.synthesize(index, 30000, 150, first_read=0, seed=94, sub_rate=0.01)
+    s, q, off = reads.download()
+    for ps in (dict(), dict(mg=3), dict(m=0, p=0)):
+        prm = {"m": 1, "p": 1, "mrq": None, "mkq": None, "mg": None, **ps}
+        res = N.Result(index)
+        N.align(index, reads, N.Params.make(prm["m"], prm["p"], prm["mrq"], prm["mkq"], prm["mg"]), 0, res)
+        stats, uq, am, fk = res.fetch()
+        o = oix.align(s.tobytes(), q.tobytes(), off, m=prm["m"], p=prm["p"], mrq=prm["mrq"], mkq=prm["mkq"],
+                      mg=prm["mg"], read_base=0, detail=False)
+        assert stats.tolist() == o.stats.tolist(), ps
+        assert uq.tolist() == o.unique.tolist() and am.tolist() == o.ambiguous.tolist(), ps
+    index.close()
